@@ -1,0 +1,109 @@
+/*
+ * salz_gpu.h - MI355X extensions of the SA-LZ C ABI (libsalz.so).
+ *
+ * Additive to the reference API (salz.h): explicit device contexts, device-resident
+ * encode for callers that already hold blocks in HBM, batched multi-block / multi-GPU
+ * encode for the CLI's block loop (programs/salzcli.c:143-179), a frame-aware decoder for
+ * streams longer than the 24-bit header can describe, per-stage
+ * statistics, and a stage-dump hook used by the parity tests.
+ *
+ * Plain C types only; `stream` arguments are hipStream_t passed as void*.
+ */
+#ifndef SALZ_GPU_H
+#define SALZ_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct salz_gpu_ctx salz_gpu_ctx;
+
+/* Number of visible HIP devices; 0 when no GPU is usable. */
+int salz_gpu_device_count(void);
+
+/* Message of the last failure on this thread ("" if none). */
+const char *salz_gpu_last_error(void);
+
+/* Device memory helpers (so callers need no second HIP runtime in their process). */
+void *salz_gpu_malloc(int device, size_t bytes);
+void salz_gpu_free(int device, void *ptr);
+int salz_gpu_memcpy_h2d(int device, void *dst, const void *src, size_t bytes);
+int salz_gpu_memcpy_d2h(int device, void *dst, const void *src, size_t bytes);
+int salz_gpu_synchronize(int device);
+
+/* Context on `device` with device workspace for blocks of up to max_block bytes
+ * (about 90 bytes of HBM per block byte). NULL on failure. */
+salz_gpu_ctx *salz_gpu_ctx_create(int device, size_t max_block);
+void salz_gpu_ctx_destroy(salz_gpu_ctx *ctx);
+
+/*
+ * Encode one block already resident in device memory. d_src holds src_len bytes, d_dst has
+ * dst_cap bytes; *dst_len receives the stream length (bit-identical to salz_encode_safe).
+ * `stream` (hipStream_t or NULL for the context's own) orders the call; the function
+ * returns after the stream has drained. Returns 0 / -1 like salz_encode_safe.
+ */
+int salz_gpu_encode_device(salz_gpu_ctx *ctx, const uint8_t *d_src, size_t src_len,
+                           uint8_t *d_dst, size_t dst_cap, size_t *dst_len, void *stream);
+
+/* salz_encode_safe on an explicit context (host buffers). */
+int salz_gpu_encode_host(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, uint8_t *dst,
+                         size_t *dst_len);
+
+/* Intermediate arrays of one encode (n = src_len - 8 entries; cost has n + 1).
+ * Any member may be NULL. Layout and meaning: oracle/salz_oracle.h (oracle_stages). */
+typedef struct {
+    int32_t *sa, *psv, *nsv, *lp, *ln, *dlen, *doff, *cost;
+} salz_gpu_dump;
+
+int salz_gpu_encode_dump(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, uint8_t *dst,
+                         size_t *dst_len, const salz_gpu_dump *dump);
+
+typedef struct {
+    double ms_upload, ms_sa, ms_lcp, ms_ansv, ms_parse, ms_emit, ms_total;
+    int32_t sa_rounds, parse_iters;
+    uint64_t sa_sorted_elems, lcp_long_bytes, emit_bits, emit_bytes;
+    uint32_t exit_nodes;
+    uint32_t radix_scatter_launches;
+    double ms_radix_scatter;
+    uint64_t radix_scatter_elems;
+} salz_gpu_stats;
+
+/* Per-stage HIP-event timing of subsequent calls (small overhead when on). */
+void salz_gpu_set_timing(salz_gpu_ctx *ctx, int on);
+int salz_gpu_get_stats(const salz_gpu_ctx *ctx, salz_gpu_stats *out);
+
+/*
+ * Encode src as consecutive blocks of block_size bytes (the last may be shorter), spreading
+ * blocks over `n_devices` GPUs (<= 0: all visible) with one host thread per device pulling
+ * block indices from a shared counter. Output is the reference CLI container
+ * (programs/salzcli.c:102-185): "ZLAS" magic, u32 block size, then per block u32 length +
+ * stream, in block order. *dst_len: [in] capacity, [out] bytes written.
+ * Returns 0 / -1.
+ */
+int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, uint8_t *dst,
+                       size_t *dst_len, int n_devices);
+
+/* Upper bound of salz_encode_blocks output for (src_len, block_size). */
+size_t salz_blocks_len_max(size_t src_len, size_t block_size);
+
+/*
+ * Decode one stream whose true length is frame_len (the container's u32 length field).
+ * Identical to salz_decode_safe except that when the 24-bit header length equals
+ * (frame_len - 4) mod 2^24 the frame length is used, so streams longer than 16 MiB - 1
+ * (whose header field the reference truncates, lib/salz.c:770) decode. Returns 0 / -1.
+ */
+int salz_decode_frame(const uint8_t *src, size_t frame_len, uint8_t *dst, size_t *dst_len);
+
+/* Decode a salz_encode_blocks / salzcli container with `threads` host threads
+ * (<= 0: one per core). *dst_len: [in] capacity, [out] bytes. Returns 0 / -1. */
+int salz_decode_blocks(const uint8_t *src, size_t src_len, uint8_t *dst, size_t *dst_len,
+                       int threads);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SALZ_GPU_H */

@@ -1,0 +1,108 @@
+// common.hpp - shared CDNA4 (gfx950) device helpers for the SA-LZ pipeline.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+
+namespace salz {
+
+constexpr int kWave = 64;  // CDNA wavefront width
+
+// ---- error plumbing (host) -------------------------------------------------------------
+void set_error(const char *fmt, ...);
+
+#define SALZ_HIP(call)                                                                    \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            ::salz::set_error("%s:%d: %s -> %s", __FILE__, __LINE__, #call,               \
+                              hipGetErrorString(e_));                                     \
+            return -1;                                                                    \
+        }                                                                                 \
+    } while (0)
+
+#define SALZ_LAUNCH_CHECK() SALZ_HIP(hipGetLastError())
+
+static inline unsigned grid_for(size_t n, unsigned per_block)
+{
+    size_t g = (n + per_block - 1) / per_block;
+    return g == 0 ? 1u : (unsigned)g;
+}
+
+static inline int bit_width(uint64_t v)  // bits needed to represent v (0 -> 0)
+{
+    int b = 0;
+    while (v) {
+        b++;
+        v >>= 1;
+    }
+    return b;
+}
+
+// ---- wave primitives (device) --------------------------------------------------------------
+__device__ __forceinline__ unsigned lane_id()
+{
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// number of set bits of `mask` in lanes strictly below this lane
+__device__ __forceinline__ unsigned count_below(uint64_t mask)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, int src)
+{
+    return (uint32_t)__shfl((int)v, src, kWave);
+}
+
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src)
+{
+    uint32_t lo = shfl_u32((uint32_t)v, src), hi = shfl_u32((uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t shfl_up_u32(uint32_t v, unsigned d)
+{
+    return (uint32_t)__shfl_up((int)v, d, kWave);
+}
+
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, unsigned d)
+{
+    uint32_t lo = shfl_up_u32((uint32_t)v, d), hi = shfl_up_u32((uint32_t)(v >> 32), d);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t shfl_xor_u32(uint32_t v, int m)
+{
+    return (uint32_t)__shfl_xor((int)v, m, kWave);
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint32_t o = shfl_xor_u32(v, m);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// Unaligned little-endian 8-byte load from an 8-byte-aligned, padded byte buffer.
+__device__ __forceinline__ uint64_t load_u64_any(const uint8_t *base, size_t pos)
+{
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(base + (pos & ~(size_t)7));
+    unsigned sh = (unsigned)(pos & 7) * 8u;
+    uint64_t a = w[0];
+    if (sh == 0)
+        return a;
+    uint64_t b = w[1];
+    return (a >> sh) | (b << (64u - sh));
+}
+
+}  // namespace salz

@@ -1,0 +1,106 @@
+// internal.hpp - device workspace and stage entry points of the MI355X SA-LZ pipeline.
+//
+// One Workspace per (device, max block size). Every array is sized for the largest block
+// the context accepts and reused across calls; stages that run later alias the scratch
+// of stages that ran earlier (see DESIGN.md "Data layout in HBM").
+#pragma once
+
+#include "common.hpp"
+
+#include <vector>
+
+namespace salz {
+
+// Per-call statistics, filled when Workspace::timing is set (bench.py / tests).
+struct StageStats {
+    float ms_upload, ms_sa, ms_lcp, ms_ansv, ms_parse, ms_emit, ms_total;
+    int sa_rounds;
+    int parse_iters;
+    uint64_t sa_sorted_elems;  // sum over rounds of active suffixes sorted
+    uint32_t exit_nodes;
+    uint64_t lcp_long_bytes;
+    float ms_radix_scatter;   // summed over every radix scatter launch (HIP events)
+    uint32_t radix_scatter_launches;
+    uint64_t radix_scatter_elems;
+    uint64_t emit_bits, emit_bytes;
+};
+
+// Parse/emit scratch carving (parse.hip owns the layout, emit.hip reads it).
+struct ParseState {
+    uint32_t chunk;         // positions per parse lane
+    uint32_t nchunks;
+    uint8_t *choice;        // final decisions: 0 literal, 1 PSV, 2 NSV
+    uint32_t *cost;         // exact suffix costs, cost[n] = 0
+    uint32_t *ex, *sm;      // chunk exit and in-chunk bit sum per position
+    uint32_t n_exit;        // |E|
+    uint32_t *elist;        // E nodes (positions), ascending; last is n
+    uint32_t *jt0;          // parent (compact) per E node, snapshot level 0
+    uint32_t levels;        // pointer-jumping snapshots stored at jt0 + k*n_exit
+};
+
+struct Workspace {
+    int device = -1;
+    size_t cap_N = 0;  // largest block (bytes) this workspace accepts
+    size_t cap_n = 0;  // cap_N - 8
+    size_t np2 = 0;    // power of two >= cap_n (ANSV tree leaves)
+
+    uint8_t *text = nullptr;  // padded copy of the block
+    uint32_t *rank = nullptr, *sa = nullptr;
+    uint64_t *keyA = nullptr, *keyB = nullptr;  // n+1 each
+    uint32_t *valA = nullptr, *valB = nullptr;
+    uint32_t *u0 = nullptr, *u1 = nullptr, *u2 = nullptr, *u3 = nullptr;  // n+2 each
+    uint64_t *g64 = nullptr;                                             // n+2
+    uint32_t *offA = nullptr, *offB = nullptr;                           // n+2 each
+    uint4 *cand = nullptr;                                               // n
+    uint8_t *out = nullptr;                                              // encoded_len_max
+    size_t out_cap = 0;
+    uint32_t *radix_counts = nullptr;
+    size_t radix_counts_elems = 0;
+    void *scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
+    uint64_t *dscal = nullptr;  // device scalars
+    uint64_t *hscal = nullptr;  // pinned host mirror
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    bool timing = false;
+    StageStats stats{};
+    ParseState parse{};
+    hipEvent_t ev[16] = {};
+    // begin/end event pairs around every radix scatter launch, resolved after the call
+    uint32_t *dbg_round = nullptr;  // SALZ_DEBUG_SAROUND: round that committed sa[r]
+    uint32_t *dbg_sa = nullptr;     // snapshot of sa after the suffix sort
+    std::vector<hipEvent_t> rx_pool;
+    size_t rx_used = 0;
+};
+
+int workspace_alloc(Workspace &ws, int device, size_t max_block);
+
+// Copy device scalars dscal[off, off + bytes) to hscal (same offset) and wait for them.
+int read_scalars(Workspace &ws, size_t off, size_t bytes, const char *tag);
+void workspace_free(Workspace &ws);
+
+// scans (scan.hip)
+size_t scan_temp_elems(size_t n);
+int scan_sum_u32(const uint32_t *in, uint32_t *out, size_t n, bool inclusive,
+                 uint32_t *total_out, Workspace &ws, hipStream_t st);
+int scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, bool inclusive,
+                 uint32_t *total_out, Workspace &ws, hipStream_t st);
+int scan_sum_u64(const uint64_t *in, uint64_t *out, size_t n, bool inclusive,
+                 uint64_t *total_out, Workspace &ws, hipStream_t st);
+
+// radix sort of (u64 key, u32 value) pairs on key bits [bit_lo, bit_hi) (radix.hip).
+// On return *keys / *vals point at whichever buffer holds the sorted result.
+constexpr int kRadixTile = 4096;
+int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
+                     uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st);
+
+// stages
+int stage_suffix_array(Workspace &ws, uint32_t n);                 // sa.hip   -> ws.sa
+int stage_lcp(Workspace &ws, uint32_t n, uint32_t *lcp_out);       // lcp.hip  -> lcp[r]
+int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp);  // ansv.hip -> ws.cand
+int stage_parse(Workspace &ws, uint32_t n);                        // parse.hip
+int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap,
+               size_t *out_len);                                   // emit.hip -> dst
+
+
+}  // namespace salz

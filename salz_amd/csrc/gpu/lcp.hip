@@ -1,0 +1,192 @@
+// lcp.hip - LCP array of the suffix array via Phi / irreducible PLCP.
+//
+// The reference has no LCP pass: it extends each candidate match with 8-byte compares
+// seeded by the previous position's length (lib/salz.c:492-538). Its lengths equal the
+// exact LCP of the suffix pair in T[0,n), so the GPU path computes the
+// exact LCP array once and derives every candidate length from range minima (ansv.hip).
+//
+//   Phi[SA[r]] = SA[r-1]; PLCP[i] = lcp(i, Phi[i]).
+//   i is reducible iff i > 0, Phi[i] > 0 and T[i-1] == T[Phi[i]-1]; then
+//   PLCP[i] = PLCP[i-1] - 1. PLCP[i] + i is non-decreasing, so an inclusive max-scan over
+//   (irreducible ? PLCP[i] + i : 0) recovers every PLCP value exactly.
+// Irreducible values are summed O(n log n) (Kärkkäinen-Manzini-Puglisi); each thread
+// compares the first 32 bytes, longer ones go to a work list resolved in doubling windows
+// split into 512-byte wave tasks (64 lanes x 8 bytes), so a single 10^8-byte match is
+// spread over the whole chip instead of serialising one lane.
+#include "internal.hpp"
+
+namespace salz {
+namespace {
+
+constexpr int kT = 256;
+constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint32_t kShortBytes = 32;
+constexpr uint32_t kTaskBytes = 512;
+
+__global__ void k_phi(const uint32_t *__restrict__ sa, uint32_t n, uint32_t *__restrict__ phi)
+{
+    size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (r >= n)
+        return;
+    phi[sa[r]] = r ? sa[r - 1] : kNone;
+}
+
+__global__ void k_plcp_short(const uint8_t *__restrict__ T, const uint32_t *__restrict__ phi,
+                             uint32_t n, uint32_t *__restrict__ plv, uint32_t *__restrict__ queue,
+                             uint32_t *__restrict__ qcount)
+{
+    size_t ii = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (ii >= n)
+        return;
+    uint32_t i = (uint32_t)ii, j = phi[i];
+    if (j == kNone) {  // smallest suffix: PLCP = 0
+        plv[i] = i;
+        return;
+    }
+    bool irr = i == 0 || j == 0 || T[i - 1] != T[j - 1];
+    if (!irr) {
+        plv[i] = 0;
+        return;
+    }
+    uint32_t limit = n - (i > j ? i : j);
+    uint32_t L = 0;
+    bool done = false;
+#pragma unroll
+    for (int w = 0; w < (int)(kShortBytes / 8); w++) {
+        if (!done && L < limit) {
+            uint64_t x = load_u64_any(T, (size_t)i + L) ^ load_u64_any(T, (size_t)j + L);
+            if (x) {
+                L += (uint32_t)__builtin_ctzll(x) >> 3;
+                done = true;
+            } else {
+                L += 8;
+            }
+        }
+    }
+    if (L >= limit) {
+        L = limit;
+        done = true;
+    }
+    if (done) {
+        plv[i] = L + i;
+    } else {
+        plv[i] = 0;
+        uint32_t q = atomicAdd(qcount, 1u);
+        queue[q] = i;
+    }
+}
+
+// One wave per 512-byte task: task t -> item t / nch, bytes [L + (t % nch) * 512, +512).
+__global__ __launch_bounds__(256) void k_plcp_long(const uint8_t *__restrict__ T,
+                                                   const uint32_t *__restrict__ phi, uint32_t n,
+                                                   const uint32_t *__restrict__ items,
+                                                   uint32_t nitems, uint32_t nch, uint32_t L,
+                                                   uint32_t *__restrict__ found)
+{
+    size_t task = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    unsigned lane = threadIdx.x & 63;
+    if (task >= (size_t)nitems * nch)
+        return;
+    uint32_t item = (uint32_t)(task / nch), ch = (uint32_t)(task % nch);
+    uint32_t i = items[item], j = phi[i];
+    uint32_t limit = n - (i > j ? i : j);
+    uint64_t start = (uint64_t)L + (uint64_t)ch * kTaskBytes + (uint64_t)lane * 8;
+    uint32_t mis = kNone;
+    if (start < limit) {
+        uint64_t x = load_u64_any(T, i + start) ^ load_u64_any(T, j + start);
+        if (x) {
+            uint64_t pos = start + ((uint32_t)__builtin_ctzll(x) >> 3);
+            if (pos < limit)
+                mis = (uint32_t)pos;
+        }
+    }
+    mis = wave_min_u32(mis);
+    if (lane == 0 && mis != kNone)
+        atomicMin(&found[item], mis);
+}
+
+__global__ void k_plcp_resolve(const uint32_t *__restrict__ phi, uint32_t n,
+                               const uint32_t *__restrict__ items, uint32_t nitems,
+                               const uint32_t *__restrict__ found, uint64_t window_end,
+                               uint32_t *__restrict__ plv, uint32_t *__restrict__ next_items,
+                               uint32_t *__restrict__ next_count)
+{
+    size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (x >= nitems)
+        return;
+    uint32_t i = items[x], j = phi[i];
+    uint32_t limit = n - (i > j ? i : j);
+    uint32_t f = found[x];
+    if (f != kNone) {
+        plv[i] = f + i;
+    } else if (window_end >= limit) {
+        plv[i] = limit + i;
+    } else {
+        uint32_t q = atomicAdd(next_count, 1u);
+        next_items[q] = i;
+    }
+}
+
+__global__ void k_lcp_final(const uint32_t *__restrict__ sa, const uint32_t *__restrict__ mx,
+                            uint32_t n, uint32_t *__restrict__ lcp)
+{
+    size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (r >= n)
+        return;
+    uint32_t i = sa[r];
+    lcp[r] = r ? mx[i] - i : 0u;
+}
+
+}  // namespace
+
+int stage_lcp(Workspace &ws, uint32_t n, uint32_t *lcp_out)
+{
+    hipStream_t st = ws.stream;
+    uint32_t *phi = ws.u0, *plv = ws.u1;
+    uint32_t *qa = ws.valA, *qb = ws.valB, *found = ws.offA;
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(ws.dscal) + 32;  // 2 counters
+
+    ws.stats.lcp_long_bytes = 0;
+    hipLaunchKernelGGL(k_phi, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.sa, n, phi);
+    SALZ_LAUNCH_CHECK();
+    SALZ_HIP(hipMemsetAsync(cnt, 0, 8, st));
+    hipLaunchKernelGGL(k_plcp_short, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, phi, n, plv,
+                       qa, cnt);
+    SALZ_LAUNCH_CHECK();
+    if (read_scalars(ws, 0, 256, "lcp.q0") != 0)
+        return -1;
+    uint32_t nitems = reinterpret_cast<uint32_t *>(ws.hscal)[32];
+
+    uint64_t L = kShortBytes;
+    while (nitems) {
+        uint64_t W = L < kTaskBytes ? kTaskBytes : L;
+        W = (W + kTaskBytes - 1) / kTaskBytes * kTaskBytes;
+        uint32_t nch = (uint32_t)(W / kTaskBytes);
+        SALZ_HIP(hipMemsetAsync(found, 0xff, sizeof(uint32_t) * nitems, st));
+        SALZ_HIP(hipMemsetAsync(cnt + 1, 0, 4, st));
+        size_t tasks = (size_t)nitems * nch;
+        hipLaunchKernelGGL(k_plcp_long, dim3(grid_for(tasks * 64, 256)), dim3(256), 0, st,
+                           ws.text, phi, n, qa, nitems, nch, (uint32_t)L, found);
+        SALZ_LAUNCH_CHECK();
+        ws.stats.lcp_long_bytes += tasks * kTaskBytes;
+        hipLaunchKernelGGL(k_plcp_resolve, dim3(grid_for(nitems, kT)), dim3(kT), 0, st, phi, n,
+                           qa, nitems, found, L + W, plv, qb, cnt + 1);
+        SALZ_LAUNCH_CHECK();
+        if (read_scalars(ws, 0, 256, "lcp.q") != 0)
+            return -1;
+        nitems = reinterpret_cast<uint32_t *>(ws.hscal)[33];
+        uint32_t *t = qa;
+        qa = qb;
+        qb = t;
+        L += W;
+    }
+
+    if (scan_max_u32(plv, plv, n, true, nullptr, ws, st) != 0)
+        return -1;
+    hipLaunchKernelGGL(k_lcp_final, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.sa, plv, n,
+                       lcp_out);
+    SALZ_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // namespace salz

@@ -1,0 +1,721 @@
+// pipeline.hip - device contexts, stage orchestration and the extern "C" ABI of libsalz.so.
+//
+// salz_encode_safe (/root/reference/lib/salz.c:777-823) becomes:
+//   H2D (or D2D) of the block into a padded HBM copy
+//   -> stage_suffix_array (sa.hip)     replaces libsais, :463-469
+//   -> stage_lcp          (lcp.hip)    exact LCP array (feeds the candidate lengths)
+//   -> stage_candidates   (ansv.hip)   :471-560
+//   -> stage_parse        (parse.hip)  :610-662
+//   -> stage_emit         (emit.hip)   :664-775
+//   -> D2H of the encoded stream.
+// One Workspace per context, reused across calls; a mutex per context keeps the reference
+// API's reentrancy (concurrent callers serialise per device).
+#include "internal.hpp"
+#include "../../../include/salz.h"
+#include "../../../include/salz_gpu.h"
+
+#include <atomic>
+#include <cstdarg>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace salz {
+
+static thread_local char g_err[512];
+
+void set_error(const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+template <typename T> static int dalloc(T **p, size_t count)
+{
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, count * sizeof(T) + 256);
+    if (e != hipSuccess) {
+        set_error("hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
+        return -1;
+    }
+    *p = static_cast<T *>(q);
+    return 0;
+}
+
+void workspace_free(Workspace &ws)
+{
+    if (ws.device >= 0)
+        (void)hipSetDevice(ws.device);
+    void *ptrs[] = {ws.dbg_round, ws.dbg_sa, ws.text, ws.rank,     ws.sa,   ws.keyA, ws.keyB, ws.valA, ws.valB,
+                    ws.u0,   ws.u1,       ws.u2,   ws.u3,   ws.g64,  ws.offA, ws.offB,
+                    ws.cand, ws.out,      ws.radix_counts,  ws.scan_tmp,      ws.dscal};
+    for (void *p : ptrs)
+        if (p)
+            (void)hipFree(p);
+    if (ws.hscal)
+        (void)hipHostFree(ws.hscal);
+    for (hipEvent_t &e : ws.ev)
+        if (e)
+            (void)hipEventDestroy(e);
+    for (hipEvent_t e : ws.rx_pool)
+        (void)hipEventDestroy(e);
+    if (ws.own_stream && ws.stream)
+        (void)hipStreamDestroy(ws.stream);
+    ws = Workspace{};
+}
+
+static size_t out_bound(size_t N) { return (size_t)salz_encoded_len_max(N) + N / 4 + 4096; }
+
+int workspace_alloc(Workspace &ws, int device, size_t max_block)
+{
+    workspace_free(ws);
+    SALZ_HIP(hipSetDevice(device));
+    ws.device = device;
+    size_t N = max_block < 8192 ? 8192 : max_block;
+    ws.cap_N = N;
+    ws.cap_n = N - 8;
+    ws.np2 = 2048;
+    while (ws.np2 < ws.cap_n)
+        ws.np2 <<= 1;
+    const size_t n1 = ws.cap_n + 2;
+    const size_t ntiles = (ws.cap_n + kRadixTile - 1) / kRadixTile;
+    ws.radix_counts_elems = 256 * ntiles + 256;
+    ws.out_cap = out_bound(N);
+    size_t scan_elems = scan_temp_elems(ws.radix_counts_elems > n1 ? ws.radix_counts_elems : n1);
+    ws.scan_tmp_bytes = scan_elems * sizeof(uint64_t);
+    if (dalloc(&ws.text, N + 256) || dalloc(&ws.rank, n1) || dalloc(&ws.sa, n1) ||
+        dalloc(&ws.keyA, n1) || dalloc(&ws.keyB, n1) || dalloc(&ws.valA, n1) ||
+        dalloc(&ws.valB, n1) || dalloc(&ws.u0, n1) || dalloc(&ws.u1, n1) || dalloc(&ws.u2, n1) ||
+        dalloc(&ws.u3, n1) || dalloc(&ws.g64, n1) || dalloc(&ws.offA, n1) ||
+        dalloc(&ws.offB, n1) || dalloc(&ws.cand, ws.cap_n + 1) || dalloc(&ws.out, ws.out_cap) ||
+        dalloc(&ws.radix_counts, ws.radix_counts_elems) ||
+        dalloc(reinterpret_cast<uint8_t **>(&ws.scan_tmp), ws.scan_tmp_bytes) ||
+        dalloc(&ws.dscal, 512)) {
+        std::string keep = g_err;
+        workspace_free(ws);
+        set_error("%s", keep.c_str());
+        return -1;
+    }
+    void *h = nullptr;
+    SALZ_HIP(hipHostMalloc(&h, 4096, hipHostMallocDefault));
+    ws.hscal = static_cast<uint64_t *>(h);
+    SALZ_HIP(hipStreamCreateWithFlags(&ws.stream, hipStreamNonBlocking));
+    ws.own_stream = true;
+    for (hipEvent_t &e : ws.ev)
+        SALZ_HIP(hipEventCreate(&e));
+    if (getenv("SALZ_DEBUG_SAROUND")) {
+        if (dalloc(&ws.dbg_round, n1) || dalloc(&ws.dbg_sa, n1))
+            return -1;
+    }
+    ws.rx_pool.resize(2048);
+    for (hipEvent_t &e : ws.rx_pool)
+        SALZ_HIP(hipEventCreate(&e));
+    return 0;
+}
+
+int read_scalars(Workspace &ws, size_t off, size_t bytes, const char *tag)
+{
+    uint8_t *h = reinterpret_cast<uint8_t *>(ws.hscal) + off;
+    const uint8_t *d = reinterpret_cast<const uint8_t *>(ws.dscal) + off;
+    SALZ_HIP(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ws.stream));
+    SALZ_HIP(hipStreamSynchronize(ws.stream));
+    static const bool verify = getenv("SALZ_DEBUG_SCALARS") != nullptr;
+    if (verify) {
+        uint8_t chk[512];
+        SALZ_HIP(hipDeviceSynchronize());
+        SALZ_HIP(hipMemcpy(chk, d, bytes, hipMemcpyDeviceToHost));
+        if (memcmp(chk, h, bytes) != 0) {
+            for (size_t i = 0; i + 4 <= bytes; i += 4) {
+                uint32_t a, b;
+                memcpy(&a, h + i, 4);
+                memcpy(&b, chk + i, 4);
+                if (a != b)
+                    fprintf(stderr, "STALE %s: word %zu async %u sync %u\n", tag, (off + i) / 4, a, b);
+            }
+        }
+    }
+    return 0;
+}
+
+enum : int { EV_START, EV_UP, EV_SA, EV_LCP, EV_ANSV, EV_PARSE, EV_EMIT };
+
+static int mark(Workspace &ws, int which)
+{
+    if (ws.timing)
+        SALZ_HIP(hipEventRecord(ws.ev[which], ws.stream));
+    return 0;
+}
+
+static float elapsed(Workspace &ws, int a, int b)
+{
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, ws.ev[a], ws.ev[b]);
+    return ms;
+}
+
+struct HostDump {
+    const salz_gpu_dump *d;
+};
+
+static int dump_after_sa(Workspace &ws, uint32_t n, const salz_gpu_dump *d)
+{
+    if (d && d->sa) {
+        SALZ_HIP(hipMemcpyAsync(d->sa, ws.sa, sizeof(uint32_t) * n, hipMemcpyDeviceToHost,
+                                ws.stream));
+        SALZ_HIP(hipStreamSynchronize(ws.stream));
+    }
+    return 0;
+}
+
+static int dump_after_parse(Workspace &ws, uint32_t n, const salz_gpu_dump *d)
+{
+    if (!d || !(d->psv || d->nsv || d->lp || d->ln || d->dlen || d->doff || d->cost))
+        return 0;
+    std::vector<uint4> cand(n);
+    std::vector<uint8_t> choice(n);
+    std::vector<uint32_t> cost((size_t)n + 1);
+    SALZ_HIP(hipMemcpyAsync(cand.data(), ws.cand, sizeof(uint4) * n, hipMemcpyDeviceToHost,
+                            ws.stream));
+    SALZ_HIP(hipMemcpyAsync(choice.data(), ws.parse.choice, n, hipMemcpyDeviceToHost, ws.stream));
+    SALZ_HIP(hipMemcpyAsync(cost.data(), ws.parse.cost, sizeof(uint32_t) * ((size_t)n + 1),
+                            hipMemcpyDeviceToHost, ws.stream));
+    SALZ_HIP(hipStreamSynchronize(ws.stream));
+    for (uint32_t p = 0; p < n; p++) {
+        const uint4 c = cand[p];
+        if (d->psv) d->psv[p] = (int32_t)(p - c.x);
+        if (d->lp) d->lp[p] = (int32_t)c.y;
+        if (d->nsv) d->nsv[p] = (int32_t)(p - c.z);
+        if (d->ln) d->ln[p] = (int32_t)c.w;
+        int32_t len = 1, off = 0;
+        if (choice[p] == 1) {
+            len = (int32_t)c.y;
+            off = (int32_t)c.x;
+        } else if (choice[p] == 2) {
+            len = (int32_t)c.w;
+            off = (int32_t)c.z;
+        }
+        if (d->dlen) d->dlen[p] = len;
+        if (d->doff) d->doff[p] = off;
+    }
+    if (d->cost)
+        for (size_t q = 0; q <= n; q++)
+            d->cost[q] = (int32_t)cost[q];
+    return 0;
+}
+
+// SALZ_DEBUG_HASH=1: checksum each stage's output on the host (diagnostics only).
+static void debug_hash(Workspace &ws, const char *what, const void *dptr, size_t bytes)
+{
+    static const bool on = getenv("SALZ_DEBUG_HASH") != nullptr;
+    if (!on)
+        return;
+    std::vector<uint8_t> h(bytes);
+    (void)hipStreamSynchronize(ws.stream);
+    (void)hipMemcpy(h.data(), dptr, bytes, hipMemcpyDeviceToHost);
+    uint64_t x = 1469598103934665603ull;
+    for (size_t i = 0; i < bytes; i++)
+        x = (x ^ h[i]) * 1099511628211ull;
+    fprintf(stderr, "hash %-8s %016llx\n", what, (unsigned long long)x);
+}
+
+// Device-side diagnostics (no host sync): text checksum and 8-byte order of the SA.
+__global__ void k_dbg_text_sum(const uint8_t *T, size_t N, unsigned long long *out)
+{
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < N)
+        atomicAdd(out, (unsigned long long)T[i] * (unsigned long long)(i % 65521 + 1));
+}
+
+__global__ void k_dbg_sa_order(const uint8_t *T, const uint32_t *sa, uint32_t n, unsigned int *bad)
+{
+    size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (r == 0 || r >= n)
+        return;
+    uint32_t a = sa[r - 1], b = sa[r];
+    uint64_t ka = load_u64_any(T, a), kb = load_u64_any(T, b);
+    uint32_t la = n - a, lb = n - b;
+    if (la < 8) ka &= (1ull << (8 * la)) - 1;
+    if (lb < 8) kb &= (1ull << (8 * lb)) - 1;
+    ka = __builtin_bswap64(ka);
+    kb = __builtin_bswap64(kb);
+    if (ka > kb || (ka == kb && la < 8 && lb < 8 && la > lb))
+        atomicAdd(bad, 1u);
+}
+
+__global__ void k_copy_bytes(uint8_t *dst, const uint8_t *src, size_t N)
+{
+    size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    if (i + 16 <= N && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
+        *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(src + i);
+    } else {
+        for (size_t j = i; j < i + 16 && j < N; j++)
+            dst[j] = src[j];
+    }
+}
+
+// SALZ_DEBUG_CAND=1: validate candidates after ANSV; on a bad one, cross-check SA / LCP.
+static void debug_cand(Workspace &ws, uint32_t n)
+{
+    static const bool on = getenv("SALZ_DEBUG_CAND") != nullptr;
+    if (!on)
+        return;
+    (void)hipStreamSynchronize(ws.stream);
+    std::vector<uint4> cand(n);
+    (void)hipMemcpy(cand.data(), ws.cand, 16ull * n, hipMemcpyDeviceToHost);
+    long bad = 0;
+    uint32_t first = 0;
+    for (uint32_t p = 1; p < n; p++) {
+        uint4 c = cand[p];
+        bool ok = c.y <= n - p && c.w <= n - p && c.x >= 1 && c.x <= p + 1 && c.z >= 1 &&
+                  c.z <= p + 1;
+        if (!ok && !bad++)
+            first = p;
+    }
+    fprintf(stderr, "cand check: %ld bad\n", bad);
+    if (!bad)
+        return;
+    std::vector<uint32_t> sa(n), lcp(n), isa(n);
+    std::vector<uint8_t> T(n + 8);
+    (void)hipMemcpy(sa.data(), ws.sa, 4ull * n, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(lcp.data(), ws.u3, 4ull * n, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(T.data(), ws.text, n + 8, hipMemcpyDeviceToHost);
+    std::vector<uint8_t> seen(n, 0);
+    long dup = 0;
+    for (uint32_t r = 0; r < n; r++) {
+        if (sa[r] >= n || seen[sa[r]]++) dup++;
+        else isa[sa[r]] = r;
+    }
+    fprintf(stderr, "sa: %ld invalid/duplicate entries\n", dup);
+    // Kasai LCP from the GPU SA, and an order check of adjacent suffixes
+    long bad_lcp = 0, bad_order = 0;
+    uint32_t h = 0;
+    for (uint32_t i = 0; i < n && !dup; i++) {
+        uint32_t r = isa[i];
+        if (r == 0) { h = 0; continue; }
+        uint32_t j = sa[r - 1];
+        while (i + h < n && j + h < n && T[i + h] == T[j + h]) h++;
+        bool ordered = (j + h == n) || (i + h < n && T[j + h] < T[i + h]);
+        if (!ordered && !bad_order++)
+            fprintf(stderr, "order: rank %u (pos %u) before rank %u (pos %u) wrong\n", r - 1, j, r, i);
+        if (lcp[r] != h && !bad_lcp++)
+            fprintf(stderr, "lcp[%u] (pos %u) gpu %u host %u\n", r, i, lcp[r], h);
+        if (h) h--;
+    }
+    uint4 c = cand[first];
+    fprintf(stderr, "first bad cand p=%u rank %u: {%u %u %u %u}; lcp bad %ld order bad %ld\n", first,
+            dup ? 0 : isa[first], c.x, c.y, c.z, c.w, bad_lcp, bad_order);
+}
+
+// Encode one block. src is host or device memory; the stream goes to device buffer dst.
+static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t N, uint8_t *dst,
+                       size_t cap, size_t *out_len, const salz_gpu_dump *dump)
+{
+    if (N <= 8) {
+        set_error("block of %zu bytes: the reference codec needs more than 8 bytes", N);
+        return -1;  // lib/salz.c:197 wraps (N < 8) or crashes (N == 8)
+    }
+    if (N > ws.cap_N || N - 8 >= 0x7fffffffu) {
+        set_error("block of %zu bytes exceeds context capacity %zu", N, ws.cap_N);
+        return -1;
+    }
+    SALZ_HIP(hipSetDevice(ws.device));
+    hipStream_t st = ws.stream;
+    const uint32_t n = (uint32_t)(N - 8);
+    ws.stats = StageStats{};
+    ws.rx_used = 0;
+
+    if (mark(ws, EV_START)) return -1;
+    static const bool copy_kernel = getenv("SALZ_COPY_KERNEL") != nullptr;
+    static const bool dev_check = getenv("SALZ_DEBUG_DEVICE") != nullptr;
+    if (src_dev && copy_kernel) {
+        hipLaunchKernelGGL(k_copy_bytes, dim3(grid_for((N + 15) / 16, 256)), dim3(256), 0, st, ws.text,
+                           src, N);
+        SALZ_LAUNCH_CHECK();
+    } else if (!src_dev && copy_kernel) {
+        SALZ_HIP(hipMemcpy(ws.text, src, N, hipMemcpyHostToDevice));
+        SALZ_HIP(hipDeviceSynchronize());
+    } else {
+        SALZ_HIP(hipMemcpyAsync(ws.text, src, N, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                st));
+    }
+    unsigned long long *dsum = reinterpret_cast<unsigned long long *>(ws.dscal) + 200;
+    unsigned int *dbad = reinterpret_cast<unsigned int *>(ws.dscal) + 420;
+    if (dev_check) {
+        SALZ_HIP(hipMemsetAsync(dsum, 0, 8, st));
+        SALZ_HIP(hipMemsetAsync(dbad, 0, 4, st));
+        hipLaunchKernelGGL(k_dbg_text_sum, dim3(grid_for(N, 256)), dim3(256), 0, st, ws.text, N, dsum);
+    }
+    SALZ_HIP(hipMemsetAsync(ws.text + N, 0, 128, st));
+    if (mark(ws, EV_UP)) return -1;
+    if (stage_suffix_array(ws, n)) return -1;
+    if (mark(ws, EV_SA)) return -1;
+    if (ws.dbg_sa)
+        SALZ_HIP(hipMemcpyAsync(ws.dbg_sa, ws.sa, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, st));
+    debug_hash(ws, "text", ws.text, N);
+    if (dev_check)
+        hipLaunchKernelGGL(k_dbg_sa_order, dim3(grid_for(n, 256)), dim3(256), 0, st, ws.text, ws.sa, n,
+                           dbad);
+    debug_hash(ws, "sa", ws.sa, sizeof(uint32_t) * n);
+    if (dump_after_sa(ws, n, dump)) return -1;
+    if (stage_lcp(ws, n, ws.u3)) return -1;
+    if (mark(ws, EV_LCP)) return -1;
+    debug_hash(ws, "lcp", ws.u3, sizeof(uint32_t) * n);
+    if (stage_candidates(ws, n, ws.u3)) return -1;
+    if (mark(ws, EV_ANSV)) return -1;
+    debug_hash(ws, "cand", ws.cand, sizeof(uint4) * n);
+    debug_cand(ws, n);
+    if (stage_parse(ws, n)) return -1;
+    if (mark(ws, EV_PARSE)) return -1;
+    debug_hash(ws, "choice", ws.parse.choice, n);
+    debug_hash(ws, "cost", ws.parse.cost, sizeof(uint32_t) * ((size_t)n + 1));
+    if (dump_after_parse(ws, n, dump)) return -1;
+    if (stage_emit(ws, n, (uint32_t)N, dst, cap, out_len)) return -1;
+    if (mark(ws, EV_EMIT)) return -1;
+    SALZ_HIP(hipStreamSynchronize(st));
+    if (dev_check) {
+        unsigned long long s = 0;
+        unsigned int b = 0;
+        SALZ_HIP(hipMemcpy(&s, dsum, 8, hipMemcpyDeviceToHost));
+        SALZ_HIP(hipMemcpy(&b, dbad, 4, hipMemcpyDeviceToHost));
+        unsigned long long hs = 0;
+        if (!src_dev) {
+            for (size_t i = 0; i < N; i++)
+                hs += (unsigned long long)src[i] * (unsigned long long)(i % 65521 + 1);
+        }
+        fprintf(stderr, "devcheck: text_sum %llx host %llx sa_order_bad %u\n", s, hs, b);
+    }
+    if (ws.timing) {
+        ws.stats.ms_upload = elapsed(ws, EV_START, EV_UP);
+        ws.stats.ms_sa = elapsed(ws, EV_UP, EV_SA);
+        ws.stats.ms_lcp = elapsed(ws, EV_SA, EV_LCP);
+        ws.stats.ms_ansv = elapsed(ws, EV_LCP, EV_ANSV);
+        ws.stats.ms_parse = elapsed(ws, EV_ANSV, EV_PARSE);
+        ws.stats.ms_emit = elapsed(ws, EV_PARSE, EV_EMIT);
+        ws.stats.ms_total = elapsed(ws, EV_START, EV_EMIT);
+        float rx = 0.f;
+        for (size_t i = 0; i + 1 < ws.rx_used; i += 2) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, ws.rx_pool[i], ws.rx_pool[i + 1]);
+            rx += ms;
+        }
+        ws.stats.ms_radix_scatter = rx;
+    }
+    return 0;
+}
+
+}  // namespace salz
+
+using namespace salz;
+
+struct salz_gpu_ctx {
+    Workspace ws;
+    std::mutex mu;
+};
+
+extern "C" {
+
+const char *salz_gpu_last_error(void) { return g_err; }
+
+// Test-only: fetch the SALZ_DEBUG_SAROUND snapshots of the last call (which: 0 sa, 1 round).
+int salz_debug_fetch(salz_gpu_ctx *ctx, int which, uint32_t *host, size_t count)
+{
+    const uint32_t *src = which == 0 ? ctx->ws.dbg_sa : ctx->ws.dbg_round;
+    if (!src)
+        return -1;
+    return hipMemcpy(host, src, count * 4, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+
+int salz_gpu_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    return n;
+}
+
+void *salz_gpu_malloc(int device, size_t bytes)
+{
+    void *p = nullptr;
+    if (hipSetDevice(device) != hipSuccess || hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+        set_error("hipMalloc(%zu) on device %d failed", bytes, device);
+        return nullptr;
+    }
+    return p;
+}
+
+void salz_gpu_free(int device, void *ptr)
+{
+    if (ptr && hipSetDevice(device) == hipSuccess)
+        (void)hipFree(ptr);
+}
+
+int salz_gpu_memcpy_h2d(int device, void *dst, const void *src, size_t bytes)
+{
+    SALZ_HIP(hipSetDevice(device));
+    SALZ_HIP(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int salz_gpu_memcpy_d2h(int device, void *dst, const void *src, size_t bytes)
+{
+    SALZ_HIP(hipSetDevice(device));
+    SALZ_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int salz_gpu_synchronize(int device)
+{
+    SALZ_HIP(hipSetDevice(device));
+    SALZ_HIP(hipDeviceSynchronize());
+    return 0;
+}
+
+salz_gpu_ctx *salz_gpu_ctx_create(int device, size_t max_block)
+{
+    salz_gpu_ctx *c = new (std::nothrow) salz_gpu_ctx();
+    if (!c) {
+        set_error("out of host memory");
+        return nullptr;
+    }
+    if (workspace_alloc(c->ws, device, max_block) != 0) {
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void salz_gpu_ctx_destroy(salz_gpu_ctx *ctx)
+{
+    if (!ctx)
+        return;
+    workspace_free(ctx->ws);
+    delete ctx;
+}
+
+void salz_gpu_set_timing(salz_gpu_ctx *ctx, int on)
+{
+    if (ctx)
+        ctx->ws.timing = on != 0;
+}
+
+int salz_gpu_get_stats(const salz_gpu_ctx *ctx, salz_gpu_stats *o)
+{
+    if (!ctx || !o)
+        return -1;
+    const StageStats &s = ctx->ws.stats;
+    o->ms_upload = s.ms_upload;
+    o->ms_sa = s.ms_sa;
+    o->ms_lcp = s.ms_lcp;
+    o->ms_ansv = s.ms_ansv;
+    o->ms_parse = s.ms_parse;
+    o->ms_emit = s.ms_emit;
+    o->ms_total = s.ms_total;
+    o->sa_rounds = s.sa_rounds;
+    o->parse_iters = s.parse_iters;
+    o->sa_sorted_elems = s.sa_sorted_elems;
+    o->lcp_long_bytes = s.lcp_long_bytes;
+    o->emit_bits = s.emit_bits;
+    o->emit_bytes = s.emit_bytes;
+    o->exit_nodes = s.exit_nodes;
+    o->radix_scatter_launches = s.radix_scatter_launches;
+    o->ms_radix_scatter = s.ms_radix_scatter;
+    o->radix_scatter_elems = s.radix_scatter_elems;
+    return 0;
+}
+
+int salz_gpu_encode_device(salz_gpu_ctx *ctx, const uint8_t *d_src, size_t src_len,
+                           uint8_t *d_dst, size_t dst_cap, size_t *dst_len, void *stream)
+{
+    if (!ctx || !d_src || !d_dst || !dst_len) {
+        set_error("NULL argument");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    Workspace &ws = ctx->ws;
+    hipStream_t saved = ws.stream;
+    if (stream)
+        ws.stream = static_cast<hipStream_t>(stream);
+    size_t len = 0;
+    int rc = encode_core(ws, d_src, true, src_len, d_dst, dst_cap, &len, nullptr);
+    ws.stream = saved;
+    if (rc == 0)
+        *dst_len = len;
+    return rc;
+}
+
+static int encode_host_locked(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, uint8_t *dst,
+                              size_t *dst_len, const salz_gpu_dump *dump)
+{
+    Workspace &ws = ctx->ws;
+    if (src_len > ws.cap_N) {
+        int dev = ws.device;
+        if (workspace_alloc(ws, dev, src_len) != 0)
+            return -1;
+    }
+    size_t cap = *dst_len < ws.out_cap ? *dst_len : ws.out_cap;
+    size_t len = 0;
+    if (encode_core(ws, src, false, src_len, ws.out, cap, &len, dump) != 0)
+        return -1;
+    if (hipMemcpy(dst, ws.out, len, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error("D2H copy of the encoded stream failed");
+        return -1;
+    }
+    *dst_len = len;  // set only on success (lib/salz.c:818)
+    return 0;
+}
+
+int salz_gpu_encode_host(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, uint8_t *dst,
+                         size_t *dst_len)
+{
+    if (!ctx || !src || !dst || !dst_len) {
+        set_error("NULL argument");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return encode_host_locked(ctx, src, src_len, dst, dst_len, nullptr);
+}
+
+int salz_gpu_encode_dump(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, uint8_t *dst,
+                         size_t *dst_len, const salz_gpu_dump *dump)
+{
+    if (!ctx || !src || !dst || !dst_len) {
+        set_error("NULL argument");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return encode_host_locked(ctx, src, src_len, dst, dst_len, dump);
+}
+
+// ---- default contexts behind salz_encode_safe ----------------------------------------------
+
+static std::mutex g_default_mu;
+static std::vector<salz_gpu_ctx *> g_default;
+
+static salz_gpu_ctx *default_ctx(int device, size_t need)
+{
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    if (g_default.empty()) {
+        int n = salz_gpu_device_count();
+        g_default.assign(n > 0 ? (size_t)n : 0, nullptr);
+    }
+    if (device < 0 || (size_t)device >= g_default.size()) {
+        set_error("no usable HIP device (gfx950) for salz_encode_safe");
+        return nullptr;
+    }
+    if (!g_default[device])
+        g_default[device] = salz_gpu_ctx_create(device, need);
+    return g_default[device];
+}
+
+// Called by salz_encode_safe (salz.c) after argument checks.
+int salz_gpu_encode_default(const uint8_t *src, size_t src_len, uint8_t *dst, size_t *dst_len)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+        dev = 0;
+    salz_gpu_ctx *c = default_ctx(dev, src_len);
+    if (!c)
+        return -1;
+    std::lock_guard<std::mutex> lk(c->mu);
+    return encode_host_locked(c, src, src_len, dst, dst_len, nullptr);
+}
+
+// ---- multi-block / multi-GPU container encode ---------------------------------------------
+
+size_t salz_blocks_len_max(size_t src_len, size_t block_size)
+{
+    if (block_size == 0)
+        return 0;
+    size_t blocks = src_len / block_size + 1;
+    return 8 + blocks * 4 + (size_t)salz_encoded_len_max(block_size) * blocks;
+}
+
+int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, uint8_t *dst,
+                       size_t *dst_len, int n_devices)
+{
+    if (!src || !dst || !dst_len || block_size == 0 || block_size > 0xffffffffu) {
+        set_error("invalid argument");
+        return -1;
+    }
+    int avail = salz_gpu_device_count();
+    if (avail <= 0) {
+        set_error("no usable HIP device");
+        return -1;
+    }
+    int ndev = (n_devices <= 0 || n_devices > avail) ? avail : n_devices;
+    // Block count follows the reference CLI loop (programs/salzcli.c:143-179): it always
+    // encodes the trailing fread() chunk, even an empty one when src_len is a multiple.
+    size_t nblocks = src_len / block_size + 1;
+    std::vector<std::vector<uint8_t>> streams(nblocks);
+    std::vector<int> rcs(nblocks, -1);
+    std::atomic<size_t> next{0};
+    std::vector<std::string> errs((size_t)ndev);
+    auto worker = [&](int dev) {
+        size_t need = block_size < src_len ? block_size : src_len;
+        salz_gpu_ctx *c = salz_gpu_ctx_create(dev, need < 9 ? 9 : need);
+        if (!c) {
+            errs[dev] = g_err;
+            return;
+        }
+        for (;;) {
+            size_t b = next.fetch_add(1);
+            if (b >= nblocks)
+                break;
+            size_t off = b * block_size;
+            size_t len = off + block_size <= src_len ? block_size : src_len - off;
+            size_t cap = (size_t)salz_encoded_len_max(block_size);
+            streams[b].resize(cap);
+            size_t out = cap;
+            {
+                std::lock_guard<std::mutex> lk(c->mu);
+                rcs[b] = encode_host_locked(c, src + off, len, streams[b].data(), &out, nullptr);
+            }
+            if (rcs[b] != 0) {
+                errs[dev] = g_err;
+                next.store(nblocks);
+                break;
+            }
+            streams[b].resize(out);
+        }
+        salz_gpu_ctx_destroy(c);
+    };
+    std::vector<std::thread> th;
+    for (int d = 0; d < ndev; d++)
+        th.emplace_back(worker, d);
+    for (auto &t : th)
+        t.join();
+    size_t need = 8;
+    for (size_t b = 0; b < nblocks; b++) {
+        if (rcs[b] != 0) {
+            std::string e;
+            for (auto &s : errs)
+                if (!s.empty())
+                    e = s;
+            set_error("block %zu failed: %s", b, e.c_str());
+            return -1;
+        }
+        need += 4 + streams[b].size();
+    }
+    if (need > *dst_len) {
+        set_error("container exceeds destination capacity");
+        return -1;
+    }
+    const uint32_t magic = 0x53414C5Au, bs = (uint32_t)block_size;
+    size_t o = 0;
+    memcpy(dst + o, &magic, 4);
+    memcpy(dst + o + 4, &bs, 4);
+    o += 8;
+    for (size_t b = 0; b < nblocks; b++) {
+        uint32_t L = (uint32_t)streams[b].size();
+        memcpy(dst + o, &L, 4);
+        memcpy(dst + o + 4, streams[b].data(), L);
+        o += 4 + L;
+    }
+    *dst_len = o;
+    return 0;
+}
+
+}  // extern "C"

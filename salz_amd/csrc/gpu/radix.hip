@@ -1,0 +1,320 @@
+// radix.hip - stable LSD radix sort of (u64 key, u32 value) pairs for gfx950.
+//
+// One 8-bit digit per pass, 4096-element tiles (256 threads x 16 items), reduce-then-scan:
+//   k_radix_hist    per-tile digit counts (LDS atomics into per-wave sub-histograms)
+//   scan            digit-major exclusive scan of the counts -> global tile offsets
+//   k_radix_scatter stable tile-local ranking with wave ballots (8 ballots build the peer
+//                   mask of lanes sharing a digit; mbcnt gives the rank below), then the
+//                   tile is staged in LDS in digit order and written out in contiguous runs.
+// Used by the prefix-doubling suffix sorter (sa.hip), which passes only the key bits that
+// vary in a round.
+#include "internal.hpp"
+
+#include <cstdlib>
+#include <vector>
+
+namespace salz {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kItems = 16;
+constexpr int kTile = kThreads * kItems;
+static_assert(kTile == kRadixTile, "tile size mismatch");
+
+__global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restrict__ keys,
+                                                         uint32_t m, int shift,
+                                                         uint32_t *__restrict__ counts,
+                                                         uint32_t ntiles)
+{
+    __shared__ uint32_t h[4][256];
+    unsigned tid = threadIdx.x, wave = tid >> 6;
+    for (int i = tid; i < 4 * 256; i += kThreads)
+        (&h[0][0])[i] = 0;
+    __syncthreads();
+    size_t base = (size_t)blockIdx.x * kTile;
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        size_t i = base + (size_t)j * kThreads + tid;
+        if (i < m) {
+            unsigned d = (unsigned)(keys[i] >> shift) & 255u;
+            atomicAdd(&h[wave][d], 1u);
+        }
+    }
+    __syncthreads();
+    counts[(size_t)tid * ntiles + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+}
+
+__global__ __launch_bounds__(kThreads) void k_radix_scatter(
+    const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+    uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t m, int shift,
+    const uint32_t *__restrict__ offs, uint32_t ntiles)
+{
+    __shared__ uint64_t skey[kTile];
+    __shared__ uint32_t sval[kTile];
+    __shared__ uint32_t cnt[4][256];
+    __shared__ uint32_t dstart[256];
+    __shared__ uint32_t gbase[256];
+    __shared__ uint32_t wsum[4];
+
+    const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (int i = tid; i < 4 * 256; i += kThreads)
+        (&cnt[0][0])[i] = 0;
+    __syncthreads();
+
+    // Warp-striped: wave w owns tile elements [w*1024, (w+1)*1024), item j covers 64 of them.
+    const size_t base = (size_t)blockIdx.x * kTile + (size_t)wave * (kItems * 64);
+    uint64_t k[kItems];
+    uint32_t v[kItems];
+    uint32_t lrank[kItems];
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        size_t i = base + (size_t)j * 64 + lane;
+        bool ok = i < m;
+        k[j] = ok ? kin[i] : 0ull;
+        v[j] = ok ? vin[i] : 0u;
+    }
+
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        size_t i = base + (size_t)j * 64 + lane;
+        bool ok = i < m;
+        unsigned d = (unsigned)(k[j] >> shift) & 255u;
+        uint64_t peers = wave_ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            bool bit = (d >> b) & 1u;
+            uint64_t bb = wave_ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        if (!ok)
+            peers = 0;
+        unsigned below = count_below(peers);
+        unsigned total = (unsigned)__popcll(peers);
+        int leader = peers ? (int)__ffsll((unsigned long long)peers) - 1 : (int)lane;
+        uint32_t old = 0;
+        if (ok && (int)lane == leader) {
+            old = cnt[wave][d];
+            cnt[wave][d] = old + total;
+        }
+        old = shfl_u32(old, leader);
+        lrank[j] = old + below;
+    }
+    __syncthreads();
+
+    // Per digit (thread = digit): wave prefixes and tile-local digit starts.
+    {
+        uint32_t c0 = cnt[0][tid], c1 = cnt[1][tid], c2 = cnt[2][tid], c3 = cnt[3][tid];
+        uint32_t tot = c0 + c1 + c2 + c3;
+        gbase[tid] = offs[(size_t)tid * ntiles + blockIdx.x];
+        // block exclusive scan of tot over 256 digits
+        uint32_t x = tot;
+#pragma unroll
+        for (unsigned dd = 1; dd < 64; dd <<= 1) {
+            uint32_t y = shfl_up_u32(x, dd);
+            if (lane >= dd)
+                x += y;
+        }
+        if (lane == 63)
+            wsum[wave] = x;
+        __syncthreads();
+        uint32_t pre = 0;
+        for (unsigned w = 0; w < wave; w++)
+            pre += wsum[w];
+        dstart[tid] = pre + x - tot;
+        cnt[0][tid] = 0;
+        cnt[1][tid] = c0;
+        cnt[2][tid] = c0 + c1;
+        cnt[3][tid] = c0 + c1 + c2;
+    }
+    __syncthreads();
+
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        size_t i = base + (size_t)j * 64 + lane;
+        if (i < m) {
+            unsigned d = (unsigned)(k[j] >> shift) & 255u;
+            uint32_t s = dstart[d] + cnt[wave][d] + lrank[j];
+            skey[s] = k[j];
+            sval[s] = v[j];
+        }
+    }
+    __syncthreads();
+
+    size_t tbase = (size_t)blockIdx.x * kTile;
+    uint32_t tcount = (uint32_t)((m - tbase) < (size_t)kTile ? (m - tbase) : (size_t)kTile);
+    for (uint32_t s = tid; s < tcount; s += kThreads) {
+        uint64_t key = skey[s];
+        unsigned d = (unsigned)(key >> shift) & 255u;
+        uint32_t g = gbase[d] + (s - dstart[d]);
+        kout[g] = key;
+        vout[g] = sval[s];
+    }
+}
+
+}  // namespace
+
+static uint64_t pair_hash(uint64_t k, uint32_t v)
+{
+    uint64_t x = k * 0x9E3779B97F4A7C15ull ^ ((uint64_t)v * 0xC2B2AE3D27D4EB4Full);
+    x ^= x >> 29;
+    return x * 0xBF58476D1CE4E5B9ull;
+}
+
+// SALZ_DEBUG_RADIX: host check of one sort (sorted on [lo,hi), same multiset of pairs).
+static void debug_radix(const uint64_t *dk, const uint32_t *dv, uint32_t m, int lo, int hi,
+                        hipStream_t st, uint64_t *sum_in, bool after)
+{
+    (void)hipStreamSynchronize(st);
+    std::vector<uint64_t> k(m);
+    std::vector<uint32_t> v(m);
+    (void)hipMemcpy(k.data(), dk, 8ull * m, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(v.data(), dv, 4ull * m, hipMemcpyDeviceToHost);
+    uint64_t s = 0;
+    for (uint32_t i = 0; i < m; i++)
+        s += pair_hash(k[i], v[i]);
+    if (!after) {
+        *sum_in = s;
+        return;
+    }
+    uint64_t mask = (hi >= 64 ? ~0ull : ((1ull << hi) - 1)) & ~((1ull << lo) - 1);
+    long unsorted = 0;
+    for (uint32_t i = 1; i < m; i++)
+        if ((k[i - 1] & mask) > (k[i] & mask) && !unsorted++)
+            fprintf(stderr, "RADIX unsorted at %u of %u bits [%d,%d)\n", i, m, lo, hi);
+    if (s != *sum_in || unsorted)
+        fprintf(stderr, "RADIX BAD m=%u bits [%d,%d): unsorted %ld multiset %s\n", m, lo, hi,
+                unsorted, s == *sum_in ? "ok" : "CHANGED");
+}
+
+int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
+                     uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st)
+{
+    if (m <= 1 || bit_hi <= bit_lo)
+        return 0;
+    static const bool dbg = getenv("SALZ_DEBUG_RADIX") != nullptr;
+    uint64_t dsum = 0;
+    if (dbg)
+        debug_radix(*keys, *vals, m, bit_lo, bit_hi, st, &dsum, false);
+    uint32_t ntiles = (m + kTile - 1) / kTile;
+    size_t ncounts = (size_t)ntiles * 256;
+    if (ncounts > ws.radix_counts_elems) {
+        set_error("radix: count buffer too small");
+        return -1;
+    }
+    uint64_t *kin = *keys, *kout = keys_alt;
+    uint32_t *vin = *vals, *vout = vals_alt;
+    for (int shift = bit_lo; shift < bit_hi; shift += 8) {
+        hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(kThreads), 0, st, kin, m, shift,
+                           ws.radix_counts, ntiles);
+        SALZ_LAUNCH_CHECK();
+        if (scan_sum_u32(ws.radix_counts, ws.radix_counts, ncounts, false, nullptr, ws, st) != 0)
+            return -1;
+        bool timed = ws.timing && ws.rx_used + 2 <= ws.rx_pool.size();
+        if (timed)
+            SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used], st));
+        hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, kout,
+                           vout, m, shift, ws.radix_counts, ntiles);
+        SALZ_LAUNCH_CHECK();
+        if (timed) {
+            SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used + 1], st));
+            ws.rx_used += 2;
+            ws.stats.radix_scatter_launches++;
+            ws.stats.radix_scatter_elems += m;
+        }
+        uint64_t *tk = kin;
+        kin = kout;
+        kout = tk;
+        uint32_t *tv = vin;
+        vin = vout;
+        vout = tv;
+    }
+    *keys = kin;
+    *vals = vin;
+    if (dbg)
+        debug_radix(kin, vin, m, bit_lo, bit_hi, st, &dsum, true);
+    return 0;
+}
+
+}  // namespace salz
+
+// ---- test-only: device-resident radix sort self-test (no host work between sorts) ---------
+namespace salz {
+namespace {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x)
+{
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__global__ void k_selftest_fill(uint64_t *k, uint32_t *v, uint32_t m, uint64_t seed, int bits,
+                                unsigned long long *sum)
+{
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m)
+        return;
+    uint64_t x = mix64(seed * 0x9E3779B97F4A7C15ull + i);
+    if (bits < 64)
+        x &= (1ull << bits) - 1;
+    // few distinct keys in half the runs: exercises stability
+    if (seed & 1)
+        x &= 0xF0F0ull;
+    k[i] = x;
+    v[i] = (uint32_t)i;
+    atomicAdd(sum, (unsigned long long)mix64(x ^ ((uint64_t)i << 40)));
+}
+
+__global__ void k_selftest_check(const uint64_t *k, const uint32_t *v, uint32_t m,
+                                 unsigned long long *sum, unsigned int *bad)
+{
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m)
+        return;
+    atomicAdd(sum, (unsigned long long)mix64(k[i] ^ ((uint64_t)v[i] << 40)));
+    if (i > 0 && (k[i - 1] > k[i] || (k[i - 1] == k[i] && v[i - 1] >= v[i])))
+        atomicAdd(bad, 1u);
+}
+
+}  // namespace
+}  // namespace salz
+
+extern "C" long salz_debug_radix_selftest(int device, uint32_t m, int bits, int iters,
+                                          uint64_t seed)
+{
+    using namespace salz;
+    Workspace ws;
+    if (workspace_alloc(ws, device, (size_t)m + 8) != 0)
+        return -1;
+    long failures = 0;
+    unsigned long long *dsum = reinterpret_cast<unsigned long long *>(ws.dscal) + 100;
+    unsigned int *dbad = reinterpret_cast<unsigned int *>(ws.dscal) + 300;
+    for (int it = 0; it < iters; it++) {
+        (void)hipMemsetAsync(dsum, 0, 16, ws.stream);
+        (void)hipMemsetAsync(dbad, 0, 4, ws.stream);
+        hipLaunchKernelGGL(k_selftest_fill, dim3(grid_for(m, 256)), dim3(256), 0, ws.stream,
+                           ws.keyA, ws.valA, m, seed + it, bits, dsum);
+        uint64_t *K = ws.keyA;
+        uint32_t *V = ws.valA;
+        if (radix_sort_pairs(&K, &V, ws.keyB, ws.valB, m, 0, bits, ws, ws.stream) != 0) {
+            failures++;
+            break;
+        }
+        hipLaunchKernelGGL(k_selftest_check, dim3(grid_for(m, 256)), dim3(256), 0, ws.stream, K, V,
+                           m, dsum + 1, dbad);
+        unsigned long long h[2];
+        unsigned int b = 0;
+        (void)hipMemcpyAsync(h, dsum, 16, hipMemcpyDeviceToHost, ws.stream);
+        (void)hipMemcpyAsync(&b, dbad, 4, hipMemcpyDeviceToHost, ws.stream);
+        (void)hipStreamSynchronize(ws.stream);
+        if (b || h[0] != h[1]) {
+            failures++;
+            fprintf(stderr, "radix selftest it=%d m=%u bits=%d: %u order/stability errors, multiset %s\n",
+                    it, m, bits, b, h[0] == h[1] ? "ok" : "CHANGED");
+        }
+    }
+    workspace_free(ws);
+    return failures;
+}

@@ -1,0 +1,184 @@
+// scan.hip - device-wide prefix scans (reduce-then-scan, 4096-element tiles).
+//
+// Used by every stage that compacts or ranks: group-head ranking in the suffix sorter,
+// radix digit offsets, PLCP max-propagation, parse exit sets and emission offsets.
+#include "internal.hpp"
+
+namespace salz {
+namespace {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+template <typename T> struct SumOp {
+    __device__ __forceinline__ static T id() { return T(0); }
+    __device__ __forceinline__ T operator()(T a, T b) const { return a + b; }
+};
+template <typename T> struct MaxOp {
+    __device__ __forceinline__ static T id() { return T(0); }
+    __device__ __forceinline__ T operator()(T a, T b) const { return a > b ? a : b; }
+};
+
+__device__ __forceinline__ uint32_t up(uint32_t v, unsigned d) { return shfl_up_u32(v, d); }
+__device__ __forceinline__ uint64_t up(uint64_t v, unsigned d) { return shfl_up_u64(v, d); }
+
+// LDS index with one pad word per 16 elements: a thread's 16 consecutive elements start on
+// distinct banks.
+__device__ __forceinline__ int pidx(int i) { return i + (i >> 4); }
+
+// Exclusive block scan over 256 threads; returns exclusive prefix, writes block total.
+template <typename T, typename Op>
+__device__ __forceinline__ T block_excl(T v, T *wsum, T &total, Op op)
+{
+    unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    T x = v;
+#pragma unroll
+    for (unsigned d = 1; d < 64; d <<= 1) {
+        T y = up(x, d);
+        if (lane >= d)
+            x = op(y, x);
+    }
+    if (lane == 63)
+        wsum[wave] = x;
+    __syncthreads();
+    T wpre = Op::id();
+    for (unsigned w = 0; w < wave; w++)
+        wpre = op(wpre, wsum[w]);
+    total = op(op(wsum[0], wsum[1]), op(wsum[2], wsum[3]));
+    T ex = up(x, 1);
+    if (lane == 0)
+        ex = Op::id();
+    __syncthreads();
+    return op(wpre, ex);
+}
+
+template <typename T, typename Op>
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const T *__restrict__ in, size_t n,
+                                                              T *__restrict__ partial)
+{
+    __shared__ T wsum[4];
+    Op op;
+    size_t base = (size_t)blockIdx.x * kScanTile;
+    T acc = Op::id();
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        size_t i = base + (size_t)j * kScanThreads + threadIdx.x;
+        if (i < n)
+            acc = op(acc, in[i]);
+    }
+    T total;
+    block_excl<T, Op>(acc, wsum, total, op);
+    if (threadIdx.x == 0)
+        partial[blockIdx.x] = total;
+}
+
+template <typename T, typename Op>
+__global__ __launch_bounds__(kScanThreads) void k_scan_tiles(const T *__restrict__ in, T *out,
+                                                             size_t n, const T *__restrict__ carry,
+                                                             int inclusive, T *total_out)
+{
+    __shared__ T s[kScanTile + kScanTile / 16];
+    __shared__ T wsum[4];
+    Op op;
+    size_t base = (size_t)blockIdx.x * kScanTile;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        int l = j * kScanThreads + threadIdx.x;
+        size_t i = base + l;
+        s[pidx(l)] = i < n ? in[i] : Op::id();
+    }
+    __syncthreads();
+    T loc[kScanItems];
+    T sum = Op::id();
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        loc[k] = s[pidx(threadIdx.x * kScanItems + k)];
+        sum = op(sum, loc[k]);
+    }
+    T total;
+    T run = block_excl<T, Op>(sum, wsum, total, op);
+    T c = carry ? carry[blockIdx.x] : Op::id();
+    run = op(c, run);
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        T nxt = op(run, loc[k]);
+        s[pidx(threadIdx.x * kScanItems + k)] = inclusive ? nxt : run;
+        run = nxt;
+    }
+    if (total_out && threadIdx.x == kScanThreads - 1 && blockIdx.x == gridDim.x - 1)
+        *total_out = run;  // includes the carry of this (last) tile
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        int l = j * kScanThreads + threadIdx.x;
+        size_t i = base + l;
+        if (i < n)
+            out[i] = s[pidx(l)];
+    }
+}
+
+template <typename T, typename Op>
+int scan_impl(const T *in, T *out, size_t n, bool inclusive, T *total_out, T *tmp,
+              size_t tmp_elems, hipStream_t st)
+{
+    if (n == 0)
+        return 0;
+    size_t tiles = (n + kScanTile - 1) / kScanTile;
+    if (tiles == 1) {
+        hipLaunchKernelGGL((k_scan_tiles<T, Op>), dim3(1), dim3(kScanThreads), 0, st, in, out,
+                           n, (const T *)nullptr, inclusive ? 1 : 0, total_out);
+        SALZ_LAUNCH_CHECK();
+        return 0;
+    }
+    if (tmp_elems < tiles) {
+        set_error("scan: temp too small (%zu < %zu)", tmp_elems, tiles);
+        return -1;
+    }
+    T *partial = tmp;
+    hipLaunchKernelGGL((k_scan_reduce<T, Op>), dim3((unsigned)tiles), dim3(kScanThreads), 0,
+                       st, in, n, partial);
+    SALZ_LAUNCH_CHECK();
+    if (scan_impl<T, Op>(partial, partial, tiles, false, nullptr, tmp + tiles,
+                         tmp_elems - tiles, st) != 0)
+        return -1;
+    hipLaunchKernelGGL((k_scan_tiles<T, Op>), dim3((unsigned)tiles), dim3(kScanThreads), 0, st,
+                       in, out, n, (const T *)partial, inclusive ? 1 : 0, total_out);
+    SALZ_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // namespace
+
+size_t scan_temp_elems(size_t n)
+{
+    size_t t = 0;
+    while (n > (size_t)kScanTile) {
+        n = (n + kScanTile - 1) / kScanTile;
+        t += n;
+    }
+    return t + 16;
+}
+
+int scan_sum_u32(const uint32_t *in, uint32_t *out, size_t n, bool inclusive,
+                 uint32_t *total_out, Workspace &ws, hipStream_t st)
+{
+    return scan_impl<uint32_t, SumOp<uint32_t>>(in, out, n, inclusive, total_out,
+                                                (uint32_t *)ws.scan_tmp, ws.scan_tmp_bytes / 4, st);
+}
+
+int scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, bool inclusive,
+                 uint32_t *total_out, Workspace &ws, hipStream_t st)
+{
+    return scan_impl<uint32_t, MaxOp<uint32_t>>(in, out, n, inclusive, total_out,
+                                                (uint32_t *)ws.scan_tmp, ws.scan_tmp_bytes / 4, st);
+}
+
+int scan_sum_u64(const uint64_t *in, uint64_t *out, size_t n, bool inclusive,
+                 uint64_t *total_out, Workspace &ws, hipStream_t st)
+{
+    return scan_impl<uint64_t, SumOp<uint64_t>>(in, out, n, inclusive, total_out,
+                                                (uint64_t *)ws.scan_tmp, ws.scan_tmp_bytes / 8, st);
+}
+
+}  // namespace salz

@@ -1,0 +1,158 @@
+"""GPU parity: the HIP pipeline against the CPU oracle and the reference's golden vectors.
+
+Every comparison is bit-exact (integer / byte work). Stage arrays are compared one by one
+so a mismatch names the stage (SA, PSV/NSV, lengths, decisions, costs, bytes).
+"""
+import numpy as np
+import pytest
+
+from tests.helpers import enc_max, gen, golden, oracle_decode, oracle_encode, oracle_stages, sha256
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def salz():
+    import salz_amd
+
+    if salz_amd.device_count() == 0:
+        pytest.fail("no HIP device visible: GPU tests need an MI355X")
+    return salz_amd
+
+
+@pytest.fixture(scope="module")
+def ctx(salz):
+    c = salz.Context(0, 1 << 25)
+    yield c
+    c.close()
+
+
+def _first_diff(a, b):
+    idx = np.nonzero(a != b)[0]
+    return int(idx[0]) if len(idx) else -1
+
+
+def _special(kind, n):
+    if kind == "zeros":
+        return np.zeros(n, np.uint8)
+    if kind == "period3":
+        return np.frombuffer((b"abc" * (n // 3 + 1))[:n], np.uint8).copy()
+    if kind == "runs":
+        rng = np.random.default_rng(5)
+        return np.repeat(rng.integers(0, 3, n // 50 + 1, dtype=np.uint8), 50)[:n].copy()
+    raise ValueError(kind)
+
+
+STAGE_CASES = [
+    ("fib", 10007, 0, 0),
+    ("smx", 20011, 3, 4),
+    ("smx", 70000, 9, 2),
+    ("smx", 50000, 5, 256),
+    ("text", 100003, 1, 0),
+    ("mixed", 300000, 2, 0),
+    ("zeros", 5000, 0, 0),
+    ("period3", 9001, 0, 0),
+    ("runs", 40000, 0, 0),
+]
+
+
+def _make(kind, n, seed, alpha):
+    if kind in ("zeros", "period3", "runs"):
+        return _special(kind, n)
+    return gen(kind, n, seed, alpha)
+
+
+@pytest.mark.parametrize("kind,n,seed,alpha", STAGE_CASES)
+def test_stages_match_oracle(ctx, kind, n, seed, alpha):
+    src = _make(kind, n, seed, alpha)
+    out, d = ctx.encode_dump(src)
+    o = oracle_stages(src)
+    for k in ("sa", "psv", "nsv", "lp", "ln", "dlen", "doff"):
+        i = _first_diff(d[k], o[k])
+        assert i < 0, f"{k} differs at {i}: gpu {d[k][i]} oracle {o[k][i]}"
+    i = _first_diff(d["cost"][1:], o["cost"][1:])
+    assert i < 0, f"cost differs at {i + 1}"
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and out == ref
+
+
+@pytest.mark.parametrize("vec", [v for v in golden("appendix_c.json")["vectors"] if v["n"] <= 1 << 24],
+                         ids=lambda v: f"{v['kind']}{v['n']}-{v['alphabet']}")
+def test_appendix_c_golden(ctx, vec):
+    src = gen(vec["kind"], vec["n"], vec["seed"], vec["alphabet"])
+    assert sha256(src) == vec["in_sha256"]
+    out = ctx.encode(src)
+    assert len(out) == vec["out_len"]
+    assert sha256(out) == vec["out_sha256"]
+
+
+def test_edge_sizes(ctx, salz):
+    rng = np.random.default_rng(11)
+    for N in list(range(9, 81)) + [127, 128, 129, 4095, 4096, 4097, 65536 + 9]:
+        for kind in ("rand4", "zeros", "rand256"):
+            if kind == "rand4":
+                src = rng.integers(97, 101, N, dtype=np.uint8)
+            elif kind == "zeros":
+                src = np.zeros(N, np.uint8)
+            else:
+                src = rng.integers(0, 256, N, dtype=np.uint8)
+            rc, ref = oracle_encode(src)
+            out = ctx.encode(src)
+            assert rc == 0 and out == ref, (N, kind)
+
+
+def test_short_blocks_fail_like_reference(ctx, salz):
+    for N in range(0, 9):
+        with pytest.raises(salz.SalzError):
+            ctx.encode(np.zeros(N, np.uint8))
+
+
+def test_capacity_failure(ctx, salz):
+    src = gen("text", 50000, 3)
+    rc, ref = oracle_encode(src)
+    assert rc == 0
+    assert ctx.encode(src, dst_capacity=len(ref)) == ref
+    with pytest.raises(salz.SalzError):
+        ctx.encode(src, dst_capacity=len(ref) - 1)
+
+
+def test_encode_safe_default_context_and_roundtrip(salz):
+    src = gen("text", 1048575, 7)
+    out = salz.encode_safe(src)
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and out == ref
+    assert salz.decode_safe(out, len(src)) == src.tobytes()
+    rc, back = oracle_decode(out, len(src))
+    assert rc == 0 and back == src.tobytes()
+
+
+def test_plain_fallback(ctx):
+    src = gen("smx", 300000, 4, 256)
+    out = ctx.encode(src)
+    assert out[3] == 0 and len(out) == len(src) + 4
+    assert out[4:] == src.tobytes()
+
+
+def test_text_4mib_matches_oracle(ctx):
+    src = gen("text", 4 << 20, 3)
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and ctx.encode(src) == ref
+
+
+def test_device_resident_api(salz):
+    src = gen("text", 2 << 20, 5)
+    rc, ref = oracle_encode(src)
+    ctx = salz.Context(0, len(src))
+    d_src = salz.DeviceBuffer(len(src)).upload(src)
+    d_dst = salz.DeviceBuffer(enc_max(len(src)))
+    n = ctx.encode_device(d_src.ptr, len(src), d_dst.ptr, d_dst.nbytes)
+    assert d_dst.download(n) == ref
+    # same context, second block of a different size: workspace reuse is exact
+    src2 = gen("fib", 1 << 20)
+    d_src.upload(src2)
+    n2 = ctx.encode_device(d_src.ptr, len(src2), d_dst.ptr, d_dst.nbytes)
+    rc, ref2 = oracle_encode(src2)
+    assert d_dst.download(n2) == ref2
+    d_src.free()
+    d_dst.free()
+    ctx.close()
