@@ -67,8 +67,6 @@ struct Workspace {
     ParseState parse{};
     hipEvent_t ev[16] = {};
     // begin/end event pairs around every radix scatter launch, resolved after the call
-    uint32_t *dbg_round = nullptr;  // SALZ_DEBUG_SAROUND: round that committed sa[r]
-    uint32_t *dbg_sa = nullptr;     // snapshot of sa after the suffix sort
     std::vector<hipEvent_t> rx_pool;
     size_t rx_used = 0;
 };

@@ -49,7 +49,7 @@ void workspace_free(Workspace &ws)
 {
     if (ws.device >= 0)
         (void)hipSetDevice(ws.device);
-    void *ptrs[] = {ws.dbg_round, ws.dbg_sa, ws.text, ws.rank,     ws.sa,   ws.keyA, ws.keyB, ws.valA, ws.valB,
+    void *ptrs[] = {ws.text, ws.rank,     ws.sa,   ws.keyA, ws.keyB, ws.valA, ws.valB,
                     ws.u0,   ws.u1,       ws.u2,   ws.u3,   ws.g64,  ws.offA, ws.offB,
                     ws.cand, ws.out,      ws.radix_counts,  ws.scan_tmp,      ws.dscal};
     for (void *p : ptrs)
@@ -93,7 +93,7 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
         dalloc(&ws.offB, n1) || dalloc(&ws.cand, ws.cap_n + 1) || dalloc(&ws.out, ws.out_cap) ||
         dalloc(&ws.radix_counts, ws.radix_counts_elems) ||
         dalloc(reinterpret_cast<uint8_t **>(&ws.scan_tmp), ws.scan_tmp_bytes) ||
-        dalloc(&ws.dscal, 512)) {
+        dalloc(&ws.dscal, 1024)) {
         std::string keep = g_err;
         workspace_free(ws);
         set_error("%s", keep.c_str());
@@ -106,10 +106,6 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
     ws.own_stream = true;
     for (hipEvent_t &e : ws.ev)
         SALZ_HIP(hipEventCreate(&e));
-    if (getenv("SALZ_DEBUG_SAROUND")) {
-        if (dalloc(&ws.dbg_round, n1) || dalloc(&ws.dbg_sa, n1))
-            return -1;
-    }
     ws.rx_pool.resize(2048);
     for (hipEvent_t &e : ws.rx_pool)
         SALZ_HIP(hipEventCreate(&e));
@@ -245,17 +241,6 @@ __global__ void k_dbg_sa_order(const uint8_t *T, const uint32_t *sa, uint32_t n,
         atomicAdd(bad, 1u);
 }
 
-__global__ void k_copy_bytes(uint8_t *dst, const uint8_t *src, size_t N)
-{
-    size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16;
-    if (i + 16 <= N && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0) {
-        *reinterpret_cast<uint4 *>(dst + i) = *reinterpret_cast<const uint4 *>(src + i);
-    } else {
-        for (size_t j = i; j < i + 16 && j < N; j++)
-            dst[j] = src[j];
-    }
-}
-
 // SALZ_DEBUG_CAND=1: validate candidates after ANSV; on a bad one, cross-check SA / LCP.
 static void debug_cand(Workspace &ws, uint32_t n)
 {
@@ -328,19 +313,9 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t N
     ws.rx_used = 0;
 
     if (mark(ws, EV_START)) return -1;
-    static const bool copy_kernel = getenv("SALZ_COPY_KERNEL") != nullptr;
     static const bool dev_check = getenv("SALZ_DEBUG_DEVICE") != nullptr;
-    if (src_dev && copy_kernel) {
-        hipLaunchKernelGGL(k_copy_bytes, dim3(grid_for((N + 15) / 16, 256)), dim3(256), 0, st, ws.text,
-                           src, N);
-        SALZ_LAUNCH_CHECK();
-    } else if (!src_dev && copy_kernel) {
-        SALZ_HIP(hipMemcpy(ws.text, src, N, hipMemcpyHostToDevice));
-        SALZ_HIP(hipDeviceSynchronize());
-    } else {
-        SALZ_HIP(hipMemcpyAsync(ws.text, src, N, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                                st));
-    }
+    SALZ_HIP(hipMemcpyAsync(ws.text, src, N, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                            st));
     unsigned long long *dsum = reinterpret_cast<unsigned long long *>(ws.dscal) + 200;
     unsigned int *dbad = reinterpret_cast<unsigned int *>(ws.dscal) + 420;
     if (dev_check) {
@@ -352,8 +327,6 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t N
     if (mark(ws, EV_UP)) return -1;
     if (stage_suffix_array(ws, n)) return -1;
     if (mark(ws, EV_SA)) return -1;
-    if (ws.dbg_sa)
-        SALZ_HIP(hipMemcpyAsync(ws.dbg_sa, ws.sa, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, st));
     debug_hash(ws, "text", ws.text, N);
     if (dev_check)
         hipLaunchKernelGGL(k_dbg_sa_order, dim3(grid_for(n, 256)), dim3(256), 0, st, ws.text, ws.sa, n,
@@ -418,15 +391,6 @@ struct salz_gpu_ctx {
 extern "C" {
 
 const char *salz_gpu_last_error(void) { return g_err; }
-
-// Test-only: fetch the SALZ_DEBUG_SAROUND snapshots of the last call (which: 0 sa, 1 round).
-int salz_debug_fetch(salz_gpu_ctx *ctx, int which, uint32_t *host, size_t count)
-{
-    const uint32_t *src = which == 0 ? ctx->ws.dbg_sa : ctx->ws.dbg_round;
-    if (!src)
-        return -1;
-    return hipMemcpy(host, src, count * 4, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
 
 int salz_gpu_device_count(void)
 {

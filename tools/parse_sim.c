@@ -1,0 +1,111 @@
+/*
+ * parse_sim.c - CPU simulation of the GPU parse fixed point (design tool, not shipped).
+ * Given candidate arrays (offP, lenP, offN, lenN per position), runs the chunked fixed-point
+ * iteration for a chunk size and reports iterations and exit-node counts; checks the result
+ * against the sequential DP.
+ *   int parse_sim(const int32_t *psv, const int32_t *lp, const int32_t *nsv, const int32_t *ln,
+ *                 int32_t n, int32_t chunk, int32_t seed_mode, int32_t *iters_out,
+ *                 int64_t *exits_out)
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+static uint32_t vn(uint32_t v)
+{
+    static const uint32_t lim[10] = {8u, 72u, 584u, 4680u, 37448u, 299592u, 2396744u,
+                                     19173960u, 153391688u, 1227133512u};
+    uint32_t k = 1;
+    for (int i = 0; i < 10; i++)
+        k += v >= lim[i];
+    return k;
+}
+
+static uint32_t fbits(uint32_t off, uint32_t len)
+{
+    return 1u + 8u + 4u * vn((off - 1u) >> 8) + ((len - 3u) >> 3) + 4u;
+}
+
+int parse_sim(const int32_t *psv, const int32_t *lp, const int32_t *nsv, const int32_t *ln,
+              int32_t n, int32_t chunk, int32_t seed_mode, int32_t *iters_out, int64_t *exits_out)
+{
+    uint32_t *cin = malloc(4ull * (n + 1)), *cout = malloc(4ull * (n + 1));
+    uint32_t *ex = malloc(4ull * n), *sm = malloc(4ull * n), *ref = malloc(4ull * (n + 1));
+    uint8_t *chold = malloc(n), *chnew = malloc(n), *flag = calloc(n + 1, 1);
+    uint8_t *refch = malloc(n);
+    /* sequential reference DP */
+    ref[n] = 0;
+    for (int32_t p = n - 1; p >= 0; p--) {
+        uint32_t best = 9u + ref[p + 1];
+        uint8_t ch = 0;
+        if (p) {
+            if (lp[p] >= 3) {
+                uint32_t a = fbits(p - psv[p], lp[p]) + ref[p + lp[p]];
+                if ((int32_t)a < (int32_t)best) { best = a; ch = 1; }
+            }
+            if (ln[p] >= 3) {
+                uint32_t a = fbits(p - nsv[p], ln[p]) + ref[p + ln[p]];
+                if ((int32_t)a < (int32_t)best) { best = a; ch = 2; }
+            }
+        }
+        ref[p] = best;
+        refch[p] = ch;
+    }
+    for (int32_t q = 0; q <= n; q++)
+        cin[q] = seed_mode == 0 ? 9u * (uint32_t)(n - q) : (seed_mode == 1 ? 0u : 3u * (uint32_t)(n - q));
+    memset(chold, 0xff, n);
+    int it;
+    int64_t exits = 0;
+    for (it = 0; it < 100000; it++) {
+        long changed = 0;
+        for (int32_t a = 0; a < n; a += chunk) {
+            int32_t b = a + chunk < n ? a + chunk : n;
+            for (int32_t p = b - 1; p >= a; p--) {
+                uint32_t nx1 = p + 1;
+                uint32_t best = 9u + (nx1 >= (uint32_t)b ? cin[nx1] : cout[nx1]);
+                uint32_t len = 1, w = 9;
+                uint8_t ch = 0;
+                if (p) {
+                    if (lp[p] >= 3) {
+                        uint32_t q = p + lp[p], wf = fbits(p - psv[p], lp[p]);
+                        uint32_t alt = wf + (q >= (uint32_t)b ? cin[q] : cout[q]);
+                        if ((int32_t)alt < (int32_t)best) { best = alt; len = lp[p]; w = wf; ch = 1; }
+                    }
+                    if (ln[p] >= 3) {
+                        uint32_t q = p + ln[p], wf = fbits(p - nsv[p], ln[p]);
+                        uint32_t alt = wf + (q >= (uint32_t)b ? cin[q] : cout[q]);
+                        if ((int32_t)alt < (int32_t)best) { best = alt; len = ln[p]; w = wf; ch = 2; }
+                    }
+                }
+                uint32_t nx = p + len;
+                if (nx >= (uint32_t)b) { ex[p] = nx; sm[p] = w; }
+                else { ex[p] = ex[nx]; sm[p] = w + sm[nx]; }
+                cout[p] = best;
+                changed += ch != chold[p];
+                chnew[p] = ch;
+            }
+        }
+        uint8_t *t = chold; chold = chnew; chnew = t;
+        if (!changed)
+            break;
+        /* exact costs of the new decisions */
+        memset(flag, 0, n + 1);
+        for (int32_t p = 0; p < n; p++)
+            flag[ex[p]] = 1;
+        flag[n] = 1;
+        exits = 0;
+        for (int32_t q = 0; q <= n; q++)
+            exits += flag[q];
+        cout[n] = 0;
+        for (int32_t q = n - 1; q >= 0; q--) /* backward: targets are exact already */
+            cout[q] = sm[q] + cout[ex[q]];
+        uint32_t *tc = cin; cin = cout; cout = tc;
+    }
+    int ok = 1;
+    for (int32_t p = 1; p < n; p++)
+        if (chold[p] != refch[p]) { ok = 0; break; }
+    *iters_out = it + 1;
+    *exits_out = exits;
+    free(cin); free(cout); free(ex); free(sm); free(ref); free(chold); free(chnew); free(flag); free(refch);
+    return ok;
+}
