@@ -24,23 +24,26 @@ constexpr uint32_t kInf = 0xffffffffu;
 
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
-__device__ __forceinline__ void put_psv(uint4 *cand, uint32_t p, uint32_t psv_pos, uint32_t len)
+// cand is stored in the parse's chunk-interleaved layout (common.hpp, sidx).
+__device__ __forceinline__ void put_psv(uint4 *cand, uint32_t klog, uint32_t p, uint32_t psv_pos,
+                                        uint32_t len)
 {
     uint2 v = psv_pos == kInf ? make_uint2(p + 1u, 0u) : make_uint2(p - psv_pos, len);
-    reinterpret_cast<uint2 *>(cand)[2 * (size_t)p] = v;
+    reinterpret_cast<uint2 *>(cand)[2 * sidx(p, klog)] = v;
 }
 
-__device__ __forceinline__ void put_nsv(uint4 *cand, uint32_t p, uint32_t nsv_pos, uint32_t len)
+__device__ __forceinline__ void put_nsv(uint4 *cand, uint32_t klog, uint32_t p, uint32_t nsv_pos,
+                                        uint32_t len)
 {
     uint2 v = nsv_pos == kInf ? make_uint2(p + 1u, 0u) : make_uint2(p - nsv_pos, len);
-    reinterpret_cast<uint2 *>(cand)[2 * (size_t)p + 1] = v;
+    reinterpret_cast<uint2 *>(cand)[2 * sidx(p, klog) + 1] = v;
 }
 
 __global__ __launch_bounds__(kT) void k_ansv_local(
     const uint32_t *__restrict__ sa, const uint32_t *__restrict__ lcp, uint32_t n, uint32_t np2,
     uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp, uint4 *__restrict__ cand,
     uint32_t *__restrict__ qp, uint32_t *__restrict__ qp_len, uint32_t *__restrict__ qn,
-    uint32_t *__restrict__ qn_len, uint32_t *__restrict__ qcount)
+    uint32_t *__restrict__ qn_len, uint32_t *__restrict__ qcount, uint32_t klog)
 {
     __shared__ uint32_t vsa[2 * kB];
     __shared__ uint32_t vlc[2 * kB];
@@ -98,7 +101,7 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
             node >>= 1;
         }
         if (hit != kInf) {
-            put_psv(cand, v, vsa[kB + hit], lm);
+            put_psv(cand, klog, v, vsa[kB + hit], lm);
         } else {
             uint32_t q = atomicAdd(&qcount[0], 1u);
             qp[q] = r;
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
             node >>= 1;
         }
         if (hit != kInf) {
-            put_nsv(cand, v, vsa[kB + hit], lm);
+            put_nsv(cand, klog, v, vsa[kB + hit], lm);
         } else {
             uint32_t q = atomicAdd(&qcount[1], 1u);
             qn[q] = r;
@@ -173,7 +176,7 @@ struct Tree {
 // Queries that left their block: continue the climb from the block root.
 __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
                               const uint32_t *__restrict__ qlen, uint32_t nq, int nsv,
-                              uint4 *__restrict__ cand)
+                              uint4 *__restrict__ cand, uint32_t klog)
 {
     uint32_t x = blockIdx.x * kT + threadIdx.x;
     if (x >= nq)
@@ -207,12 +210,12 @@ __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
     }
     uint32_t pos = hit == kInf ? kInf : t.sa[hit];
     if (nsv)
-        put_nsv(cand, v, pos, lm);
+        put_nsv(cand, klog, v, pos, lm);
     else
-        put_psv(cand, v, pos, lm);
+        put_psv(cand, klog, v, pos, lm);
 }
 
-__global__ void k_cand_origin(uint4 *cand) { cand[0] = make_uint4(1u, 1u, 1u, 1u); }
+__global__ void k_cand_origin(uint4 *cand) { cand[0] = make_uint4(1u, 1u, 1u, 1u); }  // sidx(0) == 0
 
 }  // namespace
 
@@ -244,7 +247,7 @@ int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp)
                                 sizeof(uint32_t) * (nblocks - used_blocks), st));
     }
     hipLaunchKernelGGL(k_ansv_local, dim3(used_blocks), dim3(kT), 0, st, ws.sa, lcp, n, np2, tsa,
-                       tlcp, ws.cand, qp, qpl, qn, qnl, cnt);
+                       tlcp, ws.cand, qp, qpl, qn, qnl, cnt, ws.klog);
     SALZ_LAUNCH_CHECK();
     for (uint32_t lo = nblocks / 2; lo >= 1; lo >>= 1) {
         hipLaunchKernelGGL(k_tree_level, dim3(grid_for(lo, kT)), dim3(kT), 0, st, tsa, tlcp, lo,
@@ -258,12 +261,12 @@ int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp)
     Tree t{tsa, tlcp, ws.sa, lcp, n, np2};
     if (nqp) {
         hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqp, kT)), dim3(kT), 0, st, t, qp, qpl,
-                           nqp, 0, ws.cand);
+                           nqp, 0, ws.cand, ws.klog);
         SALZ_LAUNCH_CHECK();
     }
     if (nqn) {
         hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqn, kT)), dim3(kT), 0, st, t, qn, qnl,
-                           nqn, 1, ws.cand);
+                           nqn, 1, ws.cand, ws.klog);
         SALZ_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(k_cand_origin, dim3(1), dim3(1), 0, st, ws.cand);

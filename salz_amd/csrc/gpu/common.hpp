@@ -93,6 +93,28 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
     return v;
 }
 
+// ---- chunk-interleaved layout of the per-position parse arrays --------------------------
+// The parse walks each chunk of K = 2^klog positions backwards, one lane per chunk, and the
+// 64 lanes of a wave own 64 consecutive chunks (a "tile" of 64K positions). Position
+// p = (tile t, lane l, row j) with j = p mod K, l = (p / K) mod 64, t = p / 64K is stored at
+// t*64K + j*64 + l, so a wave stepping row j in lockstep touches 64 consecutive elements.
+// Arrays in this layout: candidates (ansv.hip), choices, costs and parse state (parse.hip).
+constexpr uint32_t kTileChunks = 64;
+constexpr uint32_t kMaxChunkLog = 9;  // K <= 512
+constexpr size_t kLayoutPad = (size_t)kTileChunks << kMaxChunkLog;  // storage granularity
+
+__host__ __device__ __forceinline__ size_t sidx(uint32_t p, uint32_t klog)
+{
+    const uint32_t j = p & ((1u << klog) - 1u), c = p >> klog;
+    return ((size_t)(c >> 6) << (klog + 6)) | ((size_t)j << 6) | (c & 63u);
+}
+
+__host__ __device__ __forceinline__ uint64_t spos(size_t s, uint32_t klog)
+{
+    const size_t t = s >> (klog + 6), j = (s >> 6) & ((1u << klog) - 1u), l = s & 63u;
+    return (((uint64_t)t * 64u + l) << klog) | j;
+}
+
 // Unaligned little-endian 8-byte load from an 8-byte-aligned, padded byte buffer.
 __device__ __forceinline__ uint64_t load_u64_any(const uint8_t *base, size_t pos)
 {

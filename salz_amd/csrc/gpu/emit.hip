@@ -58,10 +58,10 @@ __device__ __forceinline__ uint64_t vn_bits(uint32_t v, uint32_t k)
     return r;
 }
 
-__global__ void k_mark_start(const uint32_t *__restrict__ eidx, const uint32_t *__restrict__ ex,
+__global__ void k_mark_start(const uint32_t *__restrict__ eidx, const uint64_t *__restrict__ pst,
                              uint32_t *__restrict__ emark)
 {
-    emark[eidx[ex[0]]] = 1u;
+    emark[eidx[(uint32_t)pst[0]]] = 1u;  // exit of position 0 (slot sidx(0) == 0)
 }
 
 __global__ void k_mark_step(const uint32_t *__restrict__ jt, uint32_t *emark, uint32_t ne)
@@ -86,19 +86,21 @@ struct Token {
     uint32_t len, off;  // len 1 = literal
 };
 
-__device__ __forceinline__ Token token_at(const uint4 *cand, const uint8_t *choice, uint32_t p)
+__device__ __forceinline__ Token token_at(const uint4 *cand, const uint8_t *choice, uint32_t p,
+                                          uint32_t klog)
 {
-    uint8_t ch = choice[p];
+    const size_t s = sidx(p, klog);
+    uint8_t ch = choice[s];
     if (ch == 0)
         return {1u, 0u};
-    uint4 c = cand[p];
+    uint4 c = cand[s];
     return ch == 1 ? Token{c.y, c.x} : Token{c.w, c.z};
 }
 
 __global__ void k_emit_count(const uint4 *__restrict__ cand, const uint8_t *__restrict__ choice,
                              const uint32_t *__restrict__ entry, uint32_t n, uint32_t N,
                              uint32_t chunk, uint32_t nch, uint64_t *__restrict__ cbits,
-                             uint64_t *__restrict__ cbytes)
+                             uint64_t *__restrict__ cbytes, uint32_t klog)
 {
     uint32_t g = blockIdx.x * kT + threadIdx.x;
     if (g > nch)
@@ -112,7 +114,7 @@ __global__ void k_emit_count(const uint4 *__restrict__ cand, const uint8_t *__re
         if (p != kNone) {
             uint32_t b = (n - g * chunk) < chunk ? n : g * chunk + chunk;
             while (p < b) {
-                Token t = token_at(cand, choice, p);
+                Token t = token_at(cand, choice, p, klog);
                 if (t.len == 1) {
                     bits += 1;
                     bytes += 1;
@@ -197,7 +199,8 @@ __global__ void k_emit_write(const uint8_t *__restrict__ T, const uint4 *__restr
                              const uint8_t *__restrict__ choice, const uint32_t *__restrict__ entry,
                              uint32_t n, uint32_t N, uint32_t chunk, uint32_t nch,
                              const uint64_t *__restrict__ bst, const uint64_t *__restrict__ yst,
-                             uint64_t btotal, uint64_t *W, uint32_t *Yk, uint8_t *out)
+                             uint64_t btotal, uint64_t *W, uint32_t *Yk, uint8_t *out,
+                             uint32_t klog)
 {
     uint32_t g = blockIdx.x * kT + threadIdx.x;
     if (g > nch)
@@ -223,7 +226,7 @@ __global__ void k_emit_write(const uint8_t *__restrict__ T, const uint4 *__restr
         uint32_t p = g == 0 ? 0u : entry[g];
         uint32_t b = (n - g * chunk) < chunk ? n : g * chunk + chunk;
         while (p < b) {
-            Token t = token_at(cand, choice, p);
+            Token t = token_at(cand, choice, p, klog);
             if (t.len == 1) {
                 s.put(0, 1);
                 s.byte(T[p]);
@@ -272,7 +275,7 @@ int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap, 
     SALZ_HIP(hipMemsetAsync(entry, 0xff, sizeof(uint32_t) * ((size_t)nch + 1), st));
     if (ne) {
         SALZ_HIP(hipMemsetAsync(emark, 0, sizeof(uint32_t) * ne, st));
-        hipLaunchKernelGGL(k_mark_start, dim3(1), dim3(1), 0, st, eidx, ps.ex, emark);
+        hipLaunchKernelGGL(k_mark_start, dim3(1), dim3(1), 0, st, eidx, ps.pst, emark);
         SALZ_LAUNCH_CHECK();
         for (uint32_t k = 0; k < ps.levels; k++) {
             hipLaunchKernelGGL(k_mark_step, dim3(grid_for(ne, kT)), dim3(kT), 0, st,
@@ -284,7 +287,7 @@ int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap, 
         SALZ_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(k_emit_count, dim3(grid_for((size_t)nch + 1, kT)), dim3(kT), 0, st,
-                       ws.cand, ps.choice, entry, n, N, ps.chunk, nch, cbits, cbytes);
+                       ws.cand, ps.choice, entry, n, N, ps.chunk, nch, cbits, cbytes, ws.klog);
     SALZ_LAUNCH_CHECK();
     if (scan_sum_u64(cbits, cbits, (size_t)nch + 1, false, tot + 0, ws, st) != 0)
         return -1;
@@ -317,7 +320,7 @@ int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap, 
         SALZ_HIP(hipMemsetAsync(W, 0, sizeof(uint64_t) * (nwords + 1), st));
         hipLaunchKernelGGL(k_emit_write, dim3(grid_for((size_t)nch + 1, kT)), dim3(kT), 0, st,
                            ws.text, ws.cand, ps.choice, entry, n, N, ps.chunk, nch, cbits, cbytes,
-                           btotal, W, Yk, dst);
+                           btotal, W, Yk, dst, ws.klog);
         SALZ_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_place_words, dim3(grid_for(nwords, kT)), dim3(kT), 0, st, W, Yk,
                            nwords, dst);

@@ -25,13 +25,14 @@ struct StageStats {
     uint64_t emit_bits, emit_bytes;
 };
 
-// Parse/emit scratch carving (parse.hip owns the layout, emit.hip reads it).
+// Parse/emit scratch carving (parse.hip owns the layout, emit.hip reads it). Per-position
+// arrays are in the chunk-interleaved layout (common.hpp, sidx with Workspace::klog).
 struct ParseState {
-    uint32_t chunk;         // positions per parse lane
+    uint32_t chunk;         // positions per parse lane (1 << klog)
     uint32_t nchunks;
     uint8_t *choice;        // final decisions: 0 literal, 1 PSV, 2 NSV
     uint32_t *cost;         // exact suffix costs, cost[n] = 0
-    uint32_t *ex, *sm;      // chunk exit and in-chunk bit sum per position
+    uint64_t *pst;          // per position: chunk-local cost estimate << 32 | chunk exit
     uint32_t n_exit;        // |E|
     uint32_t *elist;        // E nodes (positions), ascending; last is n
     uint32_t *jt0;          // parent (compact) per E node, snapshot level 0
@@ -43,6 +44,8 @@ struct Workspace {
     size_t cap_N = 0;  // largest block (bytes) this workspace accepts
     size_t cap_n = 0;  // cap_N - 8
     size_t np2 = 0;    // power of two >= cap_n (ANSV tree leaves)
+    size_t cap_s = 0;  // storage slots of the interleaved per-position arrays (>= cap_n + 1)
+    uint32_t klog = 9; // parse chunk = 1 << klog positions for the current block
 
     uint8_t *text = nullptr;  // padded copy of the block
     uint32_t *rank = nullptr, *sa = nullptr;
@@ -51,7 +54,8 @@ struct Workspace {
     uint32_t *u0 = nullptr, *u1 = nullptr, *u2 = nullptr, *u3 = nullptr;  // n+2 each
     uint64_t *g64 = nullptr;                                             // n+2
     uint32_t *offA = nullptr, *offB = nullptr;                           // n+2 each
-    uint4 *cand = nullptr;                                               // n
+    uint4 *cand = nullptr;                                               // cap_s, interleaved
+    uint64_t *pst = nullptr;                                             // cap_s, interleaved
     uint8_t *out = nullptr;                                              // encoded_len_max
     size_t out_cap = 0;
     uint32_t *radix_counts = nullptr;
@@ -97,6 +101,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n);                 // sa.hip   -
 int stage_lcp(Workspace &ws, uint32_t n, uint32_t *lcp_out);       // lcp.hip  -> lcp[r]
 int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp);  // ansv.hip -> ws.cand
 int stage_parse(Workspace &ws, uint32_t n);                        // parse.hip
+uint32_t parse_chunk_log(uint32_t n);                              // parse.hip: klog for n
 int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap,
                size_t *out_len);                                   // emit.hip -> dst
 

@@ -2,13 +2,14 @@
 //
 // The reference runs one backward min-plus pass: cost[p] = min(9 + cost[p+1],
 // w(PSV) + cost[p+lenP], w(NSV) + cost[p+lenN]) in 32-bit signed arithmetic, strict '<',
-// candidate order literal, PSV, NSV. Here the text is cut into chunks of kChunk positions,
-// one lane per chunk, and the pass is iterated to a fixed point:
+// candidate order literal, PSV, NSV. Here the text is cut into chunks of K = 2^klog
+// positions, one lane per chunk, and the pass is iterated to a fixed point:
 //
 //   1. every chunk runs the backward pass over its own positions, reading the previous
 //      iteration's exact costs for targets beyond its end; per position it records the
-//      decision, the first position at or past the chunk end its path reaches (its exit)
-//      and the bit sum along the way;
+//      decision, the chunk-local cost estimate and the first position at or past the chunk
+//      end its path reaches (its exit). The estimate is (bits along the path to the exit)
+//      + (previous cost at the exit), so the in-chunk bit sum is estimate - cin[exit];
 //   2. exact costs of the new decisions: exit targets E form a forest rooted at n; pointer
 //      jumping over the compacted E gives their path sums, every other position adds its
 //      in-chunk sum to its exit's cost;
@@ -16,17 +17,18 @@
 //      the reference's tie order, over exact successor costs, so by backward induction from
 //      n it is the reference's decision (DESIGN.md "Parse").
 //
+// All per-position arrays (candidates, choices, costs, state) use the chunk-interleaved
+// layout of common.hpp: the 64 lanes of a wave walk 64 neighbouring chunks in lockstep, so
+// the streaming loads and stores of one step are one contiguous run per wave.
 // The pointer-jumping snapshots of the final E forest are kept for emission's path marking.
 #include "internal.hpp"
 
 #include <cstdlib>
-#include <vector>
 
 namespace salz {
 namespace {
 
 constexpr int kT = 256;
-constexpr uint32_t kChunk = 512;
 
 // vnibble_size (lib/salz.c:565-588)
 __device__ __forceinline__ uint32_t vn_size(uint32_t v)
@@ -51,81 +53,109 @@ __device__ __forceinline__ uint32_t factor_bits(uint32_t off, uint32_t len)
     return 1u + 8u + 4u * vn_size((off - 1u) >> 8) + ((len - 3u) >> 3) + 4u;
 }
 
-__global__ __launch_bounds__(kT) void k_cost_seed(uint32_t *cost, uint32_t n)
+// Storage slots 0..S-1 -> cost seed 9 * (n - p) (all literals); slots past n unused.
+__global__ __launch_bounds__(kT) void k_cost_seed(uint32_t *cost, uint32_t n, uint32_t klog,
+                                                  size_t S)
 {
-    size_t q = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (q <= n)
-        cost[q] = 9u * (n - (uint32_t)q);
+    size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (s >= S)
+        return;
+    uint64_t p = spos(s, klog);
+    if (p <= n)
+        cost[s] = 9u * (n - (uint32_t)p);
 }
 
 __global__ __launch_bounds__(kT) void k_parse_chunk(
-    const uint4 *__restrict__ cand, const uint32_t *__restrict__ cin, uint32_t *cloc,
-    const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t *ex, uint32_t *sm,
-    uint32_t n, uint32_t *__restrict__ changed)
+    const uint4 *__restrict__ cand, const uint32_t *__restrict__ cin, uint64_t *__restrict__ pst,
+    const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, uint32_t klog,
+    uint32_t *__restrict__ changed)
 {
-    size_t g = (size_t)blockIdx.x * kT + threadIdx.x;
-    size_t a64 = g * kChunk;
-    if (a64 >= n)
-        return;
-    const uint32_t a = (uint32_t)a64;
-    const uint32_t b = (n - a) < kChunk ? n : a + kChunk;
+    const uint32_t c = blockIdx.x * kT + threadIdx.x;  // chunk
+    const uint64_t a64 = (uint64_t)c << klog;
     uint32_t diff = 0;
-    for (uint32_t p = b; p-- > a;) {
-        uint32_t nx1 = p + 1;
-        uint32_t best = 9u + (nx1 >= b ? cin[nx1] : cloc[nx1]);
-        uint32_t len = 1, w = 9;
-        uint8_t ch = 0;
-        if (p != 0) {
-            const uint4 c = cand[p];
-            if (c.y >= 3u) {
-                uint32_t wf = factor_bits(c.x, c.y), q = p + c.y;
-                uint32_t alt = wf + (q >= b ? cin[q] : cloc[q]);
-                if ((int32_t)alt < (int32_t)best) {
-                    best = alt;
-                    len = c.y;
-                    w = wf;
-                    ch = 1;
+    if (a64 < n) {
+        const uint32_t a = (uint32_t)a64;
+        const uint32_t K = 1u << klog;
+        const uint32_t b = (n - a) < K ? n : a + K;
+        const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
+        // state of p + 1: cost estimate and exit (p = b - 1 starts at the exit b)
+        uint32_t nc = cin[sidx(b, klog)], nex = b;
+        uint32_t j = b - a;
+        uint4 cn = cand[base + ((size_t)(j - 1) << 6)];
+        uint8_t on = chold[base + ((size_t)(j - 1) << 6)];
+        while (j-- > 0) {
+            const uint32_t p = a + j;
+            const size_t s = base + ((size_t)j << 6);
+            const uint4 cd = cn;
+            const uint8_t old = on;
+            if (j) {
+                cn = cand[s - 64];
+                on = chold[s - 64];
+            }
+            uint32_t best = 9u + nc, ex = nex;
+            uint8_t ch = 0;
+            if (p != 0) {
+                const bool fP = cd.y >= 3u, fN = cd.w >= 3u;
+                const uint32_t qP = p + cd.y, qN = p + cd.w;
+                // target state (cost estimate << 32 | exit): in-chunk from pst, else exit itself
+                uint64_t vP = 0, vN = 0;
+                if (fP)
+                    vP = qP < b ? pst[base + ((size_t)(qP - a) << 6)]
+                                : ((uint64_t)cin[sidx(qP, klog)] << 32) | qP;
+                if (fN)
+                    vN = qN < b ? pst[base + ((size_t)(qN - a) << 6)]
+                                : ((uint64_t)cin[sidx(qN, klog)] << 32) | qN;
+                const uint32_t cP = (uint32_t)(vP >> 32), eP = (uint32_t)vP;
+                const uint32_t cN = (uint32_t)(vN >> 32), eN = (uint32_t)vN;
+                if (fP) {
+                    const uint32_t alt = factor_bits(cd.x, cd.y) + cP;
+                    if ((int32_t)alt < (int32_t)best) {
+                        best = alt;
+                        ex = eP;
+                        ch = 1;
+                    }
+                }
+                if (fN) {
+                    const uint32_t alt = factor_bits(cd.z, cd.w) + cN;
+                    if ((int32_t)alt < (int32_t)best) {
+                        best = alt;
+                        ex = eN;
+                        ch = 2;
+                    }
                 }
             }
-            if (c.w >= 3u) {
-                uint32_t wf = factor_bits(c.z, c.w), q = p + c.w;
-                uint32_t alt = wf + (q >= b ? cin[q] : cloc[q]);
-                if ((int32_t)alt < (int32_t)best) {
-                    best = alt;
-                    len = c.w;
-                    w = wf;
-                    ch = 2;
-                }
-            }
+            pst[s] = ((uint64_t)best << 32) | ex;
+            chnew[s] = ch;
+            diff += ch != old;
+            nc = best;
+            nex = ex;
         }
-        uint32_t nx = p + len;
-        if (nx >= b) {
-            ex[p] = nx;
-            sm[p] = w;
-        } else {
-            ex[p] = ex[nx];
-            sm[p] = w + sm[nx];
-        }
-        cloc[p] = best;
-        chnew[p] = ch;
-        diff += ch != chold[p];
     }
-    if (diff)
+    // one atomic per wave
+    for (int m = 32; m >= 1; m >>= 1)
+        diff += shfl_xor_u32(diff, m);
+    if (lane_id() == 0 && diff)
         atomicAdd(changed, diff);
 }
 
-__global__ void k_mark_exits(const uint32_t *__restrict__ ex, uint32_t n, uint32_t *eflag)
+// eflag[exit(p)] = 1 for every position, and for n (the root).
+__global__ void k_mark_exits(const uint64_t *__restrict__ pst, uint32_t n, uint32_t klog, size_t S,
+                             uint32_t *eflag)
 {
-    size_t p = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (p < n)
-        eflag[ex[p]] = 1u;
-    if (p == 0)
+    size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (s >= S)
+        return;
+    if (spos(s, klog) < n)
+        eflag[(uint32_t)pst[s]] = 1u;
+    if (s == 0)
         eflag[n] = 1u;
 }
 
+// Compact E: node x = eidx[q] for exit position q; parent = exit of q, weight = in-chunk
+// bit sum of q's path (estimate - cin[exit]).
 __global__ void k_compact_exits(const uint32_t *__restrict__ eflag,
-                                const uint32_t *__restrict__ eidx, const uint32_t *__restrict__ ex,
-                                const uint32_t *__restrict__ sm, uint32_t n,
+                                const uint32_t *__restrict__ eidx, const uint64_t *__restrict__ pst,
+                                const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog,
                                 uint32_t *__restrict__ elist, uint32_t *__restrict__ jt0,
                                 uint32_t *__restrict__ js)
 {
@@ -138,8 +168,10 @@ __global__ void k_compact_exits(const uint32_t *__restrict__ eflag,
         jt0[x] = x;
         js[x] = 0;
     } else {
-        jt0[x] = eidx[ex[q]];
-        js[x] = sm[q];
+        const uint64_t v = pst[sidx((uint32_t)q, klog)];
+        const uint32_t e = (uint32_t)v;
+        jt0[x] = eidx[e];
+        js[x] = (uint32_t)(v >> 32) - cin[sidx(e, klog)];
     }
 }
 
@@ -155,117 +187,62 @@ __global__ void k_jump(const uint32_t *__restrict__ jt, const uint32_t *__restri
 }
 
 __global__ void k_cost_exits(const uint32_t *__restrict__ elist, const uint32_t *__restrict__ js,
-                             uint32_t ne, uint32_t *__restrict__ cost)
+                             uint32_t ne, uint32_t klog, uint32_t *__restrict__ cost)
 {
     uint32_t x = blockIdx.x * kT + threadIdx.x;
     if (x < ne)
-        cost[elist[x]] = js[x];
+        cost[sidx(elist[x], klog)] = js[x];
 }
 
-__global__ void k_cost_rest(const uint32_t *__restrict__ eflag, const uint32_t *__restrict__ ex,
-                            const uint32_t *__restrict__ sm, uint32_t n, uint32_t *cost)
+// cost[p] = (in-chunk sum) + cost[exit] for every position that is not itself an exit.
+__global__ void k_cost_rest(const uint32_t *__restrict__ eflag, const uint64_t *__restrict__ pst,
+                            const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog, size_t S,
+                            uint32_t *cost)
 {
-    size_t p = (size_t)blockIdx.x * kT + threadIdx.x;
+    size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (s >= S)
+        return;
+    const uint64_t p = spos(s, klog);
     if (p >= n || eflag[p])
         return;
-    cost[p] = sm[p] + cost[ex[p]];
-}
-
-static uint32_t host_vn_size(uint32_t v)
-{
-    static const uint32_t lim[10] = {8u, 72u, 584u, 4680u, 37448u, 299592u, 2396744u,
-                                     19173960u, 153391688u, 1227133512u};
-    uint32_t k = 1;
-    for (int i = 0; i < 10; i++)
-        k += v >= lim[i];
-    return k;
-}
-
-// SALZ_DEBUG_CHECK: verify the exit forest and exact costs of one iteration on the host.
-static void debug_check(Workspace &ws, uint32_t n, const uint8_t *dchoice, const uint32_t *dcost,
-                        const uint32_t *dex, const uint32_t *dsm, const uint32_t *deflag,
-                        const uint32_t *deidx, uint32_t ne, int it)
-{
-    hipStream_t st = ws.stream;
-    (void)hipStreamSynchronize(st);
-    std::vector<uint8_t> ch(n);
-    std::vector<uint32_t> cost(n + 1), ex(n), sm(n), ef(n + 1), ei(n + 1);
-    std::vector<uint4> cand(n);
-    (void)hipMemcpy(ch.data(), dchoice, n, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(cost.data(), dcost, 4ull * (n + 1), hipMemcpyDeviceToHost);
-    (void)hipMemcpy(ex.data(), dex, 4ull * n, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(sm.data(), dsm, 4ull * n, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(ef.data(), deflag, 4ull * (n + 1), hipMemcpyDeviceToHost);
-    (void)hipMemcpy(ei.data(), deidx, 4ull * (n + 1), hipMemcpyDeviceToHost);
-    (void)hipMemcpy(cand.data(), ws.cand, 16ull * n, hipMemcpyDeviceToHost);
-    auto tok = [&](uint32_t p, uint32_t &len, uint32_t &w) {
-        len = 1;
-        w = 9;
-        if (p == 0 || ch[p] == 0)
-            return;
-        uint4 c = cand[p];
-        uint32_t off = ch[p] == 1 ? c.x : c.z;
-        len = ch[p] == 1 ? c.y : c.w;
-        w = 1u + 8u + 4u * host_vn_size((off - 1u) >> 8) + ((len - 3u) >> 3) + 4u;
-    };
-    long bad_len = 0, bad_ex = 0, bad_flag = 0, bad_idx = 0, bad_cost = 0;
-    std::vector<uint32_t> hc(n + 1);
-    hc[n] = 0;
-    for (uint32_t p = n; p-- > 0;) {
-        uint32_t len, w;
-        tok(p, len, w);
-        if ((uint64_t)p + len > n) {
-            if (!bad_len++)
-                fprintf(stderr, "check it=%d: p=%u len=%u beyond n\n", it, p, len);
-            hc[p] = 0;
-            continue;
-        }
-        hc[p] = w + hc[p + len];
-    }
-    std::vector<uint32_t> hflag(n + 1, 0);
-    for (uint32_t p = 0; p < n; p++) {
-        uint32_t b = (p / kChunk) * kChunk + kChunk;
-        if (b > n)
-            b = n;
-        uint32_t q = p, s = 0, len, w;
-        while (q < b) {
-            tok(q, len, w);
-            s += w;
-            q += len;
-        }
-        if (ex[p] != q || sm[p] != s)
-            if (!bad_ex++)
-                fprintf(stderr, "check it=%d: p=%u ex %u/%u sm %u/%u\n", it, p, ex[p], q, sm[p], s);
-        if (q <= n)
-            hflag[q] = 1;
-    }
-    hflag[n] = 1;
-    uint32_t run = 0;
-    for (uint32_t q = 0; q <= n; q++) {
-        if (hflag[q] != ef[q] && !bad_flag++)
-            fprintf(stderr, "check it=%d: eflag[%u] dev %u host %u\n", it, q, ef[q], hflag[q]);
-        if (ei[q] != run && !bad_idx++)
-            fprintf(stderr, "check it=%d: eidx[%u] dev %u host %u\n", it, q, ei[q], run);
-        run += ef[q];
-    }
-    for (uint32_t p = 0; p <= n; p++)
-        if (hc[p] != cost[p] && p > 0 && !bad_cost++)
-            fprintf(stderr, "check it=%d: cost[%u] dev %u host %u\n", it, p, cost[p], hc[p]);
-    fprintf(stderr, "check it=%d ne=%u host_ne=%u bad: len %ld ex %ld flag %ld idx %ld cost %ld\n", it,
-            ne, run, bad_len, bad_ex, bad_flag, bad_idx, bad_cost);
+    const uint64_t v = pst[s];
+    const size_t se = sidx((uint32_t)v, klog);
+    cost[s] = (uint32_t)(v >> 32) - cin[se] + cost[se];
 }
 
 }  // namespace
+
+// Chunk length: the largest K <= 512 that still gives every SIMD of the chip a few waves
+// (parse lanes = chunks); small blocks get short chunks.
+uint32_t parse_chunk_log(uint32_t n)
+{
+    if (const char *e = getenv("SALZ_PARSE_KLOG")) {  // tests: force a chunk length
+        int k = atoi(e);
+        if (k >= 6 && k <= (int)kMaxChunkLog)
+            return (uint32_t)k;
+    }
+    uint32_t klog = kMaxChunkLog;
+    while (klog > 6 && ((uint64_t)n >> klog) < (1u << 17))
+        klog--;
+    return klog;
+}
 
 int stage_parse(Workspace &ws, uint32_t n)
 {
     hipStream_t st = ws.stream;
     ParseState &ps = ws.parse;
-    ps.chunk = kChunk;
-    ps.nchunks = (n + kChunk - 1) / kChunk;
+    const uint32_t klog = ws.klog;
+    ps.chunk = 1u << klog;
+    ps.nchunks = (n + ps.chunk - 1) / ps.chunk;
+    const size_t tile = (size_t)kTileChunks << klog;
+    const size_t S = ((size_t)n + 1 + tile - 1) / tile * tile;  // slots covering 0..n
+    if (S > ws.cap_s) {
+        set_error("parse: layout exceeds workspace (%zu > %zu)", S, ws.cap_s);
+        return -1;
+    }
     uint32_t *cost[2] = {ws.u0, ws.u1};
     uint8_t *choice[2] = {reinterpret_cast<uint8_t *>(ws.valA), reinterpret_cast<uint8_t *>(ws.valB)};
-    uint32_t *ex = ws.u2, *sm = ws.u3, *eflag = ws.offA, *eidx = ws.offB;
+    uint32_t *eflag = ws.offA, *eidx = ws.offB;
     uint32_t *elist = ws.rank;
     uint32_t *js[2] = {reinterpret_cast<uint32_t *>(ws.keyA),
                        reinterpret_cast<uint32_t *>(ws.keyA) + (ws.cap_n + 1)};
@@ -273,11 +250,13 @@ int stage_parse(Workspace &ws, uint32_t n)
     const size_t snap_cap = 2 * (ws.cap_n + 1);
     uint32_t *changed = reinterpret_cast<uint32_t *>(ws.dscal) + 48;
     uint32_t *etotal = reinterpret_cast<uint32_t *>(ws.dscal) + 49;
+    static const bool verbose = getenv("SALZ_DEBUG_PARSE") != nullptr;
 
-    hipLaunchKernelGGL(k_cost_seed, dim3(grid_for((size_t)n + 1, kT)), dim3(kT), 0, st, cost[0], n);
+    hipLaunchKernelGGL(k_cost_seed, dim3(grid_for(S, kT)), dim3(kT), 0, st, cost[0], n, klog, S);
     SALZ_LAUNCH_CHECK();
-    SALZ_HIP(hipMemsetAsync(choice[0], 0xff, n, st));
+    SALZ_HIP(hipMemsetAsync(choice[0], 0xff, S, st));
 
+    ps.pst = ws.pst;
     ps.n_exit = 0;
     ps.levels = 0;
     int it = 0;
@@ -287,13 +266,13 @@ int stage_parse(Workspace &ws, uint32_t n)
         uint8_t *chold = choice[cur], *chnew = choice[cur ^ 1];
         SALZ_HIP(hipMemsetAsync(changed, 0, 4, st));
         hipLaunchKernelGGL(k_parse_chunk, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
-                           cin, cout, chold, chnew, ex, sm, n, changed);
+                           cin, ws.pst, chold, chnew, n, klog, changed);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 256, "parse.changed") != 0)
             return -1;
         const uint32_t nchanged = reinterpret_cast<uint32_t *>(ws.hscal)[48];
-        if (getenv("SALZ_DEBUG_PARSE"))
-            fprintf(stderr, "parse it=%d changed=%u\n", it, nchanged);
+        if (verbose)
+            fprintf(stderr, "parse it=%d K=%u changed=%u\n", it, ps.chunk, nchanged);
         if (nchanged == 0) {
             ps.choice = chnew;
             ps.cost = cin;
@@ -305,22 +284,21 @@ int stage_parse(Workspace &ws, uint32_t n)
         }
         // Exact costs for the new decisions.
         SALZ_HIP(hipMemsetAsync(eflag, 0, sizeof(uint32_t) * ((size_t)n + 1), st));
-        hipLaunchKernelGGL(k_mark_exits, dim3(grid_for(n, kT)), dim3(kT), 0, st, ex, n, eflag);
+        hipLaunchKernelGGL(k_mark_exits, dim3(grid_for(S, kT)), dim3(kT), 0, st, ws.pst, n, klog, S,
+                           eflag);
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u32(eflag, eidx, (size_t)n + 1, false, etotal, ws, st) != 0)
             return -1;
         if (read_scalars(ws, 0, 256, "parse.ne") != 0)
             return -1;
         const uint32_t ne = reinterpret_cast<uint32_t *>(ws.hscal)[49];
-        if (getenv("SALZ_DEBUG_PARSE"))
-            fprintf(stderr, "parse it=%d exits=%u\n", it, ne);
         const uint32_t K = (uint32_t)bit_width(ne > 1 ? ne - 1 : 0);
         if ((size_t)(K + 1) * ne > snap_cap) {
             set_error("parse: exit forest too large for snapshot area (|E|=%u)", ne);
             return -1;
         }
         hipLaunchKernelGGL(k_compact_exits, dim3(grid_for((size_t)n + 1, kT)), dim3(kT), 0, st,
-                           eflag, eidx, ex, sm, n, elist, snap, js[0]);
+                           eflag, eidx, ws.pst, cin, n, klog, elist, snap, js[0]);
         SALZ_LAUNCH_CHECK();
         int jc = 0;
         for (uint32_t k = 0; k < K; k++) {
@@ -330,21 +308,16 @@ int stage_parse(Workspace &ws, uint32_t n)
             jc ^= 1;
         }
         hipLaunchKernelGGL(k_cost_exits, dim3(grid_for(ne, kT)), dim3(kT), 0, st, elist, js[jc], ne,
-                           cout);
+                           klog, cout);
         SALZ_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(n, kT)), dim3(kT), 0, st, eflag, ex, sm, n,
-                           cout);
+        hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(S, kT)), dim3(kT), 0, st, eflag, ws.pst, cin, n,
+                           klog, S, cout);
         SALZ_LAUNCH_CHECK();
-        static const bool check = getenv("SALZ_DEBUG_CHECK") != nullptr;
-        if (check && (it == 1 || it == 5))
-            debug_check(ws, n, chnew, cout, ex, sm, eflag, eidx, ne, it);
         ps.n_exit = ne;
         ps.levels = K;
         ps.elist = elist;
         ps.jt0 = snap;
     }
-    ps.ex = ex;
-    ps.sm = sm;
     ws.stats.parse_iters = it + 1;
     ws.stats.exit_nodes = ps.n_exit;
     return 0;

@@ -51,7 +51,7 @@ void workspace_free(Workspace &ws)
         (void)hipSetDevice(ws.device);
     void *ptrs[] = {ws.text, ws.rank,     ws.sa,   ws.keyA, ws.keyB, ws.valA, ws.valB,
                     ws.u0,   ws.u1,       ws.u2,   ws.u3,   ws.g64,  ws.offA, ws.offB,
-                    ws.cand, ws.out,      ws.radix_counts,  ws.scan_tmp,      ws.dscal};
+                    ws.cand, ws.pst, ws.out, ws.radix_counts,  ws.scan_tmp,      ws.dscal};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -80,7 +80,9 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
     ws.np2 = 2048;
     while (ws.np2 < ws.cap_n)
         ws.np2 <<= 1;
-    const size_t n1 = ws.cap_n + 2;
+    // Every per-position array has room for the interleaved layout of positions 0..cap_n.
+    ws.cap_s = (ws.cap_n + 1 + kLayoutPad - 1) / kLayoutPad * kLayoutPad;
+    const size_t n1 = ws.cap_s > ws.cap_n + 2 ? ws.cap_s : ws.cap_n + 2;
     const size_t ntiles = (ws.cap_n + kRadixTile - 1) / kRadixTile;
     ws.radix_counts_elems = 256 * ntiles + 256;
     ws.out_cap = out_bound(N);
@@ -90,7 +92,7 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
         dalloc(&ws.keyA, n1) || dalloc(&ws.keyB, n1) || dalloc(&ws.valA, n1) ||
         dalloc(&ws.valB, n1) || dalloc(&ws.u0, n1) || dalloc(&ws.u1, n1) || dalloc(&ws.u2, n1) ||
         dalloc(&ws.u3, n1) || dalloc(&ws.g64, n1) || dalloc(&ws.offA, n1) ||
-        dalloc(&ws.offB, n1) || dalloc(&ws.cand, ws.cap_n + 1) || dalloc(&ws.out, ws.out_cap) ||
+        dalloc(&ws.offB, n1) || dalloc(&ws.cand, ws.cap_s) || dalloc(&ws.pst, ws.cap_s) || dalloc(&ws.out, ws.out_cap) ||
         dalloc(&ws.radix_counts, ws.radix_counts_elems) ||
         dalloc(reinterpret_cast<uint8_t **>(&ws.scan_tmp), ws.scan_tmp_bytes) ||
         dalloc(&ws.dscal, 1024)) {
@@ -118,21 +120,6 @@ int read_scalars(Workspace &ws, size_t off, size_t bytes, const char *tag)
     const uint8_t *d = reinterpret_cast<const uint8_t *>(ws.dscal) + off;
     SALZ_HIP(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ws.stream));
     SALZ_HIP(hipStreamSynchronize(ws.stream));
-    static const bool verify = getenv("SALZ_DEBUG_SCALARS") != nullptr;
-    if (verify) {
-        uint8_t chk[512];
-        SALZ_HIP(hipDeviceSynchronize());
-        SALZ_HIP(hipMemcpy(chk, d, bytes, hipMemcpyDeviceToHost));
-        if (memcmp(chk, h, bytes) != 0) {
-            for (size_t i = 0; i + 4 <= bytes; i += 4) {
-                uint32_t a, b;
-                memcpy(&a, h + i, 4);
-                memcpy(&b, chk + i, 4);
-                if (a != b)
-                    fprintf(stderr, "STALE %s: word %zu async %u sync %u\n", tag, (off + i) / 4, a, b);
-            }
-        }
-    }
     return 0;
 }
 
@@ -170,26 +157,30 @@ static int dump_after_parse(Workspace &ws, uint32_t n, const salz_gpu_dump *d)
 {
     if (!d || !(d->psv || d->nsv || d->lp || d->ln || d->dlen || d->doff || d->cost))
         return 0;
-    std::vector<uint4> cand(n);
-    std::vector<uint8_t> choice(n);
-    std::vector<uint32_t> cost((size_t)n + 1);
-    SALZ_HIP(hipMemcpyAsync(cand.data(), ws.cand, sizeof(uint4) * n, hipMemcpyDeviceToHost,
+    // the parse arrays are chunk-interleaved (common.hpp): copy the slots, index by sidx
+    const size_t tile = (size_t)kTileChunks << ws.klog;
+    const size_t S = ((size_t)n + 1 + tile - 1) / tile * tile;
+    std::vector<uint4> cand(S);
+    std::vector<uint8_t> choice(S);
+    std::vector<uint32_t> cost(S);
+    SALZ_HIP(hipMemcpyAsync(cand.data(), ws.cand, sizeof(uint4) * S, hipMemcpyDeviceToHost,
                             ws.stream));
-    SALZ_HIP(hipMemcpyAsync(choice.data(), ws.parse.choice, n, hipMemcpyDeviceToHost, ws.stream));
-    SALZ_HIP(hipMemcpyAsync(cost.data(), ws.parse.cost, sizeof(uint32_t) * ((size_t)n + 1),
+    SALZ_HIP(hipMemcpyAsync(choice.data(), ws.parse.choice, S, hipMemcpyDeviceToHost, ws.stream));
+    SALZ_HIP(hipMemcpyAsync(cost.data(), ws.parse.cost, sizeof(uint32_t) * S,
                             hipMemcpyDeviceToHost, ws.stream));
     SALZ_HIP(hipStreamSynchronize(ws.stream));
     for (uint32_t p = 0; p < n; p++) {
-        const uint4 c = cand[p];
+        const size_t s = sidx(p, ws.klog);
+        const uint4 c = cand[s];
         if (d->psv) d->psv[p] = (int32_t)(p - c.x);
         if (d->lp) d->lp[p] = (int32_t)c.y;
         if (d->nsv) d->nsv[p] = (int32_t)(p - c.z);
         if (d->ln) d->ln[p] = (int32_t)c.w;
         int32_t len = 1, off = 0;
-        if (choice[p] == 1) {
+        if (choice[s] == 1) {
             len = (int32_t)c.y;
             off = (int32_t)c.x;
-        } else if (choice[p] == 2) {
+        } else if (choice[s] == 2) {
             len = (int32_t)c.w;
             off = (int32_t)c.z;
         }
@@ -198,100 +189,8 @@ static int dump_after_parse(Workspace &ws, uint32_t n, const salz_gpu_dump *d)
     }
     if (d->cost)
         for (size_t q = 0; q <= n; q++)
-            d->cost[q] = (int32_t)cost[q];
+            d->cost[q] = (int32_t)cost[sidx((uint32_t)q, ws.klog)];
     return 0;
-}
-
-// SALZ_DEBUG_HASH=1: checksum each stage's output on the host (diagnostics only).
-static void debug_hash(Workspace &ws, const char *what, const void *dptr, size_t bytes)
-{
-    static const bool on = getenv("SALZ_DEBUG_HASH") != nullptr;
-    if (!on)
-        return;
-    std::vector<uint8_t> h(bytes);
-    (void)hipStreamSynchronize(ws.stream);
-    (void)hipMemcpy(h.data(), dptr, bytes, hipMemcpyDeviceToHost);
-    uint64_t x = 1469598103934665603ull;
-    for (size_t i = 0; i < bytes; i++)
-        x = (x ^ h[i]) * 1099511628211ull;
-    fprintf(stderr, "hash %-8s %016llx\n", what, (unsigned long long)x);
-}
-
-// Device-side diagnostics (no host sync): text checksum and 8-byte order of the SA.
-__global__ void k_dbg_text_sum(const uint8_t *T, size_t N, unsigned long long *out)
-{
-    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < N)
-        atomicAdd(out, (unsigned long long)T[i] * (unsigned long long)(i % 65521 + 1));
-}
-
-__global__ void k_dbg_sa_order(const uint8_t *T, const uint32_t *sa, uint32_t n, unsigned int *bad)
-{
-    size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (r == 0 || r >= n)
-        return;
-    uint32_t a = sa[r - 1], b = sa[r];
-    uint64_t ka = load_u64_any(T, a), kb = load_u64_any(T, b);
-    uint32_t la = n - a, lb = n - b;
-    if (la < 8) ka &= (1ull << (8 * la)) - 1;
-    if (lb < 8) kb &= (1ull << (8 * lb)) - 1;
-    ka = __builtin_bswap64(ka);
-    kb = __builtin_bswap64(kb);
-    if (ka > kb || (ka == kb && la < 8 && lb < 8 && la > lb))
-        atomicAdd(bad, 1u);
-}
-
-// SALZ_DEBUG_CAND=1: validate candidates after ANSV; on a bad one, cross-check SA / LCP.
-static void debug_cand(Workspace &ws, uint32_t n)
-{
-    static const bool on = getenv("SALZ_DEBUG_CAND") != nullptr;
-    if (!on)
-        return;
-    (void)hipStreamSynchronize(ws.stream);
-    std::vector<uint4> cand(n);
-    (void)hipMemcpy(cand.data(), ws.cand, 16ull * n, hipMemcpyDeviceToHost);
-    long bad = 0;
-    uint32_t first = 0;
-    for (uint32_t p = 1; p < n; p++) {
-        uint4 c = cand[p];
-        bool ok = c.y <= n - p && c.w <= n - p && c.x >= 1 && c.x <= p + 1 && c.z >= 1 &&
-                  c.z <= p + 1;
-        if (!ok && !bad++)
-            first = p;
-    }
-    fprintf(stderr, "cand check: %ld bad\n", bad);
-    if (!bad)
-        return;
-    std::vector<uint32_t> sa(n), lcp(n), isa(n);
-    std::vector<uint8_t> T(n + 8);
-    (void)hipMemcpy(sa.data(), ws.sa, 4ull * n, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(lcp.data(), ws.u3, 4ull * n, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(T.data(), ws.text, n + 8, hipMemcpyDeviceToHost);
-    std::vector<uint8_t> seen(n, 0);
-    long dup = 0;
-    for (uint32_t r = 0; r < n; r++) {
-        if (sa[r] >= n || seen[sa[r]]++) dup++;
-        else isa[sa[r]] = r;
-    }
-    fprintf(stderr, "sa: %ld invalid/duplicate entries\n", dup);
-    // Kasai LCP from the GPU SA, and an order check of adjacent suffixes
-    long bad_lcp = 0, bad_order = 0;
-    uint32_t h = 0;
-    for (uint32_t i = 0; i < n && !dup; i++) {
-        uint32_t r = isa[i];
-        if (r == 0) { h = 0; continue; }
-        uint32_t j = sa[r - 1];
-        while (i + h < n && j + h < n && T[i + h] == T[j + h]) h++;
-        bool ordered = (j + h == n) || (i + h < n && T[j + h] < T[i + h]);
-        if (!ordered && !bad_order++)
-            fprintf(stderr, "order: rank %u (pos %u) before rank %u (pos %u) wrong\n", r - 1, j, r, i);
-        if (lcp[r] != h && !bad_lcp++)
-            fprintf(stderr, "lcp[%u] (pos %u) gpu %u host %u\n", r, i, lcp[r], h);
-        if (h) h--;
-    }
-    uint4 c = cand[first];
-    fprintf(stderr, "first bad cand p=%u rank %u: {%u %u %u %u}; lcp bad %ld order bad %ld\n", first,
-            dup ? 0 : isa[first], c.x, c.y, c.z, c.w, bad_lcp, bad_order);
 }
 
 // Encode one block. src is host or device memory; the stream goes to device buffer dst.
@@ -313,53 +212,24 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t N
     ws.rx_used = 0;
 
     if (mark(ws, EV_START)) return -1;
-    static const bool dev_check = getenv("SALZ_DEBUG_DEVICE") != nullptr;
     SALZ_HIP(hipMemcpyAsync(ws.text, src, N, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                             st));
-    unsigned long long *dsum = reinterpret_cast<unsigned long long *>(ws.dscal) + 200;
-    unsigned int *dbad = reinterpret_cast<unsigned int *>(ws.dscal) + 420;
-    if (dev_check) {
-        SALZ_HIP(hipMemsetAsync(dsum, 0, 8, st));
-        SALZ_HIP(hipMemsetAsync(dbad, 0, 4, st));
-        hipLaunchKernelGGL(k_dbg_text_sum, dim3(grid_for(N, 256)), dim3(256), 0, st, ws.text, N, dsum);
-    }
     SALZ_HIP(hipMemsetAsync(ws.text + N, 0, 128, st));
+    ws.klog = parse_chunk_log(n);
     if (mark(ws, EV_UP)) return -1;
     if (stage_suffix_array(ws, n)) return -1;
     if (mark(ws, EV_SA)) return -1;
-    debug_hash(ws, "text", ws.text, N);
-    if (dev_check)
-        hipLaunchKernelGGL(k_dbg_sa_order, dim3(grid_for(n, 256)), dim3(256), 0, st, ws.text, ws.sa, n,
-                           dbad);
-    debug_hash(ws, "sa", ws.sa, sizeof(uint32_t) * n);
     if (dump_after_sa(ws, n, dump)) return -1;
     if (stage_lcp(ws, n, ws.u3)) return -1;
     if (mark(ws, EV_LCP)) return -1;
-    debug_hash(ws, "lcp", ws.u3, sizeof(uint32_t) * n);
     if (stage_candidates(ws, n, ws.u3)) return -1;
     if (mark(ws, EV_ANSV)) return -1;
-    debug_hash(ws, "cand", ws.cand, sizeof(uint4) * n);
-    debug_cand(ws, n);
     if (stage_parse(ws, n)) return -1;
     if (mark(ws, EV_PARSE)) return -1;
-    debug_hash(ws, "choice", ws.parse.choice, n);
-    debug_hash(ws, "cost", ws.parse.cost, sizeof(uint32_t) * ((size_t)n + 1));
     if (dump_after_parse(ws, n, dump)) return -1;
     if (stage_emit(ws, n, (uint32_t)N, dst, cap, out_len)) return -1;
     if (mark(ws, EV_EMIT)) return -1;
     SALZ_HIP(hipStreamSynchronize(st));
-    if (dev_check) {
-        unsigned long long s = 0;
-        unsigned int b = 0;
-        SALZ_HIP(hipMemcpy(&s, dsum, 8, hipMemcpyDeviceToHost));
-        SALZ_HIP(hipMemcpy(&b, dbad, 4, hipMemcpyDeviceToHost));
-        unsigned long long hs = 0;
-        if (!src_dev) {
-            for (size_t i = 0; i < N; i++)
-                hs += (unsigned long long)src[i] * (unsigned long long)(i % 65521 + 1);
-        }
-        fprintf(stderr, "devcheck: text_sum %llx host %llx sa_order_bad %u\n", s, hs, b);
-    }
     if (ws.timing) {
         ws.stats.ms_upload = elapsed(ws, EV_START, EV_UP);
         ws.stats.ms_sa = elapsed(ws, EV_UP, EV_SA);

@@ -153,48 +153,11 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
 
 }  // namespace
 
-static uint64_t pair_hash(uint64_t k, uint32_t v)
-{
-    uint64_t x = k * 0x9E3779B97F4A7C15ull ^ ((uint64_t)v * 0xC2B2AE3D27D4EB4Full);
-    x ^= x >> 29;
-    return x * 0xBF58476D1CE4E5B9ull;
-}
-
-// SALZ_DEBUG_RADIX: host check of one sort (sorted on [lo,hi), same multiset of pairs).
-static void debug_radix(const uint64_t *dk, const uint32_t *dv, uint32_t m, int lo, int hi,
-                        hipStream_t st, uint64_t *sum_in, bool after)
-{
-    (void)hipStreamSynchronize(st);
-    std::vector<uint64_t> k(m);
-    std::vector<uint32_t> v(m);
-    (void)hipMemcpy(k.data(), dk, 8ull * m, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(v.data(), dv, 4ull * m, hipMemcpyDeviceToHost);
-    uint64_t s = 0;
-    for (uint32_t i = 0; i < m; i++)
-        s += pair_hash(k[i], v[i]);
-    if (!after) {
-        *sum_in = s;
-        return;
-    }
-    uint64_t mask = (hi >= 64 ? ~0ull : ((1ull << hi) - 1)) & ~((1ull << lo) - 1);
-    long unsorted = 0;
-    for (uint32_t i = 1; i < m; i++)
-        if ((k[i - 1] & mask) > (k[i] & mask) && !unsorted++)
-            fprintf(stderr, "RADIX unsorted at %u of %u bits [%d,%d)\n", i, m, lo, hi);
-    if (s != *sum_in || unsorted)
-        fprintf(stderr, "RADIX BAD m=%u bits [%d,%d): unsorted %ld multiset %s\n", m, lo, hi,
-                unsorted, s == *sum_in ? "ok" : "CHANGED");
-}
-
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st)
 {
     if (m <= 1 || bit_hi <= bit_lo)
         return 0;
-    static const bool dbg = getenv("SALZ_DEBUG_RADIX") != nullptr;
-    uint64_t dsum = 0;
-    if (dbg)
-        debug_radix(*keys, *vals, m, bit_lo, bit_hi, st, &dsum, false);
     uint32_t ntiles = (m + kTile - 1) / kTile;
     size_t ncounts = (size_t)ntiles * 256;
     if (ncounts > ws.radix_counts_elems) {
@@ -230,8 +193,6 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     }
     *keys = kin;
     *vals = vin;
-    if (dbg)
-        debug_radix(kin, vin, m, bit_lo, bit_hi, st, &dsum, true);
     return 0;
 }
 

@@ -116,66 +116,6 @@ __global__ void k_keys(const uint32_t *__restrict__ nval, const uint32_t *__rest
     key[c] = ((uint64_t)ngid[c] << kb) | (uint64_t)rank[i + h];
 }
 
-// Diagnostics (SALZ_DEBUG_DEVICE): sortedness of a radix output on [0, bits) -> bad[round].
-__global__ void k_dbg_sorted(const uint64_t *key, uint32_t m, int bits, unsigned int *bad)
-{
-    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (c == 0 || c >= m)
-        return;
-    uint64_t mask = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
-    if ((key[c - 1] & mask) > (key[c] & mask))
-        atomicAdd(bad, 1u);
-}
-
-__device__ __forceinline__ uint64_t dbg_mix(uint64_t x)
-{
-    x ^= x >> 31;
-    x *= 0x9E3779B97F4A7C15ull;
-    x ^= x >> 29;
-    return x * 0xBF58476D1CE4E5B9ull;
-}
-
-__global__ void k_dbg_multiset(const uint64_t *key, const uint32_t *val, uint32_t m,
-                               unsigned long long *sum)
-{
-    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (c < m)
-        atomicAdd(sum, (unsigned long long)dbg_mix(key[c] ^ ((uint64_t)val[c] * 0xD6E8FEB86659FD93ull)));
-}
-
-__global__ void k_dbg_init_keys(const uint8_t *T, const uint64_t *key, const uint32_t *val, uint32_t n,
-                                unsigned int *bad, unsigned long long *samples)
-{
-    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (c >= n)
-        return;
-    uint32_t i = val[c];
-    uint64_t w = 0;
-    for (uint32_t k = 0; k < 8; k++)
-        w = (w << 8) | (i + k < n ? T[i + k] : 0u);
-    uint64_t k = key[c];
-    if (w != k) {
-        unsigned int q = atomicAdd(bad, 1u);
-        if (q < 4) {
-            samples[4 * q + 0] = c;
-            samples[4 * q + 1] = i;
-            samples[4 * q + 2] = k;
-            samples[4 * q + 3] = w;
-        }
-    }
-}
-
-// group ids of the new active list must be non-decreasing and values distinct-ish (sum check)
-__global__ void k_dbg_active(const uint32_t *nval, const uint32_t *ngid, uint32_t m, uint32_t n,
-                             unsigned int *bad)
-{
-    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (c >= m)
-        return;
-    if (nval[c] >= n || (c > 0 && ngid[c - 1] > ngid[c]))
-        atomicAdd(bad, 1u);
-}
-
 }  // namespace
 
 int stage_suffix_array(Workspace &ws, uint32_t n)
@@ -200,34 +140,15 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     const int kb = bit_width(n);
     ws.stats.sa_rounds = 0;
     ws.stats.sa_sorted_elems = 0;
-    static const bool dbg = getenv("SALZ_DEBUG_DEVICE") != nullptr;
-    unsigned int *dbad = reinterpret_cast<unsigned int *>(ws.dscal) + 600;  // [64] sort, [64] active
-    unsigned long long *dms = reinterpret_cast<unsigned long long *>(ws.dscal) + 400;  // [64][2]
-    if (dbg) {
-        SALZ_HIP(hipMemsetAsync(dbad, 0, 512 + 4, st));
-        SALZ_HIP(hipMemsetAsync(reinterpret_cast<unsigned long long *>(ws.dscal) + 900, 0, 128, st));
-        SALZ_HIP(hipMemsetAsync(dms, 0, 1024, st));
-        hipLaunchKernelGGL(k_dbg_init_keys, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, K, V, n,
-                           dbad + 128, reinterpret_cast<unsigned long long *>(ws.dscal) + 900);
-    }
     for (;;) {
         ws.stats.sa_rounds++;
         ws.stats.sa_sorted_elems += m;
         uint64_t *Kx = (K == ws.keyA) ? ws.keyB : ws.keyA;
         uint32_t *Vx = (V == ws.valA) ? ws.valB : ws.valA;
-        if (dbg)
-            hipLaunchKernelGGL(k_dbg_multiset, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m,
-                               dms + 2 * (ws.stats.sa_rounds - 1 & 63));
         if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, bits, ws, st) != 0)
             return -1;
-        if (dbg)
-            hipLaunchKernelGGL(k_dbg_multiset, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m,
-                               dms + 2 * (ws.stats.sa_rounds - 1 & 63) + 1);
         Kx = (K == ws.keyA) ? ws.keyB : ws.keyA;
         Vx = (V == ws.valA) ? ws.valB : ws.valA;
-        if (dbg)
-            hipLaunchKernelGGL(k_dbg_sorted, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, m, bits,
-                               dbad + (ws.stats.sa_rounds - 1 & 63));
 
         hipLaunchKernelGGL(k_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m, n, round0,
                            hf);
@@ -261,9 +182,6 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         hipLaunchKernelGGL(k_keys, dim3(grid_for(mnew, kT)), dim3(kT), 0, st, Vx, ngid, ws.rank,
                            mnew, h, kb, Kx);
         SALZ_LAUNCH_CHECK();
-        if (dbg)
-            hipLaunchKernelGGL(k_dbg_active, dim3(grid_for(mnew, kT)), dim3(kT), 0, st, Vx, ngid, mnew,
-                               n, dbad + 64 + (ws.stats.sa_rounds - 1 & 63));
         K = Kx;
         V = Vx;
         m = mnew;
@@ -275,98 +193,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         offo = offn;
         offn = t;
     }
-    if (dbg) {
-        unsigned int b[129];
-        unsigned long long ms[128];
-        SALZ_HIP(hipStreamSynchronize(st));
-        SALZ_HIP(hipMemcpy(b, dbad, 516, hipMemcpyDeviceToHost));
-        SALZ_HIP(hipMemcpy(ms, dms, 1024, hipMemcpyDeviceToHost));
-        unsigned long long smp[16];
-        SALZ_HIP(hipMemcpy(smp, reinterpret_cast<unsigned long long *>(ws.dscal) + 900, 128,
-                           hipMemcpyDeviceToHost));
-        if (b[128])
-            for (int q = 0; q < 4 && q < (int)b[128]; q++)
-                fprintf(stderr, "initkey sample c=%llu i=%llu key=%016llx want=%016llx\n", smp[4 * q],
-                        smp[4 * q + 1], smp[4 * q + 2], smp[4 * q + 3]);
-        fprintf(stderr, "sa initkeys_bad=%u rounds:", b[128]);
-        for (int r = 0; r < ws.stats.sa_rounds && r < 64; r++)
-            fprintf(stderr, " %u/%u/%s", b[r], b[64 + r], ms[2 * r] == ms[2 * r + 1] ? "ms" : "MS!");
-        fprintf(stderr, "\n");
-    }
     return 0;
 }
 
 }  // namespace salz
-
-// ---- test-only: minimal load-integrity stress (k_sa_init's access pattern in isolation) ----
-namespace salz {
-namespace {
-
-__global__ void k_stress_fill(uint8_t *T, size_t n, uint32_t seed)
-{
-    size_t i = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (i < n)
-        T[i] = (uint8_t)(((i * 2654435761u) >> 13) ^ seed ^ (i >> 7)) | 0x20u;
-}
-
-__global__ void k_stress_check(const uint8_t *T, const uint64_t *key, const uint32_t *val, uint32_t n,
-                               unsigned int *bad)
-{
-    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (c >= n)
-        return;
-    uint32_t i = val[c];
-    uint64_t w = 0;
-    for (uint32_t k = 0; k < 8; k++)
-        w = (w << 8) | (i + k < n ? T[i + k] : 0u);
-    if (w != key[c])
-        atomicAdd(bad, 1u);
-}
-
-}  // namespace
-}  // namespace salz
-
-extern "C" long salz_debug_load_selftest(int device, uint32_t n, int iters, size_t extra_bytes,
-                                         size_t pre_bytes, uint32_t seed)
-{
-    using namespace salz;
-    if (hipSetDevice(device) != hipSuccess)
-        return -1;
-    uint8_t *T = nullptr;
-    uint64_t *key = nullptr;
-    uint32_t *val = nullptr;
-    unsigned int *bad = nullptr;
-    void *extra = nullptr, *pre = nullptr;
-    if (pre_bytes && hipMalloc(&pre, pre_bytes))
-        return -1;
-    if (hipMalloc(&T, n + 256) || hipMalloc(&key, 8ull * n) || hipMalloc(&val, 4ull * n) ||
-        hipMalloc(&bad, 4))
-        return -1;
-    if (extra_bytes && hipMalloc(&extra, extra_bytes))
-        return -1;
-    hipStream_t st;
-    (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-    (void)hipMemsetAsync(bad, 0, 4, st);
-    hipLaunchKernelGGL(k_stress_fill, dim3(grid_for(n, kT)), dim3(kT), 0, st, T, (size_t)n, seed);
-    (void)hipMemsetAsync(T + n, 0, 128, st);
-    for (int it = 0; it < iters; it++) {
-        hipLaunchKernelGGL(k_sa_init, dim3(grid_for(n, kT)), dim3(kT), 0, st, T, n, key, val);
-        hipLaunchKernelGGL(k_stress_check, dim3(grid_for(n, kT)), dim3(kT), 0, st, T, key, val, n, bad);
-        if (extra_bytes && (it & 3) == 0)
-            (void)hipMemsetAsync(extra, it & 0xff, extra_bytes, st);
-    }
-    unsigned int b = 0;
-    (void)hipMemcpyAsync(&b, bad, 4, hipMemcpyDeviceToHost, st);
-    (void)hipStreamSynchronize(st);
-    (void)hipFree(T);
-    (void)hipFree(key);
-    (void)hipFree(val);
-    (void)hipFree(bad);
-    if (extra)
-        (void)hipFree(extra);
-    if (pre)
-        (void)hipFree(pre);
-    fprintf(stderr, "load selftest: T=%p key=%p val=%p\n", (void *)T, (void *)key, (void *)val);
-    (void)hipStreamDestroy(st);
-    return (long)b;
-}

@@ -156,3 +156,64 @@ def test_device_resident_api(salz):
     d_src.free()
     d_dst.free()
     ctx.close()
+
+
+@pytest.fixture
+def klog(request, monkeypatch):
+    """Force the parse chunk length (2^klog positions per lane) through SALZ_PARSE_KLOG."""
+    monkeypatch.setenv("SALZ_PARSE_KLOG", str(request.param))
+    return request.param
+
+
+@pytest.mark.parametrize("klog", [6, 7, 8, 9], indirect=True)
+@pytest.mark.parametrize("kind,n,seed,alpha", [("text", 300007, 2, 0), ("mixed", 400000, 3, 0),
+                                               ("fib", 70001, 0, 0), ("smx", 100000, 1, 4)])
+def test_stages_every_chunk_length(ctx, klog, kind, n, seed, alpha):
+    src = _make(kind, n, seed, alpha)
+    out, d = ctx.encode_dump(src)
+    o = oracle_stages(src)
+    for k in ("dlen", "doff"):
+        i = _first_diff(d[k], o[k])
+        assert i < 0, f"K=2^{klog}: {k} differs at {i}: gpu {d[k][i]} oracle {o[k][i]}"
+    i = _first_diff(d["cost"][1:], o["cost"][1:])
+    assert i < 0, f"K=2^{klog}: cost differs at {i + 1}"
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and out == ref
+
+
+@pytest.mark.parametrize("kind,n", [("text", 20_000_000), ("mixed", 24_000_000)])
+def test_large_blocks_match_oracle(salz, kind, n):
+    """Blocks large enough for the default chunk lengths 2^7 / 2^8 (parse_chunk_log)."""
+    src = gen(kind, n, 4)
+    rc, ref = oracle_encode(src)
+    c = salz.Context(0, n)
+    assert rc == 0 and c.encode(src) == ref
+    c.close()
+
+
+def test_fib_256mib_golden(salz):
+    """SURVEY App. C / BASELINE configs[4]: 256 MiB Fibonacci word, one block, against the
+    reference's golden output hash (the oracle would take minutes at this size)."""
+    vec = next(v for v in golden("appendix_c.json")["vectors"] if v["n"] == 1 << 28)
+    src = gen("fib", vec["n"])
+    c = salz.Context(0, vec["n"])
+    out = c.encode(src)
+    c.close()
+    assert len(out) == vec["out_len"]
+    assert sha256(out) == vec["out_sha256"]
+    assert salz.decode_safe(out, len(src)) == src.tobytes()
+
+
+@pytest.mark.parametrize("block,size", [(1 << 20, 5 * (1 << 20) + 12345), (1 << 16, (1 << 18) + 777)])
+def test_encode_blocks_container(salz, block, size):
+    """The CLI container (programs/salzcli.c:102-185) from the multi-block queue equals the
+    per-block oracle streams framed in block order; decodes back (host threads)."""
+    src = gen("mixed", size, 9)
+    got = salz.encode_blocks(src, block)
+    want = bytearray(b"ZLAS" + block.to_bytes(4, "little"))
+    for off in range(0, size, block):
+        rc, s = oracle_encode(src[off:off + block])
+        assert rc == 0
+        want += len(s).to_bytes(4, "little") + s
+    assert got == bytes(want)
+    assert salz.decode_blocks(got, size) == src.tobytes()
