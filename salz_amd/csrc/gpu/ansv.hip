@@ -9,9 +9,11 @@
 // exact LCPs, so the range minimum reproduces them bit for bit.
 //
 // One heap-ordered min tree over np2 leaves holds (min SA, min LCP) per node. Each 256-thread
-// workgroup builds the bottom 11 levels of its 2048-leaf block in LDS, answers every query
-// whose answer lies inside the block there, and writes its subtree out; queries that leave
-// the block climb the global tree from the block root (k_ansv_global).
+// workgroup builds the bottom 11 levels of its 2048-leaf block in LDS and writes its subtree
+// out. Queries are answered first by a linear scan of the kNear neighbouring ranks (most
+// nearest smaller values are close; lanes read consecutive LDS words), then the rest walk the
+// block's tree as a compacted LDS queue (few, full waves instead of divergent ones); queries
+// that leave the block climb the global tree from the block root (k_ansv_global).
 // Output cand[p] = {p - PSV, lenP, p - NSV, lenN}, the reference's aux layout (:555-558).
 #include "internal.hpp"
 
@@ -21,6 +23,7 @@ namespace {
 constexpr int kT = 256;
 constexpr uint32_t kB = 2048;  // leaves per workgroup block
 constexpr uint32_t kInf = 0xffffffffu;
+constexpr uint32_t kNear = 16;  // linear neighbour scan before the tree walk
 
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
@@ -72,73 +75,116 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
         tlcp[g] = vlc[k];
     }
 
+    // Phase 1: most nearest smaller values are a few ranks away. Scan up to kNear neighbours
+    // on each side (lanes read consecutive LDS words: no bank conflicts); queue the rest.
+    __shared__ uint16_t wq[2 * kB];
+    __shared__ uint32_t wq_n;
+    if (tid == 0)
+        wq_n = 0;
+    __syncthreads();
     for (uint32_t l = tid; l < kB; l += kT) {
-        uint32_t r = b0 + l;
+        const uint32_t r = b0 + l;
         if (r >= n)
             break;
         const uint32_t v = vsa[kB + l];
-
-        // PSV: nearest smaller to the left; LCP minimum over (r', r].
-        uint32_t lm = vlc[kB + l], node = kB + l, hit = kInf;
-        while (node > 1) {
-            if (node & 1u) {
-                uint32_t s = node - 1;
-                if (vsa[s] < v) {
-                    while (s < kB) {
-                        uint32_t rc = 2 * s + 1;
-                        if (vsa[rc] < v) {
-                            s = rc;
-                        } else {
-                            lm = umin(lm, vlc[rc]);
-                            s = 2 * s;
-                        }
-                    }
-                    hit = s - kB;
-                    break;
-                }
-                lm = umin(lm, vlc[s]);
+        uint32_t lmP = vlc[kB + l], hitP = kInf;
+        for (uint32_t d = 1; d <= kNear && d <= l; d++) {
+            if (vsa[kB + l - d] < v) {
+                hitP = l - d;
+                break;
             }
-            node >>= 1;
+            lmP = umin(lmP, vlc[kB + l - d]);
         }
-        if (hit != kInf) {
-            put_psv(cand, klog, v, vsa[kB + hit], lm);
+        uint32_t lmN = kInf, hitN = kInf;
+        for (uint32_t d = 1; d <= kNear && l + d < kB; d++) {
+            lmN = umin(lmN, vlc[kB + l + d]);
+            if (vsa[kB + l + d] < v) {
+                hitN = l + d;
+                break;
+            }
+        }
+        if (hitP != kInf && hitN != kInf) {
+            cand[sidx(v, klog)] = make_uint4(v - vsa[kB + hitP], lmP, v - vsa[kB + hitN], lmN);
         } else {
-            uint32_t q = atomicAdd(&qcount[0], 1u);
-            qp[q] = r;
-            qp_len[q] = lm;
+            if (hitP != kInf)
+                put_psv(cand, klog, v, vsa[kB + hitP], lmP);
+            else
+                wq[atomicAdd(&wq_n, 1u)] = (uint16_t)(l << 1);
+            if (hitN != kInf)
+                put_nsv(cand, klog, v, vsa[kB + hitN], lmN);
+            else
+                wq[atomicAdd(&wq_n, 1u)] = (uint16_t)(l << 1 | 1u);
         }
+    }
+    __syncthreads();
 
-        // NSV: nearest smaller to the right; LCP minimum over (r, r'].
-        lm = kInf;
-        node = kB + l;
-        hit = kInf;
-        while (node > 1) {
-            if (!(node & 1u)) {
-                uint32_t s = node + 1;
-                if (vsa[s] < v) {
-                    while (s < kB) {
-                        uint32_t lc = 2 * s;
-                        if (vsa[lc] < v) {
-                            s = lc;
-                        } else {
-                            lm = umin(lm, vlc[lc]);
-                            s = 2 * s + 1;
+    // Phase 2: the queued queries walk the block's min-tree; answers outside the block go to
+    // the global queues (k_ansv_global continues from the block root).
+    const uint32_t nw = wq_n;
+    for (uint32_t w = tid; w < nw; w += kT) {
+        const uint32_t e = wq[w], l = e >> 1, r = b0 + l;
+        const uint32_t v = vsa[kB + l];
+        if (!(e & 1u)) {
+            // PSV: nearest smaller to the left; LCP minimum over (r', r].
+            uint32_t lm = vlc[kB + l], node = kB + l, hit = kInf;
+            while (node > 1) {
+                if (node & 1u) {
+                    uint32_t s = node - 1;
+                    if (vsa[s] < v) {
+                        while (s < kB) {
+                            uint32_t rc = 2 * s + 1;
+                            if (vsa[rc] < v) {
+                                s = rc;
+                            } else {
+                                lm = umin(lm, vlc[rc]);
+                                s = 2 * s;
+                            }
                         }
+                        hit = s - kB;
+                        break;
                     }
                     lm = umin(lm, vlc[s]);
-                    hit = s - kB;
-                    break;
                 }
-                lm = umin(lm, vlc[s]);
+                node >>= 1;
             }
-            node >>= 1;
-        }
-        if (hit != kInf) {
-            put_nsv(cand, klog, v, vsa[kB + hit], lm);
+            if (hit != kInf) {
+                put_psv(cand, klog, v, vsa[kB + hit], lm);
+            } else {
+                uint32_t q = atomicAdd(&qcount[0], 1u);
+                qp[q] = r;
+                qp_len[q] = lm;
+            }
         } else {
-            uint32_t q = atomicAdd(&qcount[1], 1u);
-            qn[q] = r;
-            qn_len[q] = lm;
+            // NSV: nearest smaller to the right; LCP minimum over (r, r'].
+            uint32_t lm = kInf, node = kB + l, hit = kInf;
+            while (node > 1) {
+                if (!(node & 1u)) {
+                    uint32_t s = node + 1;
+                    if (vsa[s] < v) {
+                        while (s < kB) {
+                            uint32_t lc = 2 * s;
+                            if (vsa[lc] < v) {
+                                s = lc;
+                            } else {
+                                lm = umin(lm, vlc[lc]);
+                                s = 2 * s + 1;
+                            }
+                        }
+                        lm = umin(lm, vlc[s]);
+                        hit = s - kB;
+                        break;
+                    }
+                    lm = umin(lm, vlc[s]);
+                }
+                node >>= 1;
+            }
+            if (hit != kInf) {
+                put_nsv(cand, klog, v, vsa[kB + hit], lm);
+            } else {
+                uint32_t q = atomicAdd(&qcount[1], 1u);
+                qn[q] = r;
+                qn_len[q] = lm;
+            }
         }
     }
 }

@@ -59,9 +59,9 @@ __device__ __forceinline__ uint64_t vn_bits(uint32_t v, uint32_t k)
 }
 
 __global__ void k_mark_start(const uint32_t *__restrict__ eidx, const uint64_t *__restrict__ pst,
-                             uint32_t *__restrict__ emark)
+                             uint32_t klog, uint32_t *__restrict__ emark)
 {
-    emark[eidx[(uint32_t)pst[0]]] = 1u;  // exit of position 0 (slot sidx(0) == 0)
+    emark[eidx[sidx((uint32_t)pst[0], klog)]] = 1u;  // exit of position 0 (slot sidx(0) == 0)
 }
 
 __global__ void k_mark_step(const uint32_t *__restrict__ jt, uint32_t *emark, uint32_t ne)
@@ -275,7 +275,7 @@ int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap, 
     SALZ_HIP(hipMemsetAsync(entry, 0xff, sizeof(uint32_t) * ((size_t)nch + 1), st));
     if (ne) {
         SALZ_HIP(hipMemsetAsync(emark, 0, sizeof(uint32_t) * ne, st));
-        hipLaunchKernelGGL(k_mark_start, dim3(1), dim3(1), 0, st, eidx, ps.pst, emark);
+        hipLaunchKernelGGL(k_mark_start, dim3(1), dim3(1), 0, st, eidx, ps.pst, ws.klog, emark);
         SALZ_LAUNCH_CHECK();
         for (uint32_t k = 0; k < ps.levels; k++) {
             hipLaunchKernelGGL(k_mark_step, dim3(grid_for(ne, kT)), dim3(kT), 0, st,

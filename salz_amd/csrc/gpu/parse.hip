@@ -53,7 +53,9 @@ __device__ __forceinline__ uint32_t factor_bits(uint32_t off, uint32_t len)
     return 1u + 8u + 4u * vn_size((off - 1u) >> 8) + ((len - 3u) >> 3) + 4u;
 }
 
-// Storage slots 0..S-1 -> cost seed 9 * (n - p) (all literals); slots past n unused.
+// Storage slots 0..S-1 -> cost seed 3 * (n - p); slots past n unused. Any seed gives the
+// same fixed point (the final pass confirms every decision against exact costs); one near
+// the typical optimum (~3 bits per byte) needs fewer passes on mixed data (tools/parse_sim.c).
 __global__ __launch_bounds__(kT) void k_cost_seed(uint32_t *cost, uint32_t n, uint32_t klog,
                                                   size_t S)
 {
@@ -62,7 +64,7 @@ __global__ __launch_bounds__(kT) void k_cost_seed(uint32_t *cost, uint32_t n, ui
         return;
     uint64_t p = spos(s, klog);
     if (p <= n)
-        cost[s] = 9u * (n - (uint32_t)p);
+        cost[s] = 3u * (n - (uint32_t)p);
 }
 
 __global__ __launch_bounds__(kT) void k_parse_chunk(
@@ -138,7 +140,8 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         atomicAdd(changed, diff);
 }
 
-// eflag[exit(p)] = 1 for every position, and for n (the root).
+// Exit flags and the compacted exit index live in storage (slot) order like the other parse
+// arrays: eflag[sidx(exit(p))] = 1 for every position, and for n (the root).
 __global__ void k_mark_exits(const uint64_t *__restrict__ pst, uint32_t n, uint32_t klog, size_t S,
                              uint32_t *eflag)
 {
@@ -146,32 +149,33 @@ __global__ void k_mark_exits(const uint64_t *__restrict__ pst, uint32_t n, uint3
     if (s >= S)
         return;
     if (spos(s, klog) < n)
-        eflag[(uint32_t)pst[s]] = 1u;
+        eflag[sidx((uint32_t)pst[s], klog)] = 1u;
     if (s == 0)
-        eflag[n] = 1u;
+        eflag[sidx(n, klog)] = 1u;
 }
 
-// Compact E: node x = eidx[q] for exit position q; parent = exit of q, weight = in-chunk
-// bit sum of q's path (estimate - cin[exit]).
+// Compact E: node x = eidx[slot of q] for exit position q; parent = exit of q, weight =
+// in-chunk bit sum of q's path (estimate - cin[exit]).
 __global__ void k_compact_exits(const uint32_t *__restrict__ eflag,
                                 const uint32_t *__restrict__ eidx, const uint64_t *__restrict__ pst,
-                                const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog,
+                                const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog, size_t S,
                                 uint32_t *__restrict__ elist, uint32_t *__restrict__ jt0,
                                 uint32_t *__restrict__ js)
 {
-    size_t q = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (q > n || !eflag[q])
+    size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (s >= S || !eflag[s])
         return;
-    uint32_t x = eidx[q];
-    elist[x] = (uint32_t)q;
+    const uint32_t q = (uint32_t)spos(s, klog);
+    uint32_t x = eidx[s];
+    elist[x] = q;
     if (q == n) {
         jt0[x] = x;
         js[x] = 0;
     } else {
-        const uint64_t v = pst[sidx((uint32_t)q, klog)];
-        const uint32_t e = (uint32_t)v;
-        jt0[x] = eidx[e];
-        js[x] = (uint32_t)(v >> 32) - cin[sidx(e, klog)];
+        const uint64_t v = pst[s];
+        const size_t se = sidx((uint32_t)v, klog);
+        jt0[x] = eidx[se];
+        js[x] = (uint32_t)(v >> 32) - cin[se];
     }
 }
 
@@ -202,8 +206,7 @@ __global__ void k_cost_rest(const uint32_t *__restrict__ eflag, const uint64_t *
     size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
     if (s >= S)
         return;
-    const uint64_t p = spos(s, klog);
-    if (p >= n || eflag[p])
+    if (spos(s, klog) >= n || eflag[s])
         return;
     const uint64_t v = pst[s];
     const size_t se = sidx((uint32_t)v, klog);
@@ -283,11 +286,11 @@ int stage_parse(Workspace &ws, uint32_t n)
             return -1;
         }
         // Exact costs for the new decisions.
-        SALZ_HIP(hipMemsetAsync(eflag, 0, sizeof(uint32_t) * ((size_t)n + 1), st));
+        SALZ_HIP(hipMemsetAsync(eflag, 0, sizeof(uint32_t) * S, st));
         hipLaunchKernelGGL(k_mark_exits, dim3(grid_for(S, kT)), dim3(kT), 0, st, ws.pst, n, klog, S,
                            eflag);
         SALZ_LAUNCH_CHECK();
-        if (scan_sum_u32(eflag, eidx, (size_t)n + 1, false, etotal, ws, st) != 0)
+        if (scan_sum_u32(eflag, eidx, S, false, etotal, ws, st) != 0)
             return -1;
         if (read_scalars(ws, 0, 256, "parse.ne") != 0)
             return -1;
@@ -297,8 +300,8 @@ int stage_parse(Workspace &ws, uint32_t n)
             set_error("parse: exit forest too large for snapshot area (|E|=%u)", ne);
             return -1;
         }
-        hipLaunchKernelGGL(k_compact_exits, dim3(grid_for((size_t)n + 1, kT)), dim3(kT), 0, st,
-                           eflag, eidx, ws.pst, cin, n, klog, elist, snap, js[0]);
+        hipLaunchKernelGGL(k_compact_exits, dim3(grid_for(S, kT)), dim3(kT), 0, st, eflag, eidx,
+                           ws.pst, cin, n, klog, S, elist, snap, js[0]);
         SALZ_LAUNCH_CHECK();
         int jc = 0;
         for (uint32_t k = 0; k < K; k++) {

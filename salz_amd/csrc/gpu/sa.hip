@@ -91,7 +91,11 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     uint32_t size = headpos[g + 1] - hp;
     uint32_t o = round0 ? 0u : off_old[(uint32_t)(key[c] >> kb_old)];
     uint32_t i = val[c];
-    rank[i] = hp + o + 1u;
+    // The first subgroup of an old group keeps the old group's head, so its members' ranks
+    // are unchanged; every other rank (and all of round 0) is written.
+    const bool same = !round0 && (hp == 0 || (key[hp - 1] >> kb_old) != (key[hp] >> kb_old));
+    if (!same)
+        rank[i] = hp + o + 1u;
     if (size == 1) {
         sa[c + o] = i;
     } else {
@@ -139,6 +143,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     int bits = 64, kb_old = 0, round0 = 1;
     const int kb = bit_width(n);
     ws.stats.sa_rounds = 0;
+    static const bool verbose = getenv("SALZ_DEBUG_SA") != nullptr;
     ws.stats.sa_sorted_elems = 0;
     for (;;) {
         ws.stats.sa_rounds++;
@@ -173,6 +178,9 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
             return -1;
         uint64_t tot = ws.hscal[8];
         uint32_t Gnew = (uint32_t)tot, mnew = (uint32_t)(tot >> 32);
+        if (verbose)
+            fprintf(stderr, "sa round %d h=%u m=%u bits=%d groups=%u -> survivors %u in %u groups\n",
+                    ws.stats.sa_rounds, h, m, bits, G, mnew, Gnew);
         if (mnew == 0)
             break;
         if (h >= n || Gnew == 0) {

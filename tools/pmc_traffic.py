@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic from two rocprofv3 PMC passes of the same bench command.
+
+  python tools/pmc_traffic.py FETCH_DIR/pmc_counter_collection.csv WRITE_DIR/pmc_counter_collection.csv \
+      [--kernel k_radix_scatter] [--json bench_traffic.json] [--summary out.txt]
+
+Correction (/opt/skills/guides/MI355X_MICROARCH.md, "HBM [CDNA4]"): FETCH_SIZE and WRITE_SIZE
+are in KiB; on gfx950 FETCH_SIZE counts half the bytes of wide streaming reads, so
+traffic = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 per dispatch. Reads narrower than
+16 B per lane are uncalibrated (the guide): treat the absolute as an estimate and the
+ratio to the algorithmic bytes as the signal.
+
+Algorithmic bytes of k_radix_scatter: 24 B per element (read 8 B key + 4 B value, write
+8 B key + 4 B value); elements per dispatch = Grid_Size / 256 * 4096 (4096-element tiles,
+the last tile may be partial, so this is an upper bound within one tile).
+"""
+import argparse
+import collections
+import csv
+import json
+import re
+
+
+def load(path):
+    per = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        m = re.search(r"(k_[a-z0-9_]+|__amd_rocclr_[A-Za-z]+)", r["Kernel_Name"])
+        name = m.group(1) if m else r["Kernel_Name"][:40]
+        if "unsigned long" in r["Kernel_Name"] and name.startswith("k_scan"):
+            name += "<u64>"
+        per[name].append((int(r["Dispatch_Id"]), float(r["Counter_Value"]), int(r["Grid_Size"])))
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--kernel", default="k_radix_scatter")
+    ap.add_argument("--json")
+    ap.add_argument("--summary")
+    ap.add_argument("--workload", default="bench.py default (100,000,000-byte text block, 1 step)")
+    a = ap.parse_args()
+    F, W = load(a.fetch), load(a.write)
+    lines = [f"{'kernel':28s} {'launches':>8s} {'fetch MB':>10s} {'write MB':>10s} {'traffic MB/launch':>18s}"]
+    for k in sorted(F, key=lambda k: -sum(v for _, v, _ in F[k])):
+        f = sum(v for _, v, _ in F[k]) * 1024 * 2
+        w = sum(v for _, v, _ in W.get(k, [])) * 1024
+        c = len(F[k])
+        lines.append(f"{k:28s} {c:8d} {f / 1e6:10.1f} {w / 1e6:10.1f} {(f + w) / c / 1e6:18.2f}")
+    text = "\n".join(lines)
+    print(text)
+    if a.summary:
+        open(a.summary, "w").write(text + "\n")
+    fk, wk = F[a.kernel], W[a.kernel]
+    launches = len(fk)
+    fetch = sum(v for _, v, _ in fk) * 1024 * 2 / launches
+    write = sum(v for _, v, _ in wk) * 1024 / len(wk)
+    elems = sum(g // 256 * 4096 for _, _, g in fk) / launches
+    out = {
+        "kernel": a.kernel,
+        "workload": a.workload,
+        "launches": launches,
+        "fetch_bytes_per_launch": round(fetch),
+        "write_bytes_per_launch": round(write),
+        "traffic_per_launch": round(fetch + write),
+        "alg_bytes_per_launch_upper": round(24 * elems),
+        "traffic_over_alg": round((fetch + write) / (24 * elems), 3),
+        "correction": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM section)",
+    }
+    print(json.dumps(out))
+    if a.json:
+        json.dump(out, open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
