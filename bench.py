@@ -1,20 +1,27 @@
 #!/usr/bin/env python3
-"""bench.py - compress MB/s of the MI355X SA-LZ encoder on an enwik8-sized block.
+"""bench.py - compress MB/s of the MI355X SA-LZ encoder (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], "enwik8 (100 MB) single block, SA+PLCP+LZ on one MI355X"):
-one 100,000,000-byte block of the deterministic wiki-text surrogate (tools/datagen.c; the real
-enwik8 is not available offline) per GPU, resident in HBM before timing. A step is one full
-salz_gpu_encode_device call: suffix array, LCP, PSV/NSV candidates, optimal parse and emission of
-the bit-exact reference stream into HBM.
+Default workload (BASELINE.json configs[1], "enwik8 (100 MB) single block, SA+PLCP+LZ on one
+MI355X"): one 100,000,000-byte block of the deterministic wiki-text surrogate per GPU
+(tools/datagen.c; the real enwik8 is not available offline), resident in HBM before timing.
+A step is one full salz_gpu_encode_device call per block: suffix array, LCP, PSV/NSV
+candidates, optimal parse and emission of the bit-exact reference stream into HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  (N > 1: launched by torch.distributed.run, one rank per GPU; each rank encodes its own block:
-   weak scaling over independent blocks, no data-path collective.)
+Other BASELINE configs (--workload):
+  enwik9   configs[3]: 10^9 bytes of the text surrogate in 64 MiB blocks, blocks sharded
+           round-robin over the ranks (salz_amd/dist.py); a step encodes every block once
+  silesia  configs[2]: 211,957,760 bytes of the mixed surrogate in 16 MiB blocks, sharded
+  fib256   configs[4]: the 268,435,456-byte Fibonacci word as one block per GPU
 
-Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel (the radix-sort scatter of
-the suffix sorter) by algorithmic bytes / HIP-event-measured launch time; `cpu_baseline` times the
-CPU port of the reference (oracle/liboracle.so, 1 thread) on the same block, which also serves as a
-bit-exact parity check of the GPU stream at full size.
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload enwik8|enwik9|silesia|fib256]
+  (N > 1: launched by torch.distributed.run, one rank per GPU; weak scaling for the one-block
+   workloads, strong for the sharded ones. The only exchange is the per-block encoded length,
+   all-reduced over gloo: no data-path collective.)
+
+Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel (the suffix sorter's
+radix scatter) by algorithmic bytes / HIP-event-measured launch time on the library's own
+stream; `cpu_baseline` times the CPU port of the reference (oracle/liboracle.so, 1 thread) on
+one block of the same input, which also checks full-block parity of the GPU stream.
 """
 from __future__ import annotations
 
@@ -30,17 +37,28 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md "Chip-level parameters")
 RADIX_BYTES_PER_ELEM = 24  # scatter: read 8 B key + 4 B value, write 8 B key + 4 B value
 
+WORKLOADS = {
+    # name: (config, kind, total bytes, block bytes or None = one block per rank)
+    "enwik8": ("enwik8-sized single block per GPU (BASELINE configs[1])", "text", 100_000_000, None),
+    "enwik9": ("enwik9-sized input, 64 MiB blocks sharded over GPUs (BASELINE configs[3])", "text",
+               1_000_000_000, 64 << 20),
+    "silesia": ("Silesia-sized mixed input, 16 MiB blocks sharded over GPUs (BASELINE configs[2])",
+                "mixed", 211_957_760, 16 << 20),
+    "fib256": ("256 MiB Fibonacci word, single block per GPU (BASELINE configs[4])", "fib", 1 << 28, None),
+}
+
 
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--kind", default="text", help="text | fib | smx | mixed")
-    ap.add_argument("--size", type=int, default=100_000_000)
+    ap.add_argument("--workload", default="enwik8", choices=sorted(WORKLOADS))
+    ap.add_argument("--kind", default=None, help="override the input generator (text|fib|smx|mixed)")
+    ap.add_argument("--size", type=int, default=0, help="override the total input bytes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0,
-                    help="bytes of the block timed on the CPU port (0 = whole block)")
+                    help="bytes of one block timed on the CPU port (0 = the whole first block)")
     ap.add_argument("--profile-steps", action="store_true",
                     help="per-stage HIP-event timing on every timed step (adds small overhead)")
     return ap.parse_args()
@@ -53,55 +71,65 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     dist = None
     if world > 1:
-        import torch.distributed as dist  # gloo on CPU tensors: no GPU runtime of torch's own
+        # torch first: libsalz then shares torch's HIP runtime (one runtime per process,
+        # tools/runtime_check.py); only gloo CPU tensors are used.
+        import torch.distributed as dist
 
         dist.init_process_group("gloo")
 
-    import numpy as np
-
     import salz_amd
+    from salz_amd.dist import block_count, my_blocks
     from tests.helpers import gen  # workload generator (tools/libdatagen.so)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    def allmax(x: float) -> float:
+    def allreduce(vals, op):
         if dist is None:
-            return x
+            return vals
         import torch
 
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        t = torch.tensor(vals, dtype=torch.float64)
+        dist.all_reduce(t, op=op)
+        return t.tolist()
 
-    def allsum(x: float) -> float:
-        if dist is None:
-            return x
-        import torch
+    SUM = dist.ReduceOp.SUM if dist else None
+    MAX = dist.ReduceOp.MAX if dist else None
 
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return float(t.item())
-
+    config, kind, total, block = WORKLOADS[args.workload]
+    kind = args.kind or kind
+    total = args.size or total
+    sharded = block is not None
     ndev = salz_amd.device_count()
     if ndev == 0:
         raise SystemExit("bench.py: no HIP device visible")
     device = local % ndev
-    N = args.size
-    src = gen(args.kind, N, 1, 16 if args.kind == "smx" else 256)
-    ctx = salz_amd.Context(device, N)
-    d_src = salz_amd.DeviceBuffer(N, device).upload(src)
-    cap = salz_amd.encoded_len_max(N) + 4096
-    d_dst = salz_amd.DeviceBuffer(cap, device)
+
+    src = gen(kind, total, 1, 16 if kind == "smx" else 256)
+    if sharded:
+        if total % block == 0:
+            raise SystemExit("bench.py: total must not be a multiple of the block size (reference CLI)")
+        nblocks = block_count(total, block)
+        spans = [(b * block, min(total, (b + 1) * block)) for b in my_blocks(nblocks, rank, world)]
+    else:
+        nblocks = world
+        spans = [(0, total)]
+    max_block = max([e - s for s, e in spans] + [9])
+    ctx = salz_amd.Context(device, max_block)
+    cap = salz_amd.encoded_len_max(max_block) + 4096
+    d_src = [salz_amd.DeviceBuffer(e - s, device).upload(src[s:e]) for s, e in spans]
+    d_dst = [salz_amd.DeviceBuffer(cap, device) for _ in spans]
+
+    def step():
+        return [ctx.encode_device(d.ptr, e - s, o.ptr, cap) for d, o, (s, e) in zip(d_src, d_dst, spans)]
 
     # Warmup (untimed), then one instrumented pass for the kernel-level numbers.
-    out_len = 0
     for _ in range(args.warmup):
-        out_len = ctx.encode_device(d_src.ptr, N, d_dst.ptr, cap)
+        step()
     ctx.set_timing(True)
-    out_len = ctx.encode_device(d_src.ptr, N, d_dst.ptr, cap)
-    st = ctx.stats()
+    lens = step()
+    st = ctx.stats()  # stats of the last block encoded by this rank
     ctx.set_timing(bool(args.profile_steps))
 
     # Timed region: exactly K steps bracketed by barrier + device sync on both sides.
@@ -109,23 +137,28 @@ def main():
     salz_amd.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out_len = ctx.encode_device(d_src.ptr, N, d_dst.ptr, cap)
+        lens = step()
+        if sharded and dist is not None:  # the exchange step: per-block lengths -> offsets
+            v = [0.0] * nblocks
+            for b, x in zip(my_blocks(nblocks, rank, world), lens):
+                v[b] = float(x)
+            allreduce(v, SUM)
     salz_amd.synchronize(device)
     t1 = time.perf_counter()
     barrier()
-    dt = allmax(t1 - t0)
+    dt = allreduce([t1 - t0], MAX)[0]
     if args.profile_steps:
         st = ctx.stats()
 
-    stream = d_dst.download(out_len)
-    # Exchange step of the block queue: every rank's encoded length -> container offsets.
-    total_out = allsum(float(out_len + 4))
+    streams = [o.download(n) for o, n in zip(d_dst, lens)]
+    in_bytes, out_bytes = allreduce([float(sum(e - s for s, e in spans)), float(sum(lens))], SUM)
 
-    # Round trip through the product decoder (frame rule for > 16 MiB streams).
-    back = salz_amd.decode_safe(stream, N, frame=True)
-    roundtrip_ok = back == src.tobytes()
+    # Round trip of every local block through the product decoder (frame rule > 16 MiB).
+    ok = all(salz_amd.decode_safe(s_, e - s, frame=True) == src[s:e].tobytes()
+             for s_, (s, e) in zip(streams, spans))
+    roundtrip_ok = allreduce([0.0 if ok else 1.0], SUM)[0] == 0
 
-    value = world * N * args.steps / dt / 1e6
+    value = in_bytes * args.steps / dt / 1e6
     ms_step = dt / args.steps * 1e3
 
     # Roofline of the dominant kernel (radix scatter): algorithmic bytes / event-timed duration.
@@ -133,6 +166,15 @@ def main():
     ms_rx = float(st["ms_radix_scatter"])
     bytes_rx = RADIX_BYTES_PER_ELEM * float(st["radix_scatter_elems"])
     achieved = bytes_rx / (ms_rx * 1e-3) / 1e9 if ms_rx > 0 else 0.0
+    # HBM traffic of the same kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
+    # command (tools/pmc_traffic.py -> bench_traffic.json), when they were taken on this workload.
+    traffic = None
+    tpath = os.path.join(ROOT, "bench_traffic.json")
+    if os.path.exists(tpath):
+        t = json.load(open(tpath))
+        if (t.get("kernel") == "k_radix_scatter" and t.get("kind") == kind and t.get("size") == total
+                and not sharded):
+            traffic = t["traffic_per_launch"]
     roofline = {
         "kernel": "k_radix_scatter",
         "bound": "hbm",
@@ -140,7 +182,8 @@ def main():
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": None,
+        "traffic": traffic,
+        "traffic_unit": "bytes/launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC)",
         "launches": launches,
         "avg_launch_us": round(ms_rx * 1e3 / launches, 2),
         "alg_bytes_per_launch": int(bytes_rx / launches),
@@ -148,24 +191,25 @@ def main():
 
     cpu = None
     parity_full = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline and spans:
         from tests.helpers import oracle_encode  # CPU port of the reference (baseline + checker)
 
-        sample = N if args.cpu_sample <= 0 else min(args.cpu_sample, N)
+        s, e = spans[0]
+        sample = (e - s) if args.cpu_sample <= 0 else min(args.cpu_sample, e - s)
         c0 = time.perf_counter()
-        rc, ref = oracle_encode(src[:sample])
+        rc, ref = oracle_encode(src[s:s + sample])
         c1 = time.perf_counter()
         cpu = {
             "value": round(sample / (c1 - c0) / 1e6, 3),
             "unit": "MB/s",
             "cores": 1,
             "kind": "port",
-            "sample": f"one {sample:,}-byte block of the same {args.kind} input, oracle/liboracle.so "
+            "sample": f"one {sample:,}-byte block of the same {kind} input, oracle/liboracle.so "
                       f"(clean-room C restatement of lib/salz.c + own SA-IS), 1 thread, "
                       f"{c1 - c0:.2f} s",
         }
-        if sample == N:
-            parity_full = bool(rc == 0 and ref == stream)
+        if sample == e - s:
+            parity_full = bool(rc == 0 and ref == streams[0])
 
     if rank == 0:
         line = {
@@ -177,26 +221,26 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": f"synthetic ({args.kind} surrogate, tools/datagen.c; enwik8 not available offline)",
+            "data": f"synthetic ({kind} surrogate, tools/datagen.c; the corpus is not available offline)",
             "config": {
-                "workload": "enwik8-sized single block per GPU (BASELINE configs[1])",
-                "block_bytes": N,
-                "blocks_per_gpu": 1,
-                "input": args.kind,
-                "parallelism": f"independent blocks x{world}",
+                "workload": config,
+                "input_bytes_total": int(in_bytes),
+                "block_bytes": block or total,
+                "blocks": nblocks,
+                "input": kind,
+                "parallelism": f"independent blocks over {world} GPU(s)",
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "encoded_bytes": out_len,
-            "ratio": round(N / out_len, 4),
-            "container_bytes_all_ranks": int(total_out),
-            "roundtrip_ok": roundtrip_ok,
+            "encoded_bytes": int(out_bytes),
+            "ratio": round(in_bytes / out_bytes, 4),
+            "roundtrip_ok": bool(roundtrip_ok),
             "parity_vs_cpu_port": parity_full,
-            "stages_ms": {k: round(st[k], 3) for k in
-                          ("ms_sa", "ms_lcp", "ms_ansv", "ms_parse", "ms_emit", "ms_total")},
+            "stages_ms_last_block": {k: round(st[k], 3) for k in
+                                     ("ms_sa", "ms_lcp", "ms_ansv", "ms_parse", "ms_emit", "ms_total")},
             "sa_rounds": st["sa_rounds"],
             "parse_iters": st["parse_iters"],
         }

@@ -51,7 +51,7 @@ void workspace_free(Workspace &ws)
         (void)hipSetDevice(ws.device);
     void *ptrs[] = {ws.text, ws.rank,     ws.sa,   ws.keyA, ws.keyB, ws.valA, ws.valB,
                     ws.u0,   ws.u1,       ws.u2,   ws.u3,   ws.g64,  ws.offA, ws.offB,
-                    ws.cand, ws.pst, ws.out, ws.radix_counts,  ws.scan_tmp,      ws.dscal};
+                    ws.cand, ws.pst, ws.lsc, ws.lrec, ws.lg2g, ws.out, ws.radix_counts,  ws.scan_tmp,      ws.dscal};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -92,7 +92,8 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
         dalloc(&ws.keyA, n1) || dalloc(&ws.keyB, n1) || dalloc(&ws.valA, n1) ||
         dalloc(&ws.valB, n1) || dalloc(&ws.u0, n1) || dalloc(&ws.u1, n1) || dalloc(&ws.u2, n1) ||
         dalloc(&ws.u3, n1) || dalloc(&ws.g64, n1) || dalloc(&ws.offA, n1) ||
-        dalloc(&ws.offB, n1) || dalloc(&ws.cand, ws.cap_s) || dalloc(&ws.pst, ws.cap_s) || dalloc(&ws.out, ws.out_cap) ||
+        dalloc(&ws.offB, n1) || dalloc(&ws.cand, ws.cap_s) || dalloc(&ws.pst, ws.cap_s) ||
+        dalloc(&ws.lsc, n1) || dalloc(&ws.lrec, n1 / 1024 + 2) || dalloc(&ws.lg2g, n1 / 1024 + 2) || dalloc(&ws.out, ws.out_cap) ||
         dalloc(&ws.radix_counts, ws.radix_counts_elems) ||
         dalloc(reinterpret_cast<uint8_t **>(&ws.scan_tmp), ws.scan_tmp_bytes) ||
         dalloc(&ws.dscal, 1024)) {

@@ -12,19 +12,33 @@
 //
 // rank[i] = 1 + SA position of the head of i's group; rank[n] = 0 (end of text sorts first).
 // Per round:
+//   sort        round 0: global LSD radix sort of all suffixes. Later rounds: the active
+//               list is already grouped, so only each group's members need ordering by
+//               rank[i + h]. Small groups (<= kSmall members) are sorted inside LDS, one
+//               workgroup per 2048-entry window of the list (k_seg_small, one HBM read and
+//               write); large groups are extracted, radix-sorted on (large-group id, rank)
+//               and put back (k_extract / k_putback). Ties may land in any order: equal keys
+//               stay one group, so the next round re-sorts them.
 //   k_heads     group-head flags of the sorted active list
 //   scan        -> group ids; k_headpos -> head index per group
-//   k_grpkeep   groups of size >= 2 survive; u64 scan packs (new gid, compact start)
+//   k_grpkeep   groups of size >= 2 survive; u64 scans pack (new gid, compact start) and
+//               (large-group id, start in the extracted array)
 //   k_commit    rank update for every active suffix, SA write for singletons, compaction
 //   k_keys      next round's keys: gid << kb | rank[i + h]
 #include "internal.hpp"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace salz {
 namespace {
 
 constexpr int kT = 256;
+constexpr uint32_t kSegT = 2048;     // window of the active list per k_seg_small workgroup
+constexpr uint32_t kSmall = kSegT;   // largest group sorted in LDS (must be <= kSegT)
+constexpr uint32_t kSegCap = 4096;   // LDS slots: a window's groups span < kSegT + kSmall
+constexpr int kSegThreads = 256;
+static_assert(kSegCap == 4096, "12-bit slot index in the LDS sort key");
 
 __global__ void k_sa_init(const uint8_t *__restrict__ T, uint32_t n, uint64_t *__restrict__ key,
                           uint32_t *__restrict__ val)
@@ -67,21 +81,32 @@ __global__ void k_headpos(const uint32_t *__restrict__ hf, const uint32_t *__res
 }
 
 __global__ void k_grpkeep(const uint32_t *__restrict__ headpos, uint32_t G,
-                          uint64_t *__restrict__ gsc)
+                          uint64_t *__restrict__ gsc, uint64_t *__restrict__ lsc)
 {
     size_t g = (size_t)blockIdx.x * kT + threadIdx.x;
     if (g >= G)
         return;
     uint32_t size = headpos[g + 1] - headpos[g];
     gsc[g] = size >= 2 ? (((uint64_t)size << 32) | 1ull) : 0ull;
+    lsc[g] = size > kSmall ? (((uint64_t)size << 32) | 1ull) : 0ull;
 }
+
+// Next round's group table (ginfo: size << 32 | compact start, gl: large-group id) is
+// written by each surviving group's head; large groups also get their extraction record.
+struct GroupTab {
+    uint64_t *ginfo;
+    uint32_t *gl;
+    uint64_t *lrec;
+    uint32_t *lg2g;
+};
 
 __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
                          const uint32_t *__restrict__ gall, const uint32_t *__restrict__ headpos,
-                         const uint64_t *__restrict__ gsc, const uint32_t *__restrict__ off_old,
-                         uint32_t *__restrict__ off_new, uint32_t *__restrict__ nval,
-                         uint32_t *__restrict__ ngid, uint32_t *__restrict__ rank,
-                         uint32_t *__restrict__ sa, uint32_t m, int kb_old, int round0)
+                         const uint64_t *__restrict__ gsc, const uint64_t *__restrict__ lsc,
+                         const uint32_t *__restrict__ off_old, uint32_t *__restrict__ off_new,
+                         uint32_t *__restrict__ nval, uint32_t *__restrict__ ngid,
+                         uint32_t *__restrict__ rank, uint32_t *__restrict__ sa, GroupTab tab,
+                         uint32_t m, int kb_old, int round0)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
@@ -104,9 +129,195 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
         uint32_t idx = cs + ((uint32_t)c - hp);
         nval[idx] = i;
         ngid[idx] = ng;
-        if ((uint32_t)c == hp)
+        if ((uint32_t)c == hp) {
             off_new[ng] = hp + o - cs;
+            tab.ginfo[ng] = ((uint64_t)size << 32) | cs;
+            if (size > kSmall) {
+                const uint64_t l = lsc[g];
+                const uint32_t lg = (uint32_t)l;
+                tab.gl[ng] = lg;
+                tab.lrec[lg] = (l & 0xffffffff00000000ull) | cs;
+                tab.lg2g[lg] = ng;
+            }
+        }
     }
+}
+
+// Stable 8-bit LSD passes over bits [12, 12 + nbits) of ITEMS * 256 LDS keys; wave-striped:
+// wave w owns slots [w * ITEMS * 64, (w + 1) * ITEMS * 64), item j covers 64 of them.
+template <int ITEMS>
+__device__ __forceinline__ void seg_lsd(uint64_t *sk, uint32_t (*cnt)[256], uint32_t *dstart,
+                                        uint32_t *wsum, int nbits)
+{
+    const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    __syncthreads();
+    for (int shift = 12; shift < 12 + nbits; shift += 8) {
+        for (int i = tid; i < 4 * 256; i += kSegThreads)
+            (&cnt[0][0])[i] = 0;
+        __syncthreads();
+        uint64_t k[ITEMS];
+        uint32_t lrank[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++)
+            k[j] = sk[wave * (ITEMS * 64) + j * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const unsigned d = (unsigned)(k[j] >> shift) & 255u;
+            uint64_t peers = ~0ull;
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t bb = wave_ballot(bit);
+                peers &= bit ? bb : ~bb;
+            }
+            const unsigned below = count_below(peers);
+            const int leader = (int)__ffsll((unsigned long long)peers) - 1;
+            uint32_t old = 0;
+            if ((int)lane == leader) {
+                old = cnt[wave][d];
+                cnt[wave][d] = old + (unsigned)__popcll(peers);
+            }
+            lrank[j] = shfl_u32(old, leader) + below;
+        }
+        __syncthreads();
+        {
+            const uint32_t c0 = cnt[0][tid], c1 = cnt[1][tid], c2 = cnt[2][tid], c3 = cnt[3][tid];
+            const uint32_t tot = c0 + c1 + c2 + c3;
+            uint32_t x = tot;
+#pragma unroll
+            for (unsigned dd = 1; dd < 64; dd <<= 1) {
+                const uint32_t y = shfl_up_u32(x, dd);
+                if (lane >= dd)
+                    x += y;
+            }
+            if (lane == 63)
+                wsum[wave] = x;
+            __syncthreads();
+            uint32_t pre = 0;
+            for (unsigned w = 0; w < wave; w++)
+                pre += wsum[w];
+            dstart[tid] = pre + x - tot;
+            cnt[0][tid] = 0;
+            cnt[1][tid] = c0;
+            cnt[2][tid] = c0 + c1;
+            cnt[3][tid] = c0 + c1 + c2;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; j++) {
+            const unsigned d = (unsigned)(k[j] >> shift) & 255u;
+            sk[dstart[d] + cnt[wave][d] + lrank[j]] = k[j];
+        }
+        __syncthreads();
+    }
+}
+
+// Small groups of one 2048-entry window of the active list, sorted in LDS by rank[i + h].
+// The window owns every small group that starts in it (a group of <= kSmall members ends
+// before the window's end + kSmall, and no large group can sit between two of them), so
+// the owned range [lo, hi) has < kSegCap entries. Sort key: local group << (kb + 12) |
+// rank << 12 | slot; a stable 8-bit LSD pass per digit of the (group, rank) part.
+__global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict__ K,
+                                                           uint32_t *__restrict__ V,
+                                                           const uint64_t *__restrict__ ginfo,
+                                                           uint32_t m, int kb)
+{
+    __shared__ uint64_t sk[kSegCap];
+    __shared__ uint32_t sv[kSegCap];
+    __shared__ uint32_t cnt[4][256];
+    __shared__ uint32_t dstart[256];
+    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t s_lo, s_hi, s_glast;
+
+    const unsigned tid = threadIdx.x;
+    const uint32_t t0 = blockIdx.x * kSegT;
+    const uint32_t t1 = (m - t0) < kSegT ? m : t0 + kSegT;
+    const uint64_t mask = (1ull << kb) - 1ull;
+    if (tid == 0) {
+        s_lo = 0xffffffffu;
+        s_hi = 0;
+        s_glast = 0;
+    }
+    __syncthreads();
+    for (uint32_t c = t0 + tid; c < t1; c += kSegThreads) {
+        const uint64_t g = K[c] >> kb;
+        if (c == 0 || (K[c - 1] >> kb) != g) {
+            const uint32_t size = (uint32_t)(ginfo[g] >> 32);
+            if (size <= kSmall) {
+                atomicMin(&s_lo, c);
+                atomicMax(&s_hi, c + size);
+                atomicMax(&s_glast, (uint32_t)g);
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t lo = s_lo, hi = s_hi;
+    if (lo == 0xffffffffu)
+        return;  // uniform: no small group starts in this window
+    const uint32_t count = hi - lo;
+    const uint32_t g0 = (uint32_t)(K[lo] >> kb);
+    const int nbits = kb + (32 - __builtin_clz((s_glast - g0) | 1u));
+
+    // slots actually sorted: count rounded up to 1024 (4 waves x 64 lanes x ITEMS / 4 steps)
+    const int items = (int)((count + 1023u) / 1024u) * 4;
+    for (uint32_t i = tid; i < (uint32_t)items * kSegThreads; i += kSegThreads) {
+        uint64_t key = ~0ull;  // padding sorts last in every digit
+        if (i < count) {
+            const uint64_t kk = K[lo + i];
+            key = (((kk >> kb) - g0) << (kb + 12)) | ((kk & mask) << 12) | i;
+            sv[i] = V[lo + i];
+        }
+        sk[i] = key;
+    }
+    switch (items) {
+    case 4: seg_lsd<4>(sk, cnt, dstart, wsum, nbits); break;
+    case 8: seg_lsd<8>(sk, cnt, dstart, wsum, nbits); break;
+    case 12: seg_lsd<12>(sk, cnt, dstart, wsum, nbits); break;
+    default: seg_lsd<16>(sk, cnt, dstart, wsum, nbits); break;
+    }
+
+    for (uint32_t i = tid; i < count; i += kSegThreads) {
+        const uint64_t key = sk[i];
+        const uint64_t g = g0 + (key >> (kb + 12));
+        K[lo + i] = (g << kb) | ((key >> 12) & mask);
+        V[lo + i] = sv[key & 0xfffu];
+    }
+}
+
+// Members of large groups -> contiguous extracted array, key (large-group id, rank).
+__global__ void k_extract(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
+                          const uint64_t *__restrict__ ginfo, const uint32_t *__restrict__ gl,
+                          const uint64_t *__restrict__ lrec, uint32_t m, int kb,
+                          uint64_t *__restrict__ KC, uint32_t *__restrict__ VC)
+{
+    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (c >= m)
+        return;
+    const uint64_t key = K[c];
+    const uint32_t g = (uint32_t)(key >> kb);
+    const uint64_t gi = ginfo[g];
+    if ((uint32_t)(gi >> 32) <= kSmall)
+        return;
+    const uint32_t lg = gl[g];
+    const uint32_t dst = (uint32_t)(lrec[lg] >> 32) + ((uint32_t)c - (uint32_t)gi);
+    KC[dst] = ((uint64_t)lg << kb) | (key & ((1ull << kb) - 1ull));
+    VC[dst] = V[c];
+}
+
+// Sorted large groups back to their places in the active list, original key format.
+__global__ void k_putback(const uint64_t *__restrict__ KS, const uint32_t *__restrict__ VS,
+                          const uint64_t *__restrict__ lrec, const uint32_t *__restrict__ lg2g,
+                          uint32_t mL, int kb, uint64_t *__restrict__ K, uint32_t *__restrict__ V)
+{
+    size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (x >= mL)
+        return;
+    const uint64_t key = KS[x];
+    const uint32_t lg = (uint32_t)(key >> kb);
+    const uint64_t r = lrec[lg];
+    const uint32_t orig = (uint32_t)r + ((uint32_t)x - (uint32_t)(r >> 32));
+    K[orig] = ((uint64_t)lg2g[lg] << kb) | (key & ((1ull << kb) - 1ull));
+    V[orig] = VS[x];
 }
 
 __global__ void k_keys(const uint32_t *__restrict__ nval, const uint32_t *__restrict__ ngid,
@@ -134,24 +345,68 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     uint64_t *gsc = ws.g64;
     uint32_t *d32 = reinterpret_cast<uint32_t *>(ws.dscal);
     uint64_t *d64 = ws.dscal + 8;
+    // Scratch borrowed from later stages (free while the suffix array is built): the
+    // extracted large groups live in pst (keys) and cand (values), the group table in cand.
+    uint8_t *cb = reinterpret_cast<uint8_t *>(ws.cand);
+    uint32_t *VC = reinterpret_cast<uint32_t *>(cb);
+    GroupTab tab{reinterpret_cast<uint64_t *>(cb + 4 * ws.cap_s),
+                 reinterpret_cast<uint32_t *>(cb + 12 * ws.cap_s), ws.lrec, ws.lg2g};
+    uint64_t *KC = ws.pst;
 
     SALZ_HIP(hipMemsetAsync(ws.rank + n, 0, sizeof(uint32_t), st));  // rank[n] = 0
     hipLaunchKernelGGL(k_sa_init, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, n, K, V);
     SALZ_LAUNCH_CHECK();
 
-    uint32_t m = n, h = 8;
-    int bits = 64, kb_old = 0, round0 = 1;
+    uint32_t m = n, h = 8, G_act = 0, GL = 0, mL = 0;
+    int kb_old = 0, round0 = 1;
     const int kb = bit_width(n);
     ws.stats.sa_rounds = 0;
-    static const bool verbose = getenv("SALZ_DEBUG_SA") != nullptr;
     ws.stats.sa_sorted_elems = 0;
+    static const bool verbose = getenv("SALZ_DEBUG_SA") != nullptr;
+    const char *mode_env = getenv("SALZ_SA_MODE");  // tests: "global" or "segmented"
     for (;;) {
         ws.stats.sa_rounds++;
         ws.stats.sa_sorted_elems += m;
         uint64_t *Kx = (K == ws.keyA) ? ws.keyB : ws.keyA;
         uint32_t *Vx = (V == ws.valA) ? ws.valB : ws.valA;
-        if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, bits, ws, st) != 0)
-            return -1;
+        const char *how = "global";
+        if (round0) {
+            if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, 64, ws, st) != 0)
+                return -1;
+        } else {
+            // Global sort of every active suffix on (group, rank) vs. LDS sort of the small
+            // groups + global sort of the large ones on (large group, rank): pick the one
+            // with less HBM traffic (32 B per element and 8-bit pass; 24 B per LDS-sorted or
+            // extracted/put-back element).
+            const int bits_all = kb + bit_width(G_act - 1), bits_large = kb + bit_width(GL ? GL - 1 : 0);
+            const double c_all = (double)m * ((bits_all + 7) / 8) * 32.0;
+            const double c_seg = (double)(m - mL) * 24.0 + m * 8.0 +
+                                 (double)mL * (((bits_large + 7) / 8) * 32.0 + 48.0);
+            bool seg = c_seg < c_all;
+            if (mode_env)
+                seg = strcmp(mode_env, "segmented") == 0;
+            if (!seg) {
+                if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, bits_all, ws, st) != 0)
+                    return -1;
+            } else {
+                how = "segmented";
+                hipLaunchKernelGGL(k_seg_small, dim3(grid_for(m, kSegT)), dim3(kSegThreads), 0, st,
+                                   K, V, tab.ginfo, m, kb);
+                SALZ_LAUNCH_CHECK();
+                if (mL) {
+                    hipLaunchKernelGGL(k_extract, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V,
+                                       tab.ginfo, tab.gl, tab.lrec, m, kb, KC, VC);
+                    SALZ_LAUNCH_CHECK();
+                    uint64_t *KS = KC;
+                    uint32_t *VS = VC;
+                    if (radix_sort_pairs(&KS, &VS, Kx, Vx, mL, 0, bits_large, ws, st) != 0)
+                        return -1;
+                    hipLaunchKernelGGL(k_putback, dim3(grid_for(mL, kT)), dim3(kT), 0, st, KS, VS,
+                                       tab.lrec, tab.lg2g, mL, kb, K, V);
+                    SALZ_LAUNCH_CHECK();
+                }
+            }
+        }
         Kx = (K == ws.keyA) ? ws.keyB : ws.keyA;
         Vx = (V == ws.valA) ? ws.valB : ws.valA;
 
@@ -167,20 +422,25 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
             return -1;
         uint32_t G = reinterpret_cast<uint32_t *>(ws.hscal)[0];
 
-        hipLaunchKernelGGL(k_grpkeep, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, G, gsc);
+        hipLaunchKernelGGL(k_grpkeep, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, G, gsc,
+                           ws.lsc);
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u64(gsc, gsc, G, false, d64, ws, st) != 0)
             return -1;
-        hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, gall,
-                           headpos, gsc, offo, offn, Vx, ngid, ws.rank, ws.sa, m, kb_old, round0);
+        if (scan_sum_u64(ws.lsc, ws.lsc, G, false, d64 + 1, ws, st) != 0)
+            return -1;
+        hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, gall, headpos,
+                           gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, kb_old,
+                           round0);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 128, "sa.m") != 0)
             return -1;
-        uint64_t tot = ws.hscal[8];
-        uint32_t Gnew = (uint32_t)tot, mnew = (uint32_t)(tot >> 32);
+        const uint64_t tot = ws.hscal[8], ltot = ws.hscal[9];
+        const uint32_t Gnew = (uint32_t)tot, mnew = (uint32_t)(tot >> 32);
         if (verbose)
-            fprintf(stderr, "sa round %d h=%u m=%u bits=%d groups=%u -> survivors %u in %u groups\n",
-                    ws.stats.sa_rounds, h, m, bits, G, mnew, Gnew);
+            fprintf(stderr, "sa round %d (%s) h=%u m=%u (large %u in %u groups) groups=%u -> "
+                    "survivors %u in %u groups\n", ws.stats.sa_rounds, how, h, m, mL, GL, G, mnew,
+                    Gnew);
         if (mnew == 0)
             break;
         if (h >= n || Gnew == 0) {
@@ -193,7 +453,9 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         K = Kx;
         V = Vx;
         m = mnew;
-        bits = kb + bit_width(Gnew - 1);
+        G_act = Gnew;
+        GL = (uint32_t)ltot;
+        mL = (uint32_t)(ltot >> 32);
         kb_old = kb;
         round0 = 0;
         h = (h > 0x7fffffffu) ? 0xffffffffu : 2 * h;

@@ -217,3 +217,20 @@ def test_encode_blocks_container(salz, block, size):
         want += len(s).to_bytes(4, "little") + s
     assert got == bytes(want)
     assert salz.decode_blocks(got, size) == src.tobytes()
+
+
+@pytest.mark.parametrize("mode", ["global", "segmented"])
+@pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
+                                               ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
+                                               ("runs", 120000, 0, 0), ("zeros", 70000, 0, 0)])
+def test_suffix_sort_modes(ctx, monkeypatch, mode, kind, n, seed, alpha):
+    """Both doubling-round sorts (global radix on (group, rank); LDS sort of small groups +
+    extracted large groups) give the unique suffix array."""
+    monkeypatch.setenv("SALZ_SA_MODE", mode)
+    src = _make(kind, n, seed, alpha)
+    out, d = ctx.encode_dump(src)
+    o = oracle_stages(src)
+    i = _first_diff(d["sa"], o["sa"])
+    assert i < 0, f"{mode}: sa differs at rank {i}"
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and out == ref

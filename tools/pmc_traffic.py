@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--json")
     ap.add_argument("--summary")
     ap.add_argument("--workload", default="bench.py default (100,000,000-byte text block, 1 step)")
+    ap.add_argument("--kind", default="text")
+    ap.add_argument("--size", type=int, default=100_000_000)
     a = ap.parse_args()
     F, W = load(a.fetch), load(a.write)
     lines = [f"{'kernel':28s} {'launches':>8s} {'fetch MB':>10s} {'write MB':>10s} {'traffic MB/launch':>18s}"]
@@ -60,6 +62,8 @@ def main():
     out = {
         "kernel": a.kernel,
         "workload": a.workload,
+        "kind": a.kind,
+        "size": a.size,
         "launches": launches,
         "fetch_bytes_per_launch": round(fetch),
         "write_bytes_per_launch": round(write),
