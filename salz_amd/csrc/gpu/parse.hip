@@ -67,6 +67,22 @@ __global__ __launch_bounds__(kT) void k_cost_seed(uint32_t *cost, uint32_t n, ui
         cost[s] = 3u * (n - (uint32_t)p);
 }
 
+// Target state (cost estimate << 32 | exit) of a factor from p of length len: in-chunk targets
+// come from pst, targets at or past the chunk end b are exits costed by the previous pass.
+__device__ __forceinline__ uint64_t target_state(const uint64_t *pst, const uint32_t *cin,
+                                                 size_t base, uint32_t a, uint32_t b, uint32_t klog,
+                                                 uint32_t p, uint32_t len)
+{
+    if (len < 3u)
+        return 0;
+    const uint32_t q = p + len;
+    return q < b ? pst[base + ((size_t)(q - a) << 6)] : ((uint64_t)cin[sidx(q, klog)] << 32) | q;
+}
+
+// One lane per chunk, positions b-1 down to a. The loads of a step do not depend on the step
+// before it (its targets lie at p + 3 or beyond, finished at least two steps earlier), so
+// they are software-pipelined: candidates are loaded three steps ahead and target states two
+// steps ahead, and a step waits only on memory issued two steps earlier.
 __global__ __launch_bounds__(kT) void k_parse_chunk(
     const uint4 *__restrict__ cand, const uint32_t *__restrict__ cin, uint64_t *__restrict__ pst,
     const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, uint32_t klog,
@@ -80,57 +96,64 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         const uint32_t K = 1u << klog;
         const uint32_t b = (n - a) < K ? n : a + K;
         const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
+        const uint32_t jn = b - a;
+        auto slot = [&](uint32_t j) { return base + ((size_t)j << 6); };
+        const uint4 none = make_uint4(1u, 0u, 1u, 0u);
+        // pipeline registers: c0/o0/t0 = step j, c1/o1/t1 = j-1, c2 = j-2
+        uint4 c0 = cand[slot(jn - 1)];
+        uint8_t o0 = chold[slot(jn - 1)];
+        uint4 c1 = jn >= 2 ? cand[slot(jn - 2)] : none;
+        uint8_t o1 = jn >= 2 ? chold[slot(jn - 2)] : 0;
+        uint4 c2 = jn >= 3 ? cand[slot(jn - 3)] : none;
+        uint64_t t0P = target_state(pst, cin, base, a, b, klog, a + jn - 1, c0.y);
+        uint64_t t0N = target_state(pst, cin, base, a, b, klog, a + jn - 1, c0.w);
+        uint64_t t1P = 0, t1N = 0;
+        if (jn >= 2) {
+            t1P = target_state(pst, cin, base, a, b, klog, a + jn - 2, c1.y);
+            t1N = target_state(pst, cin, base, a, b, klog, a + jn - 2, c1.w);
+        }
         // state of p + 1: cost estimate and exit (p = b - 1 starts at the exit b)
         uint32_t nc = cin[sidx(b, klog)], nex = b;
-        uint32_t j = b - a;
-        uint4 cn = cand[base + ((size_t)(j - 1) << 6)];
-        uint8_t on = chold[base + ((size_t)(j - 1) << 6)];
-        while (j-- > 0) {
+        for (uint32_t j = jn; j-- > 0;) {
             const uint32_t p = a + j;
-            const size_t s = base + ((size_t)j << 6);
-            const uint4 cd = cn;
-            const uint8_t old = on;
-            if (j) {
-                cn = cand[s - 64];
-                on = chold[s - 64];
-            }
             uint32_t best = 9u + nc, ex = nex;
             uint8_t ch = 0;
             if (p != 0) {
-                const bool fP = cd.y >= 3u, fN = cd.w >= 3u;
-                const uint32_t qP = p + cd.y, qN = p + cd.w;
-                // target state (cost estimate << 32 | exit): in-chunk from pst, else exit itself
-                uint64_t vP = 0, vN = 0;
-                if (fP)
-                    vP = qP < b ? pst[base + ((size_t)(qP - a) << 6)]
-                                : ((uint64_t)cin[sidx(qP, klog)] << 32) | qP;
-                if (fN)
-                    vN = qN < b ? pst[base + ((size_t)(qN - a) << 6)]
-                                : ((uint64_t)cin[sidx(qN, klog)] << 32) | qN;
-                const uint32_t cP = (uint32_t)(vP >> 32), eP = (uint32_t)vP;
-                const uint32_t cN = (uint32_t)(vN >> 32), eN = (uint32_t)vN;
-                if (fP) {
-                    const uint32_t alt = factor_bits(cd.x, cd.y) + cP;
+                if (c0.y >= 3u) {
+                    const uint32_t alt = factor_bits(c0.x, c0.y) + (uint32_t)(t0P >> 32);
                     if ((int32_t)alt < (int32_t)best) {
                         best = alt;
-                        ex = eP;
+                        ex = (uint32_t)t0P;
                         ch = 1;
                     }
                 }
-                if (fN) {
-                    const uint32_t alt = factor_bits(cd.z, cd.w) + cN;
+                if (c0.w >= 3u) {
+                    const uint32_t alt = factor_bits(c0.z, c0.w) + (uint32_t)(t0N >> 32);
                     if ((int32_t)alt < (int32_t)best) {
                         best = alt;
-                        ex = eN;
+                        ex = (uint32_t)t0N;
                         ch = 2;
                     }
                 }
             }
-            pst[s] = ((uint64_t)best << 32) | ex;
-            chnew[s] = ch;
-            diff += ch != old;
+            pst[slot(j)] = ((uint64_t)best << 32) | ex;
+            chnew[slot(j)] = ch;
+            diff += ch != o0;
             nc = best;
             nex = ex;
+            // advance the pipeline: step j-1 becomes current, issue loads for j-2 / j-3
+            c0 = c1;
+            o0 = o1;
+            t0P = t1P;
+            t0N = t1N;
+            c1 = c2;
+            if (j >= 2) {
+                o1 = chold[slot(j - 2)];
+                t1P = target_state(pst, cin, base, a, b, klog, p - 2, c1.y);
+                t1N = target_state(pst, cin, base, a, b, klog, p - 2, c1.w);
+            }
+            if (j >= 3)
+                c2 = cand[slot(j - 3)];
         }
     }
     // one atomic per wave

@@ -143,6 +143,31 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     }
 }
 
+// Window plan of the LDS sort, one thread per surviving group (groups are in list order, so
+// the groups that start in one window are consecutive ids): the first group starting in a
+// window writes the window's lo and first group id, the last one its hi. A large group can
+// only be the last to start in its window (it runs past the window's end), so the owned
+// small groups are [lo, hi) with hi = the large group's start in that case.
+struct SegPlan {
+    uint32_t *lo, *hi, *g0;
+};
+
+__global__ void k_seg_plan(const uint64_t *__restrict__ ginfo, uint32_t G, SegPlan plan)
+{
+    size_t g = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (g >= G)
+        return;
+    const uint64_t gi = ginfo[g];
+    const uint32_t size = (uint32_t)(gi >> 32), cs = (uint32_t)gi;
+    const uint32_t w = cs / kSegT;
+    if ((g == 0 || (uint32_t)ginfo[g - 1] / kSegT != w) && size <= kSmall) {
+        plan.lo[w] = cs;
+        plan.g0[w] = (uint32_t)g;
+    }
+    if (g + 1 == G || (uint32_t)ginfo[g + 1] / kSegT != w)
+        plan.hi[w] = size <= kSmall ? cs + size : cs;
+}
+
 // Stable 8-bit LSD passes over bits [12, 12 + nbits) of ITEMS * 256 LDS keys; wave-striped:
 // wave w owns slots [w * ITEMS * 64, (w + 1) * ITEMS * 64), item j covers 64 of them.
 template <int ITEMS>
@@ -218,45 +243,25 @@ __device__ __forceinline__ void seg_lsd(uint64_t *sk, uint32_t (*cnt)[256], uint
 // the owned range [lo, hi) has < kSegCap entries. Sort key: local group << (kb + 12) |
 // rank << 12 | slot; a stable 8-bit LSD pass per digit of the (group, rank) part.
 __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict__ K,
-                                                           uint32_t *__restrict__ V,
-                                                           const uint64_t *__restrict__ ginfo,
-                                                           uint32_t m, int kb)
+                                                           uint32_t *__restrict__ V, SegPlan plan,
+                                                           int kb)
 {
     __shared__ uint64_t sk[kSegCap];
     __shared__ uint32_t sv[kSegCap];
     __shared__ uint32_t cnt[4][256];
     __shared__ uint32_t dstart[256];
     __shared__ uint32_t wsum[4];
-    __shared__ uint32_t s_lo, s_hi, s_glast;
 
     const unsigned tid = threadIdx.x;
-    const uint32_t t0 = blockIdx.x * kSegT;
-    const uint32_t t1 = (m - t0) < kSegT ? m : t0 + kSegT;
-    const uint64_t mask = (1ull << kb) - 1ull;
-    if (tid == 0) {
-        s_lo = 0xffffffffu;
-        s_hi = 0;
-        s_glast = 0;
-    }
-    __syncthreads();
-    for (uint32_t c = t0 + tid; c < t1; c += kSegThreads) {
-        const uint64_t g = K[c] >> kb;
-        if (c == 0 || (K[c - 1] >> kb) != g) {
-            const uint32_t size = (uint32_t)(ginfo[g] >> 32);
-            if (size <= kSmall) {
-                atomicMin(&s_lo, c);
-                atomicMax(&s_hi, c + size);
-                atomicMax(&s_glast, (uint32_t)g);
-            }
-        }
-    }
-    __syncthreads();
-    const uint32_t lo = s_lo, hi = s_hi;
+    const uint32_t w = blockIdx.x;
+    const uint32_t lo = plan.lo[w];
     if (lo == 0xffffffffu)
         return;  // uniform: no small group starts in this window
+    const uint32_t hi = plan.hi[w], g0 = plan.g0[w];
     const uint32_t count = hi - lo;
-    const uint32_t g0 = (uint32_t)(K[lo] >> kb);
-    const int nbits = kb + (32 - __builtin_clz((s_glast - g0) | 1u));
+    const uint64_t mask = (1ull << kb) - 1ull;
+    const uint32_t glast = (uint32_t)(K[hi - 1] >> kb);
+    const int nbits = kb + (32 - __builtin_clz((glast - g0) | 1u));
 
     // slots actually sorted: count rounded up to 1024 (4 waves x 64 lanes x ITEMS / 4 steps)
     const int items = (int)((count + 1023u) / 1024u) * 4;
@@ -390,8 +395,14 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
                     return -1;
             } else {
                 how = "segmented";
-                hipLaunchKernelGGL(k_seg_small, dim3(grid_for(m, kSegT)), dim3(kSegThreads), 0, st,
-                                   K, V, tab.ginfo, m, kb);
+                const uint32_t nwin = grid_for(m, kSegT);
+                uint32_t *pw = reinterpret_cast<uint32_t *>(ws.lsc);  // free during the sort
+                SegPlan plan{pw, pw + nwin, pw + 2 * nwin};
+                SALZ_HIP(hipMemsetAsync(plan.lo, 0xff, sizeof(uint32_t) * nwin, st));
+                hipLaunchKernelGGL(k_seg_plan, dim3(grid_for(G_act, kT)), dim3(kT), 0, st, tab.ginfo,
+                                   G_act, plan);
+                SALZ_LAUNCH_CHECK();
+                hipLaunchKernelGGL(k_seg_small, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, kb);
                 SALZ_LAUNCH_CHECK();
                 if (mL) {
                     hipLaunchKernelGGL(k_extract, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V,
