@@ -93,6 +93,23 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
     return v;
 }
 
+// ---- device index checks ---------------------------------------------------------------
+// Kernels whose addresses come from data (suffix ranks, group tables) check them and, on a
+// violation, set a bit in this device word and skip the access instead of faulting; the
+// host reads the word with the stage's scalars and fails the call (salz_gpu_last_error).
+constexpr size_t kErrWord = 60;  // u32 index into Workspace::dscal
+enum : uint32_t {
+    kErrCommit = 1u, kErrKeys = 2u, kErrSeg = 4u, kErrExtract = 8u, kErrPutback = 16u,
+    kErrPhi = 32u, kErrAnsv = 64u, kErrParse = 128u
+};
+
+__device__ __forceinline__ bool bad_index(bool bad, uint32_t *err, uint32_t code)
+{
+    if (bad)
+        atomicOr(err, code);
+    return bad;
+}
+
 // ---- chunk-interleaved layout of the per-position parse arrays --------------------------
 // The parse walks each chunk of K = 2^klog positions backwards, one lane per chunk, and the
 // 64 lanes of a wave own 64 consecutive chunks (a "tile" of 64K positions). Position

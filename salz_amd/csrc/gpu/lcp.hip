@@ -23,12 +23,16 @@ constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kShortBytes = 32;
 constexpr uint32_t kTaskBytes = 512;
 
-__global__ void k_phi(const uint32_t *__restrict__ sa, uint32_t n, uint32_t *__restrict__ phi)
+__global__ void k_phi(const uint32_t *__restrict__ sa, uint32_t n, uint32_t *__restrict__ phi,
+                      uint32_t *err)
 {
     size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
     if (r >= n)
         return;
-    phi[sa[r]] = r ? sa[r - 1] : kNone;
+    const uint32_t i = sa[r];
+    if (bad_index(i >= n, err, kErrPhi))
+        return;
+    phi[i] = r ? sa[r - 1] : kNone;
 }
 
 __global__ void k_plcp_short(const uint8_t *__restrict__ T, const uint32_t *__restrict__ phi,
@@ -147,7 +151,8 @@ int stage_lcp(Workspace &ws, uint32_t n, uint32_t *lcp_out)
     uint32_t *cnt = reinterpret_cast<uint32_t *>(ws.dscal) + 32;  // 2 counters
 
     ws.stats.lcp_long_bytes = 0;
-    hipLaunchKernelGGL(k_phi, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.sa, n, phi);
+    uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
+    hipLaunchKernelGGL(k_phi, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.sa, n, phi, derr);
     SALZ_LAUNCH_CHECK();
     SALZ_HIP(hipMemsetAsync(cnt, 0, 8, st));
     hipLaunchKernelGGL(k_plcp_short, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, phi, n, plv,
@@ -155,6 +160,10 @@ int stage_lcp(Workspace &ws, uint32_t n, uint32_t *lcp_out)
     SALZ_LAUNCH_CHECK();
     if (read_scalars(ws, 0, 256, "lcp.q0") != 0)
         return -1;
+    if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
+        set_error("lcp: device index check failed (code 0x%x): suffix array corrupt", e);
+        return -1;
+    }
     uint32_t nitems = reinterpret_cast<uint32_t *>(ws.hscal)[32];
 
     uint64_t L = kShortBytes;

@@ -71,11 +71,13 @@ __global__ __launch_bounds__(kT) void k_cost_seed(uint32_t *cost, uint32_t n, ui
 // come from pst, targets at or past the chunk end b are exits costed by the previous pass.
 __device__ __forceinline__ uint64_t target_state(const uint64_t *pst, const uint32_t *cin,
                                                  size_t base, uint32_t a, uint32_t b, uint32_t klog,
-                                                 uint32_t p, uint32_t len)
+                                                 uint32_t p, uint32_t len, uint32_t n, uint32_t *err)
 {
     if (len < 3u)
         return 0;
     const uint32_t q = p + len;
+    if (bad_index(len > n - p, err, kErrParse))
+        return 0;
     return q < b ? pst[base + ((size_t)(q - a) << 6)] : ((uint64_t)cin[sidx(q, klog)] << 32) | q;
 }
 
@@ -86,7 +88,7 @@ __device__ __forceinline__ uint64_t target_state(const uint64_t *pst, const uint
 __global__ __launch_bounds__(kT) void k_parse_chunk(
     const uint4 *__restrict__ cand, const uint32_t *__restrict__ cin, uint64_t *__restrict__ pst,
     const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, uint32_t klog,
-    uint32_t *__restrict__ changed)
+    uint32_t *__restrict__ changed, uint32_t *err)
 {
     const uint32_t c = blockIdx.x * kT + threadIdx.x;  // chunk
     const uint64_t a64 = (uint64_t)c << klog;
@@ -105,12 +107,12 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         uint4 c1 = jn >= 2 ? cand[slot(jn - 2)] : none;
         uint8_t o1 = jn >= 2 ? chold[slot(jn - 2)] : 0;
         uint4 c2 = jn >= 3 ? cand[slot(jn - 3)] : none;
-        uint64_t t0P = target_state(pst, cin, base, a, b, klog, a + jn - 1, c0.y);
-        uint64_t t0N = target_state(pst, cin, base, a, b, klog, a + jn - 1, c0.w);
+        uint64_t t0P = target_state(pst, cin, base, a, b, klog, a + jn - 1, c0.y, n, err);
+        uint64_t t0N = target_state(pst, cin, base, a, b, klog, a + jn - 1, c0.w, n, err);
         uint64_t t1P = 0, t1N = 0;
         if (jn >= 2) {
-            t1P = target_state(pst, cin, base, a, b, klog, a + jn - 2, c1.y);
-            t1N = target_state(pst, cin, base, a, b, klog, a + jn - 2, c1.w);
+            t1P = target_state(pst, cin, base, a, b, klog, a + jn - 2, c1.y, n, err);
+            t1N = target_state(pst, cin, base, a, b, klog, a + jn - 2, c1.w, n, err);
         }
         // state of p + 1: cost estimate and exit (p = b - 1 starts at the exit b)
         uint32_t nc = cin[sidx(b, klog)], nex = b;
@@ -149,8 +151,8 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             c1 = c2;
             if (j >= 2) {
                 o1 = chold[slot(j - 2)];
-                t1P = target_state(pst, cin, base, a, b, klog, p - 2, c1.y);
-                t1N = target_state(pst, cin, base, a, b, klog, p - 2, c1.w);
+                t1P = target_state(pst, cin, base, a, b, klog, p - 2, c1.y, n, err);
+                t1N = target_state(pst, cin, base, a, b, klog, p - 2, c1.w, n, err);
             }
             if (j >= 3)
                 c2 = cand[slot(j - 3)];
@@ -292,11 +294,16 @@ int stage_parse(Workspace &ws, uint32_t n)
         uint8_t *chold = choice[cur], *chnew = choice[cur ^ 1];
         SALZ_HIP(hipMemsetAsync(changed, 0, 4, st));
         hipLaunchKernelGGL(k_parse_chunk, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
-                           cin, ws.pst, chold, chnew, n, klog, changed);
+                           cin, ws.pst, chold, chnew, n, klog, changed,
+                           reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 256, "parse.changed") != 0)
             return -1;
         const uint32_t nchanged = reinterpret_cast<uint32_t *>(ws.hscal)[48];
+        if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
+            set_error("parse: device index check failed (code 0x%x): candidate length past the end", e);
+            return -1;
+        }
         if (verbose)
             fprintf(stderr, "parse it=%d K=%u changed=%u\n", it, ps.chunk, nchanged);
         if (nchanged == 0) {

@@ -102,6 +102,20 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
         set_error("%s", keep.c_str());
         return -1;
     }
+    if (const char *pz = getenv("SALZ_POISON")) {
+        // tests/diagnostics: fill the workspace with a pattern so reads of never-written
+        // memory misbehave deterministically instead of depending on what VRAM held before
+        const int v = atoi(pz) & 0xff;
+        void *ptrs[] = {ws.rank, ws.sa, ws.keyA, ws.keyB, ws.valA, ws.valB, ws.u0, ws.u1, ws.u2,
+                        ws.u3, ws.g64, ws.offA, ws.offB, ws.cand, ws.pst, ws.lsc};
+        size_t sizes[] = {4 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1, 4 * n1, 4 * n1, 4 * n1,
+                          4 * n1, 8 * n1, 4 * n1, 4 * n1, 16 * ws.cap_s, 8 * ws.cap_s, 8 * n1};
+        for (size_t k = 0; k < sizeof(ptrs) / sizeof(ptrs[0]); k++)
+            SALZ_HIP(hipMemset(ptrs[k], v, sizes[k]));
+        SALZ_HIP(hipMemset(ws.lrec, v, 8 * (n1 / 1024 + 2)));
+        SALZ_HIP(hipMemset(ws.lg2g, v, 4 * (n1 / 1024 + 2)));
+        SALZ_HIP(hipMemset(ws.text, v, N + 256));
+    }
     void *h = nullptr;
     SALZ_HIP(hipHostMalloc(&h, 4096, hipHostMallocDefault));
     ws.hscal = static_cast<uint64_t *>(h);

@@ -106,7 +106,7 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
                          const uint32_t *__restrict__ off_old, uint32_t *__restrict__ off_new,
                          uint32_t *__restrict__ nval, uint32_t *__restrict__ ngid,
                          uint32_t *__restrict__ rank, uint32_t *__restrict__ sa, GroupTab tab,
-                         uint32_t m, int kb_old, int round0)
+                         uint32_t m, uint32_t n, int kb_old, int round0, uint32_t *err)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
@@ -116,6 +116,8 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     uint32_t size = headpos[g + 1] - hp;
     uint32_t o = round0 ? 0u : off_old[(uint32_t)(key[c] >> kb_old)];
     uint32_t i = val[c];
+    if (bad_index(i >= n || c + o >= n || hp > c || size > m, err, kErrCommit))
+        return;
     // The first subgroup of an old group keeps the old group's head, so its members' ranks
     // are unchanged; every other rank (and all of round 0) is written.
     const bool same = !round0 && (hp == 0 || (key[hp - 1] >> kb_old) != (key[hp] >> kb_old));
@@ -244,7 +246,7 @@ __device__ __forceinline__ void seg_lsd(uint64_t *sk, uint32_t (*cnt)[256], uint
 // rank << 12 | slot; a stable 8-bit LSD pass per digit of the (group, rank) part.
 __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict__ K,
                                                            uint32_t *__restrict__ V, SegPlan plan,
-                                                           int kb)
+                                                           uint32_t m, int kb, uint32_t *err)
 {
     __shared__ uint64_t sk[kSegCap];
     __shared__ uint32_t sv[kSegCap];
@@ -258,6 +260,8 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
     if (lo == 0xffffffffu)
         return;  // uniform: no small group starts in this window
     const uint32_t hi = plan.hi[w], g0 = plan.g0[w];
+    if (bad_index(hi > m || hi <= lo || hi - lo >= kSegCap, err, kErrSeg))
+        return;
     const uint32_t count = hi - lo;
     const uint64_t mask = (1ull << kb) - 1ull;
     const uint32_t glast = (uint32_t)(K[hi - 1] >> kb);
@@ -289,11 +293,23 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
     }
 }
 
+// SALZ_CHECK_SA=1: every position must appear exactly once in the suffix array.
+__global__ void k_sa_check(const uint32_t *__restrict__ sa, uint32_t n, uint32_t *seen,
+                           uint32_t *err)
+{
+    size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (r >= n)
+        return;
+    const uint32_t i = sa[r];
+    if (i >= n || atomicAdd(&seen[i], 1u) != 0)
+        atomicOr(err, 0x100u);
+}
+
 // Members of large groups -> contiguous extracted array, key (large-group id, rank).
 __global__ void k_extract(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
                           const uint64_t *__restrict__ ginfo, const uint32_t *__restrict__ gl,
-                          const uint64_t *__restrict__ lrec, uint32_t m, int kb,
-                          uint64_t *__restrict__ KC, uint32_t *__restrict__ VC)
+                          const uint64_t *__restrict__ lrec, uint32_t m, uint32_t mL, int kb,
+                          uint64_t *__restrict__ KC, uint32_t *__restrict__ VC, uint32_t *err)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
@@ -305,6 +321,8 @@ __global__ void k_extract(const uint64_t *__restrict__ K, const uint32_t *__rest
         return;
     const uint32_t lg = gl[g];
     const uint32_t dst = (uint32_t)(lrec[lg] >> 32) + ((uint32_t)c - (uint32_t)gi);
+    if (bad_index(dst >= mL, err, kErrExtract))
+        return;
     KC[dst] = ((uint64_t)lg << kb) | (key & ((1ull << kb) - 1ull));
     VC[dst] = V[c];
 }
@@ -312,27 +330,36 @@ __global__ void k_extract(const uint64_t *__restrict__ K, const uint32_t *__rest
 // Sorted large groups back to their places in the active list, original key format.
 __global__ void k_putback(const uint64_t *__restrict__ KS, const uint32_t *__restrict__ VS,
                           const uint64_t *__restrict__ lrec, const uint32_t *__restrict__ lg2g,
-                          uint32_t mL, int kb, uint64_t *__restrict__ K, uint32_t *__restrict__ V)
+                          uint32_t mL, uint32_t GL, uint32_t m, int kb, uint64_t *__restrict__ K,
+                          uint32_t *__restrict__ V, uint32_t *err)
 {
     size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
     if (x >= mL)
         return;
     const uint64_t key = KS[x];
     const uint32_t lg = (uint32_t)(key >> kb);
+    if (bad_index(lg >= GL, err, kErrPutback))
+        return;
     const uint64_t r = lrec[lg];
     const uint32_t orig = (uint32_t)r + ((uint32_t)x - (uint32_t)(r >> 32));
+    if (bad_index(orig >= m, err, kErrPutback))
+        return;
     K[orig] = ((uint64_t)lg2g[lg] << kb) | (key & ((1ull << kb) - 1ull));
     V[orig] = VS[x];
 }
 
 __global__ void k_keys(const uint32_t *__restrict__ nval, const uint32_t *__restrict__ ngid,
-                       const uint32_t *__restrict__ rank, uint32_t m, uint32_t h, int kb,
-                       uint64_t *__restrict__ key)
+                       const uint32_t *__restrict__ rank, uint32_t m, uint32_t n, uint32_t h, int kb,
+                       uint64_t *__restrict__ key, uint32_t *err)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
         return;
     uint32_t i = nval[c];
+    if (bad_index((uint64_t)i + h > n, err, kErrKeys)) {
+        key[c] = 0;
+        return;
+    }
     key[c] = ((uint64_t)ngid[c] << kb) | (uint64_t)rank[i + h];
 }
 
@@ -350,6 +377,8 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     uint64_t *gsc = ws.g64;
     uint32_t *d32 = reinterpret_cast<uint32_t *>(ws.dscal);
     uint64_t *d64 = ws.dscal + 8;
+    uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
+    SALZ_HIP(hipMemsetAsync(derr, 0, sizeof(uint32_t), st));
     // Scratch borrowed from later stages (free while the suffix array is built): the
     // extracted large groups live in pst (keys) and cand (values), the group table in cand.
     uint8_t *cb = reinterpret_cast<uint8_t *>(ws.cand);
@@ -402,18 +431,19 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
                 hipLaunchKernelGGL(k_seg_plan, dim3(grid_for(G_act, kT)), dim3(kT), 0, st, tab.ginfo,
                                    G_act, plan);
                 SALZ_LAUNCH_CHECK();
-                hipLaunchKernelGGL(k_seg_small, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, kb);
+                hipLaunchKernelGGL(k_seg_small, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, m, kb,
+                                   derr);
                 SALZ_LAUNCH_CHECK();
                 if (mL) {
                     hipLaunchKernelGGL(k_extract, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V,
-                                       tab.ginfo, tab.gl, tab.lrec, m, kb, KC, VC);
+                                       tab.ginfo, tab.gl, tab.lrec, m, mL, kb, KC, VC, derr);
                     SALZ_LAUNCH_CHECK();
                     uint64_t *KS = KC;
                     uint32_t *VS = VC;
                     if (radix_sort_pairs(&KS, &VS, Kx, Vx, mL, 0, bits_large, ws, st) != 0)
                         return -1;
                     hipLaunchKernelGGL(k_putback, dim3(grid_for(mL, kT)), dim3(kT), 0, st, KS, VS,
-                                       tab.lrec, tab.lg2g, mL, kb, K, V);
+                                       tab.lrec, tab.lg2g, mL, GL, m, kb, K, V, derr);
                     SALZ_LAUNCH_CHECK();
                 }
             }
@@ -441,11 +471,16 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         if (scan_sum_u64(ws.lsc, ws.lsc, G, false, d64 + 1, ws, st) != 0)
             return -1;
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, gall, headpos,
-                           gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, kb_old,
-                           round0);
+                           gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, kb_old,
+                           round0, derr);
         SALZ_LAUNCH_CHECK();
-        if (read_scalars(ws, 0, 128, "sa.m") != 0)
+        if (read_scalars(ws, 0, 256, "sa.m") != 0)
             return -1;
+        if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
+            set_error("suffix sort: device index check failed (code 0x%x, round %d)", e,
+                      ws.stats.sa_rounds);
+            return -1;
+        }
         const uint64_t tot = ws.hscal[8], ltot = ws.hscal[9];
         const uint32_t Gnew = (uint32_t)tot, mnew = (uint32_t)(tot >> 32);
         if (verbose)
@@ -459,7 +494,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
             return -1;
         }
         hipLaunchKernelGGL(k_keys, dim3(grid_for(mnew, kT)), dim3(kT), 0, st, Vx, ngid, ws.rank,
-                           mnew, h, kb, Kx);
+                           mnew, n, h, kb, Kx, derr);
         SALZ_LAUNCH_CHECK();
         K = Kx;
         V = Vx;
@@ -473,6 +508,19 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         uint32_t *t = offo;
         offo = offn;
         offn = t;
+    }
+    static const bool check = getenv("SALZ_CHECK_SA") != nullptr;
+    if (check) {
+        SALZ_HIP(hipMemsetAsync(ws.u0, 0, sizeof(uint32_t) * n, st));
+        hipLaunchKernelGGL(k_sa_check, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.sa, n, ws.u0, derr);
+        SALZ_LAUNCH_CHECK();
+        if (read_scalars(ws, 0, 256, "sa.check") != 0)
+            return -1;
+        if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
+            set_error("suffix sort: result is not a permutation (code 0x%x, %d rounds)", e,
+                      ws.stats.sa_rounds);
+            return -1;
+        }
     }
     return 0;
 }
