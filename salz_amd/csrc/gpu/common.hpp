@@ -135,13 +135,12 @@ __host__ __device__ __forceinline__ uint64_t spos(size_t s, uint32_t klog)
 // Unaligned little-endian 8-byte load from an 8-byte-aligned, padded byte buffer.
 __device__ __forceinline__ uint64_t load_u64_any(const uint8_t *base, size_t pos)
 {
+    // Both words are loaded unconditionally (the buffer is padded): no exec-masked second
+    // load, and the shift pair (b << 1) << (63 - sh) is 0 for sh == 0.
     const uint64_t *w = reinterpret_cast<const uint64_t *>(base + (pos & ~(size_t)7));
-    unsigned sh = (unsigned)(pos & 7) * 8u;
-    uint64_t a = w[0];
-    if (sh == 0)
-        return a;
-    uint64_t b = w[1];
-    return (a >> sh) | (b << (64u - sh));
+    const unsigned sh = (unsigned)(pos & 7) * 8u;
+    const uint64_t a = w[0], b = w[1];
+    return (a >> sh) | ((b << 1) << (63u - sh));
 }
 
 }  // namespace salz

@@ -66,7 +66,8 @@ struct Workspace {
     void *scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
     uint64_t *dscal = nullptr;  // device scalars
-    uint64_t *hscal = nullptr;  // pinned host mirror
+    uint64_t *hscal = nullptr;      // pinned host mirror (mapped)
+    uint64_t *hscal_dev = nullptr;  // its device-side address
     hipStream_t stream = nullptr;
     bool own_stream = false;
     bool timing = false;

@@ -33,15 +33,52 @@ void set_error(const char *fmt, ...)
     va_end(ap);
 }
 
-template <typename T> static int dalloc(T **p, size_t count)
+// SALZ_GUARD=1 (diagnostics): every workspace buffer gets a guard zone filled with a
+// pattern; guard_check() reports the first buffer whose zone was written.
+constexpr size_t kGuardBytes = 1 << 20;
+struct Guard {
+    const char *name;
+    uint8_t *zone;
+};
+static thread_local std::vector<Guard> *g_guards = nullptr;
+static bool guard_on() { static const bool on = getenv("SALZ_GUARD") != nullptr; return on; }
+
+template <typename T> static int dalloc_named(T **p, size_t count, const char *name)
 {
     void *q = nullptr;
-    hipError_t e = hipMalloc(&q, count * sizeof(T) + 256);
+    const size_t bytes = count * sizeof(T) + 256;
+    hipError_t e = hipMalloc(&q, bytes + (guard_on() ? kGuardBytes : 0));
     if (e != hipSuccess) {
         set_error("hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
         return -1;
     }
+    if (guard_on()) {
+        uint8_t *zone = static_cast<uint8_t *>(q) + bytes;
+        (void)hipMemset(zone, 0xA5, kGuardBytes);
+        if (!g_guards)
+            g_guards = new std::vector<Guard>();
+        g_guards->push_back({name, zone});
+    }
     *p = static_cast<T *>(q);
+    return 0;
+}
+#define dalloc(p, count) dalloc_named(p, count, #p)
+
+int guard_check(Workspace &ws, const char *stage)
+{
+    if (!guard_on() || !g_guards)
+        return 0;
+    (void)hipStreamSynchronize(ws.stream);
+    std::vector<uint8_t> h(kGuardBytes);
+    for (const Guard &g : *g_guards) {
+        (void)hipMemcpy(h.data(), g.zone, kGuardBytes, hipMemcpyDeviceToHost);
+        for (size_t i = 0; i < kGuardBytes; i++)
+            if (h[i] != 0xA5) {
+                fprintf(stderr, "GUARD: %s overrun after %s at +%zu\n", g.name, stage, i);
+                set_error("guard zone of %s written after %s", g.name, stage);
+                return -1;
+            }
+    }
     return 0;
 }
 
@@ -116,9 +153,15 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
         SALZ_HIP(hipMemset(ws.lg2g, v, 4 * (n1 / 1024 + 2)));
         SALZ_HIP(hipMemset(ws.text, v, N + 256));
     }
+    // Host mirror of the device scalars, mapped into the device: a one-wave kernel on the
+    // workspace's stream stores the words there (read_scalars), so no runtime copy path
+    // (and none of its staging buffers) is shared between concurrently encoding contexts.
     void *h = nullptr;
-    SALZ_HIP(hipHostMalloc(&h, 4096, hipHostMallocDefault));
+    SALZ_HIP(hipHostMalloc(&h, 4096, hipHostMallocMapped | hipHostMallocCoherent));
     ws.hscal = static_cast<uint64_t *>(h);
+    void *hd = nullptr;
+    SALZ_HIP(hipHostGetDevicePointer(&hd, h, 0));
+    ws.hscal_dev = static_cast<uint64_t *>(hd);
     SALZ_HIP(hipStreamCreateWithFlags(&ws.stream, hipStreamNonBlocking));
     ws.own_stream = true;
     for (hipEvent_t &e : ws.ev)
@@ -129,16 +172,100 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
     return 0;
 }
 
+__global__ void k_read_scalars(const uint32_t *__restrict__ d, uint32_t *h, uint32_t words)
+{
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+        __hip_atomic_store(&h[i], d[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 int read_scalars(Workspace &ws, size_t off, size_t bytes, const char *tag)
 {
-    uint8_t *h = reinterpret_cast<uint8_t *>(ws.hscal) + off;
-    const uint8_t *d = reinterpret_cast<const uint8_t *>(ws.dscal) + off;
-    SALZ_HIP(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ws.stream));
+    (void)tag;
+    const uint32_t *d = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(ws.dscal) + off);
+    uint32_t *h = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(ws.hscal_dev) + off);
+    hipLaunchKernelGGL(k_read_scalars, dim3(1), dim3(64), 0, ws.stream, d, h,
+                       (uint32_t)((bytes + 3) / 4));
+    SALZ_LAUNCH_CHECK();
     SALZ_HIP(hipStreamSynchronize(ws.stream));
     return 0;
 }
 
 enum : int { EV_START, EV_UP, EV_SA, EV_LCP, EV_ANSV, EV_PARSE, EV_EMIT };
+
+// SALZ_CHECK_STAGES=1 (diagnostics): bound checks of the LCP array and the candidates.
+__global__ void k_check_lcp(const uint32_t *sa, const uint32_t *lcp, const uint8_t *T, uint32_t n,
+                            uint32_t *err)
+{
+    size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (r == 0 || r >= n)
+        return;
+    const uint32_t a = sa[r - 1], b = sa[r], l = lcp[r];
+    const uint32_t mx = a > b ? a : b;
+    bool bad = l > n - mx;
+    if (!bad && a + l < n && b + l < n && T[a + l] >= T[b + l])
+        bad = true;  // adjacent suffixes must differ right after the LCP, in order
+    if (!bad && l > 0 && T[a + l - 1] != T[b + l - 1])
+        bad = true;
+    if (bad)
+        atomicOr(err, 0x200u);
+}
+
+// adjacent suffixes in order on their first 16 bytes (end of text sorts first)
+__global__ void k_check_sa(const uint32_t *sa, const uint8_t *T, uint32_t n, uint32_t *err)
+{
+    size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (r == 0 || r >= n)
+        return;
+    const uint32_t a = sa[r - 1], b = sa[r];
+    for (uint32_t k = 0; k < 16; k++) {
+        const bool ea = a + k >= n, eb = b + k >= n;
+        if (ea || eb) {
+            if (!ea)  // b ended first: b < a, out of order
+                atomicOr(err, 0x800u);
+            return;
+        }
+        if (T[a + k] != T[b + k]) {
+            if (T[a + k] > T[b + k])
+                atomicOr(err, 0x800u);
+            return;
+        }
+    }
+}
+
+__global__ void k_check_cand(const uint4 *cand, uint32_t n, uint32_t klog, uint32_t *err)
+{
+    size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n)
+        return;
+    const uint4 c = cand[sidx((uint32_t)p, klog)];
+    if (c.y > n - p || c.w > n - p || c.x == 0 || c.z == 0 || c.x > p + 1 || c.z > p + 1)
+        atomicOr(err, 0x400u);
+}
+
+static int check_stage(Workspace &ws, uint32_t n, int which)
+{
+    static const bool on = getenv("SALZ_CHECK_STAGES") != nullptr;
+    if (!on)
+        return 0;
+    uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
+    if (which == 2)
+        hipLaunchKernelGGL(k_check_sa, dim3(grid_for(n, 256)), dim3(256), 0, ws.stream, ws.sa,
+                           ws.text, n, derr);
+    else if (which == 0)
+        hipLaunchKernelGGL(k_check_lcp, dim3(grid_for(n, 256)), dim3(256), 0, ws.stream, ws.sa,
+                           ws.u3, ws.text, n, derr);
+    else
+        hipLaunchKernelGGL(k_check_cand, dim3(grid_for(n, 256)), dim3(256), 0, ws.stream, ws.cand,
+                           n, ws.klog, derr);
+    if (read_scalars(ws, 0, 256, "check") != 0)
+        return -1;
+    if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
+        set_error("stage check after %s failed (code 0x%x)",
+                  which == 2 ? "sa" : which == 0 ? "lcp" : "ansv", e);
+        return -1;
+    }
+    return 0;
+}
 
 static int mark(Workspace &ws, int which)
 {
@@ -232,17 +359,17 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t N
     SALZ_HIP(hipMemsetAsync(ws.text + N, 0, 128, st));
     ws.klog = parse_chunk_log(n);
     if (mark(ws, EV_UP)) return -1;
-    if (stage_suffix_array(ws, n)) return -1;
+    if (stage_suffix_array(ws, n) || guard_check(ws, "sa") || check_stage(ws, n, 2)) return -1;
     if (mark(ws, EV_SA)) return -1;
     if (dump_after_sa(ws, n, dump)) return -1;
-    if (stage_lcp(ws, n, ws.u3)) return -1;
+    if (stage_lcp(ws, n, ws.u3) || guard_check(ws, "lcp") || check_stage(ws, n, 0)) return -1;
     if (mark(ws, EV_LCP)) return -1;
-    if (stage_candidates(ws, n, ws.u3)) return -1;
+    if (stage_candidates(ws, n, ws.u3) || guard_check(ws, "ansv") || check_stage(ws, n, 1)) return -1;
     if (mark(ws, EV_ANSV)) return -1;
-    if (stage_parse(ws, n)) return -1;
+    if (stage_parse(ws, n) || guard_check(ws, "parse")) return -1;
     if (mark(ws, EV_PARSE)) return -1;
     if (dump_after_parse(ws, n, dump)) return -1;
-    if (stage_emit(ws, n, (uint32_t)N, dst, cap, out_len)) return -1;
+    if (stage_emit(ws, n, (uint32_t)N, dst, cap, out_len) || guard_check(ws, "emit")) return -1;
     if (mark(ws, EV_EMIT)) return -1;
     SALZ_HIP(hipStreamSynchronize(st));
     if (ws.timing) {
@@ -440,23 +567,28 @@ int salz_gpu_encode_dump(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, 
 
 // ---- default contexts behind salz_encode_safe ----------------------------------------------
 
+// Cached contexts: slot 0 of each device serves salz_encode_safe; salz_encode_blocks uses
+// slots 0..k-1 so that k blocks are in flight per device (their own streams and workspaces).
+constexpr int kMaxSlots = 8;
 static std::mutex g_default_mu;
-static std::vector<salz_gpu_ctx *> g_default;
+static std::vector<salz_gpu_ctx *> g_default;  // [device * kMaxSlots + slot]
 
-static salz_gpu_ctx *default_ctx(int device, size_t need)
+static salz_gpu_ctx *default_ctx(int device, size_t need, int slot = 0)
 {
     std::lock_guard<std::mutex> lk(g_default_mu);
     if (g_default.empty()) {
         int n = salz_gpu_device_count();
-        g_default.assign(n > 0 ? (size_t)n : 0, nullptr);
+        g_default.assign(n > 0 ? (size_t)n * kMaxSlots : 0, nullptr);
     }
-    if (device < 0 || (size_t)device >= g_default.size()) {
+    if (device < 0 || (size_t)device * kMaxSlots >= g_default.size() || slot < 0 ||
+        slot >= kMaxSlots) {
         set_error("no usable HIP device (gfx950) for salz_encode_safe");
         return nullptr;
     }
-    if (!g_default[device])
-        g_default[device] = salz_gpu_ctx_create(device, need);
-    return g_default[device];
+    salz_gpu_ctx *&c = g_default[(size_t)device * kMaxSlots + slot];
+    if (!c)
+        c = salz_gpu_ctx_create(device, need);
+    return c;
 }
 
 // Called by salz_encode_safe (salz.c) after argument checks.
@@ -495,18 +627,23 @@ int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, ui
         return -1;
     }
     int ndev = (n_devices <= 0 || n_devices > avail) ? avail : n_devices;
+    // Blocks in flight per device: small blocks are dominated by per-block launch and
+    // host-sync latency, so several streams (one context each) overlap them on one GPU.
+    const int per_dev = block_size >= (64u << 20) ? 1 : block_size >= (8u << 20) ? 2 : block_size >= (1u << 20) ? 4 : kMaxSlots;
     // Block count follows the reference CLI loop (programs/salzcli.c:143-179): it always
     // encodes the trailing fread() chunk, even an empty one when src_len is a multiple.
     size_t nblocks = src_len / block_size + 1;
     std::vector<std::vector<uint8_t>> streams(nblocks);
     std::vector<int> rcs(nblocks, -1);
     std::atomic<size_t> next{0};
-    std::vector<std::string> errs((size_t)ndev);
-    auto worker = [&](int dev) {
+    std::vector<std::string> werr((size_t)ndev * per_dev);
+    auto worker = [&](int dev, int slot) {
+        // cached contexts (workspace reused across calls), one per block in flight
         size_t need = block_size < src_len ? block_size : src_len;
-        salz_gpu_ctx *c = salz_gpu_ctx_create(dev, need < 9 ? 9 : need);
+        salz_gpu_ctx *c = default_ctx(dev, need < 9 ? 9 : need, slot);
+        std::string &err = werr[(size_t)dev * per_dev + slot];
         if (!c) {
-            errs[dev] = g_err;
+            err = g_err;
             return;
         }
         for (;;) {
@@ -523,24 +660,24 @@ int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, ui
                 rcs[b] = encode_host_locked(c, src + off, len, streams[b].data(), &out, nullptr);
             }
             if (rcs[b] != 0) {
-                errs[dev] = g_err;
+                err = g_err;
                 next.store(nblocks);
                 break;
             }
             streams[b].resize(out);
         }
-        salz_gpu_ctx_destroy(c);
     };
     std::vector<std::thread> th;
     for (int d = 0; d < ndev; d++)
-        th.emplace_back(worker, d);
+        for (int k = 0; k < per_dev; k++)
+            th.emplace_back(worker, d, k);
     for (auto &t : th)
         t.join();
     size_t need = 8;
     for (size_t b = 0; b < nblocks; b++) {
         if (rcs[b] != 0) {
             std::string e;
-            for (auto &s : errs)
+            for (auto &s : werr)
                 if (!s.empty())
                     e = s;
             set_error("block %zu failed: %s", b, e.c_str());

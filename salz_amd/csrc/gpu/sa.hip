@@ -305,6 +305,81 @@ __global__ void k_sa_check(const uint32_t *__restrict__ sa, uint32_t n, uint32_t
         atomicOr(err, 0x100u);
 }
 
+// SALZ_CHECK_ROUNDS=1 (diagnostics): per-round invariants of the suffix sorter.
+__global__ void k_dbg_sorted(const uint64_t *__restrict__ K, uint32_t m, uint32_t *err, uint32_t code)
+{
+    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (c == 0 || c >= m)
+        return;
+    if (K[c - 1] > K[c])
+        atomicOr(err, code);
+}
+
+__global__ void k_dbg_pairs(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
+                            const uint32_t *__restrict__ rank, const uint8_t *__restrict__ T,
+                            uint32_t m, uint32_t n, uint32_t h, int kb, int round0, uint32_t *err)
+{
+    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (c >= m)
+        return;
+    const uint32_t i = V[c];
+    if (i >= n) {
+        atomicOr(err, 0x10000u);
+        return;
+    }
+    uint64_t want;
+    if (round0) {
+        uint64_t w = load_u64_any(T, i);
+        const uint32_t left = n - i;
+        if (left < 8)
+            w &= (1ull << (8u * left)) - 1ull;
+        want = __builtin_bswap64(w);
+        const uint64_t got = K[c];
+        if (got != want) {
+            atomicOr(err, 0x20000u);
+            if (atomicCAS(err + 2, 0u, 1u) == 0u) {
+                err[4] = (uint32_t)c;
+                err[5] = i;
+                err[6] = (uint32_t)(got >> 32);
+                err[7] = (uint32_t)got;
+                err[8] = (uint32_t)(want >> 32);
+                err[9] = (uint32_t)want;
+                err[10] = atomicAdd(err + 3, 0u);
+            }
+            atomicAdd(err + 3, 1u);
+        }
+    } else if ((K[c] & ((1ull << kb) - 1ull)) != rank[i + h]) {
+        atomicOr(err, 0x40000u);
+    }
+}
+
+__global__ void k_dbg_heads(const uint32_t *__restrict__ hf, const uint32_t *__restrict__ gall,
+                            const uint32_t *__restrict__ headpos, uint32_t m, uint32_t *err)
+{
+    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (c >= m)
+        return;
+    const uint32_t g = gall[c];
+    const uint32_t prev = c ? gall[c - 1] : 0u;
+    if (g - prev != hf[c] || g == 0)
+        atomicOr(err, 0x2000u);
+    else if (headpos[g - 1] > c || headpos[g] <= c)
+        atomicOr(err, 0x4000u);
+}
+
+__global__ void k_dbg_gsc(const uint32_t *__restrict__ headpos, const uint64_t *__restrict__ gsc,
+                          uint32_t G, uint64_t total, uint32_t *err)
+{
+    size_t g = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (g >= G)
+        return;
+    const uint32_t size = headpos[g + 1] - headpos[g];
+    const uint64_t want = size >= 2 ? (((uint64_t)size << 32) | 1ull) : 0ull;
+    const uint64_t nxt = g + 1 < G ? gsc[g + 1] : total;
+    if (nxt - gsc[g] != want)
+        atomicOr(err, 0x8000u);
+}
+
 // Members of large groups -> contiguous extracted array, key (large-group id, rank).
 __global__ void k_extract(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
                           const uint64_t *__restrict__ ginfo, const uint32_t *__restrict__ gl,
@@ -378,7 +453,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     uint32_t *d32 = reinterpret_cast<uint32_t *>(ws.dscal);
     uint64_t *d64 = ws.dscal + 8;
     uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
-    SALZ_HIP(hipMemsetAsync(derr, 0, sizeof(uint32_t), st));
+    SALZ_HIP(hipMemsetAsync(derr, 0, sizeof(uint32_t) * 12, st));
     // Scratch borrowed from later stages (free while the suffix array is built): the
     // extracted large groups live in pst (keys) and cand (values), the group table in cand.
     uint8_t *cb = reinterpret_cast<uint8_t *>(ws.cand);
@@ -387,9 +462,23 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
                  reinterpret_cast<uint32_t *>(cb + 12 * ws.cap_s), ws.lrec, ws.lg2g};
     uint64_t *KC = ws.pst;
 
+    static const bool dbg_rounds = getenv("SALZ_CHECK_ROUNDS") != nullptr;
     SALZ_HIP(hipMemsetAsync(ws.rank + n, 0, sizeof(uint32_t), st));  // rank[n] = 0
     hipLaunchKernelGGL(k_sa_init, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, n, K, V);
     SALZ_LAUNCH_CHECK();
+    if (dbg_rounds) {
+        hipLaunchKernelGGL(k_dbg_pairs, dim3(grid_for(n, kT)), dim3(kT), 0, st, K, V, ws.rank, ws.text, n, n,
+                           0u, 0, 1, derr);
+        SALZ_LAUNCH_CHECK();
+        if (read_scalars(ws, 0, 512, "sa.init") != 0)
+            return -1;
+        if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
+            const uint32_t *d = reinterpret_cast<uint32_t *>(ws.hscal) + kErrWord;
+            set_error("suffix sort: init pairs check failed (code 0x%x): %u bad; first c=%u i=%u key "
+                      "%08x%08x want %08x%08x", e, d[3], d[4], d[5], d[6], d[7], d[8], d[9]);
+            return -1;
+        }
+    }
 
     uint32_t m = n, h = 8, G_act = 0, GL = 0, mL = 0;
     int kb_old = 0, round0 = 1;
@@ -404,6 +493,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         uint64_t *Kx = (K == ws.keyA) ? ws.keyB : ws.keyA;
         uint32_t *Vx = (V == ws.valA) ? ws.valB : ws.valA;
         const char *how = "global";
+        bool seg_round = false;
         if (round0) {
             if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, 64, ws, st) != 0)
                 return -1;
@@ -424,6 +514,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
                     return -1;
             } else {
                 how = "segmented";
+                seg_round = true;
                 const uint32_t nwin = grid_for(m, kSegT);
                 uint32_t *pw = reinterpret_cast<uint32_t *>(ws.lsc);  // free during the sort
                 SegPlan plan{pw, pw + nwin, pw + 2 * nwin};
@@ -451,6 +542,13 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         Kx = (K == ws.keyA) ? ws.keyB : ws.keyA;
         Vx = (V == ws.valA) ? ws.valB : ws.valA;
 
+        if (dbg_rounds && !seg_round) {
+            hipLaunchKernelGGL(k_dbg_sorted, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, m, derr, 0x1000u);
+            SALZ_LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_dbg_pairs, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, ws.rank, ws.text, m,
+                               n, h / 2, kb, round0, derr);
+            SALZ_LAUNCH_CHECK();
+        }
         hipLaunchKernelGGL(k_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m, n, round0,
                            hf);
         SALZ_LAUNCH_CHECK();
@@ -462,6 +560,10 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         if (read_scalars(ws, 0, 64, "sa.G") != 0)
             return -1;
         uint32_t G = reinterpret_cast<uint32_t *>(ws.hscal)[0];
+        if (dbg_rounds) {
+            hipLaunchKernelGGL(k_dbg_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, hf, gall, headpos, m, derr);
+            SALZ_LAUNCH_CHECK();
+        }
 
         hipLaunchKernelGGL(k_grpkeep, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, G, gsc,
                            ws.lsc);
@@ -470,6 +572,12 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
             return -1;
         if (scan_sum_u64(ws.lsc, ws.lsc, G, false, d64 + 1, ws, st) != 0)
             return -1;
+        if (dbg_rounds) {
+            if (read_scalars(ws, 0, 256, "sa.dbg") != 0)
+                return -1;
+            hipLaunchKernelGGL(k_dbg_gsc, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, gsc, G, ws.hscal[8], derr);
+            SALZ_LAUNCH_CHECK();
+        }
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, gall, headpos,
                            gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, kb_old,
                            round0, derr);

@@ -3,10 +3,12 @@
 Every comparison is bit-exact (integer / byte work). Stage arrays are compared one by one
 so a mismatch names the stage (SA, PSV/NSV, lengths, decisions, costs, bytes).
 """
+import os
+
 import numpy as np
 import pytest
 
-from tests.helpers import enc_max, gen, golden, oracle_decode, oracle_encode, oracle_stages, sha256
+from tests.helpers import ROOT, enc_max, gen, golden, oracle_decode, oracle_encode, oracle_stages, sha256
 
 pytestmark = pytest.mark.gpu
 
@@ -234,3 +236,26 @@ def test_suffix_sort_modes(ctx, monkeypatch, mode, kind, n, seed, alpha):
     assert i < 0, f"{mode}: sa differs at rank {i}"
     rc, ref = oracle_encode(src)
     assert rc == 0 and out == ref
+
+
+def test_cli_roundtrip_matches_reference_container(salz, tmp_path):
+    """salz_amd/salz (programs/salzcli.c mirror): -3 compresses to the reference container
+    (blocks of 1 << 18, each the oracle's stream), -d restores the file, -k keeps the input."""
+    import subprocess
+
+    cli = os.path.join(ROOT, "salz_amd", "salz")
+    src = gen("text", 700_001, 6)
+    f = tmp_path / "doc.txt"
+    f.write_bytes(src.tobytes())
+    subprocess.run([cli, "-3", "-k", "-q", str(f)], check=True, timeout=120)
+    packed = (tmp_path / "doc.txt.salz").read_bytes()
+    block = 1 << 18
+    want = bytearray(b"ZLAS" + block.to_bytes(4, "little"))
+    for off in range(0, len(src), block):
+        rc, s = oracle_encode(src[off:off + block])
+        assert rc == 0
+        want += len(s).to_bytes(4, "little") + s
+    assert packed == bytes(want)
+    f.unlink()
+    subprocess.run([cli, "-d", "-q", str(tmp_path / "doc.txt.salz")], check=True, timeout=120)
+    assert f.read_bytes() == src.tobytes()

@@ -1,14 +1,10 @@
 set -o pipefail
 mkdir -p gpurun_out/dg
-for k in 1 2 3 4; do
-timeout -k 10 200 python bench.py --workload silesia --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/dg/s$k.json 2> gpurun_out/dg/s$k.err
-echo "plain $k rc=$? $(tail -1 gpurun_out/dg/s$k.err | cut -c1-200)"
-SALZ_CHECK_SA=1 timeout -k 10 200 python bench.py --workload silesia --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/dg/c$k.json 2> gpurun_out/dg/c$k.err
-echo "checked $k rc=$? $(tail -1 gpurun_out/dg/c$k.err | cut -c1-200)"
-done
-timeout -k 10 200 python bench.py --no-cpu-baseline --kind mixed --steps 2 --warmup 1 > gpurun_out/dg/m.json 2> gpurun_out/dg/m.err
-echo "mixed rc=$?"
-for k in 5 6; do
-timeout -k 10 200 python bench.py --workload silesia --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/dg/s$k.json 2> gpurun_out/dg/s$k.err
-echo "plain $k rc=$? $(tail -1 gpurun_out/dg/s$k.err | cut -c1-200)"
-done
+export SALZ_CHECK_STAGES=1
+timeout -k 10 200 python tools/diag_concurrency.py --threads 4 --iters 30 --device > gpurun_out/dg/c_text.log 2>&1 &&
+timeout -k 10 200 python tools/diag_concurrency.py --threads 4 --iters 30 --device --kind mixed --size 2000001 > gpurun_out/dg/c_mixed.log 2>&1 &&
+timeout -k 10 200 python tools/diag_concurrency.py --threads 3 --iters 15 --device --kind text --size 9000001 > gpurun_out/dg/c_text9.log 2>&1 &&
+timeout -k 10 200 python tools/diag_concurrency.py --threads 4 --iters 40 --kind mixed --size 300001 > gpurun_out/dg/c_small.log 2>&1
+rc=$?
+for f in c_text c_mixed c_text9 c_small; do echo "== $f"; tail -2 gpurun_out/dg/$f.log; done
+exit $rc

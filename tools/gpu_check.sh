@@ -20,3 +20,4 @@ SALZ_DEBUG_SA=1 timeout -k 10 200 python bench.py --no-cpu-baseline --workload f
 timeout -k 10 200 python bench.py --no-cpu-baseline --kind mixed --steps 2 --warmup 1 > $out/mixed.json 2> $out/mixed.err &&
 timeout -k 10 200 python bench.py --workload silesia --steps 2 --warmup 1 > $out/silesia.json 2> $out/silesia.err &&
 timeout -k 10 300 python bench.py --workload enwik9 --steps 1 --warmup 1 > $out/enwik9.json 2> $out/enwik9.err
+timeout -k 10 300 python tools/bench_levels.py --size 50000003 > $out/levels.jsonl 2> $out/levels.err
