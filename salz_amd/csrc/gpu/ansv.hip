@@ -17,6 +17,9 @@
 // Output cand[p] = {p - PSV, lenP, p - NSV, lenN}, the reference's aux layout (:555-558).
 #include "internal.hpp"
 
+#include <cstdio>
+#include <cstdlib>
+
 namespace salz {
 namespace {
 
@@ -46,12 +49,15 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     const uint32_t *__restrict__ sa, const uint32_t *__restrict__ lcp, uint32_t n, uint32_t np2,
     uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp, uint4 *__restrict__ cand,
     uint32_t *__restrict__ qp, uint32_t *__restrict__ qp_len, uint32_t *__restrict__ qn,
-    uint32_t *__restrict__ qn_len, uint32_t *__restrict__ qcount, uint32_t klog)
+    uint32_t *__restrict__ qn_len, uint32_t *__restrict__ qcount, uint32_t klog,
+    unsigned long long *prof)
 {
     __shared__ uint32_t vsa[2 * kB];
     __shared__ uint32_t vlc[2 * kB];
     const uint32_t tid = threadIdx.x;
     const uint32_t b0 = blockIdx.x * kB;
+    // SALZ_PROF_ANSV (diagnostics): per-phase cycle totals of thread 0
+    const unsigned long long t0 = prof ? clock64() : 0ull;
 
     for (uint32_t l = tid; l < kB; l += kT) {
         uint32_t r = b0 + l;
@@ -75,6 +81,11 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
         tlcp[g] = vlc[k];
     }
 
+    unsigned long long t1 = 0;
+    if (prof) {
+        __syncthreads();
+        t1 = clock64();
+    }
     // Phase 1: most nearest smaller values are a few ranks away. Scan up to kNear neighbours
     // on each side (lanes read consecutive LDS words: no bank conflicts); queue the rest.
     __shared__ uint16_t wq[2 * kB];
@@ -117,6 +128,9 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
         }
     }
     __syncthreads();
+    unsigned long long t2 = 0;
+    if (prof)
+        t2 = clock64();
 
     // Phase 2: the queued queries walk the block's min-tree; answers outside the block go to
     // the global queues (k_ansv_global continues from the block root).
@@ -185,6 +199,16 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
                 qn[q] = r;
                 qn_len[q] = lm;
             }
+        }
+    }
+    if (prof) {
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned long long t3 = clock64();
+            atomicAdd(&prof[0], t1 - t0);
+            atomicAdd(&prof[1], t2 - t1);
+            atomicAdd(&prof[2], t3 - t2);
+            atomicAdd(&prof[3], (unsigned long long)nw);
         }
     }
 }
@@ -292,9 +316,21 @@ int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp)
         SALZ_HIP(hipMemsetAsync(tlcp + nblocks + used_blocks, 0xff,
                                 sizeof(uint32_t) * (nblocks - used_blocks), st));
     }
+    static const bool prof_on = getenv("SALZ_PROF_ANSV") != nullptr;
+    unsigned long long *prof = prof_on ? reinterpret_cast<unsigned long long *>(ws.dscal) + 200 : nullptr;
+    if (prof)
+        SALZ_HIP(hipMemsetAsync(prof, 0, 32, st));
     hipLaunchKernelGGL(k_ansv_local, dim3(used_blocks), dim3(kT), 0, st, ws.sa, lcp, n, np2, tsa,
-                       tlcp, ws.cand, qp, qpl, qn, qnl, cnt, ws.klog);
+                       tlcp, ws.cand, qp, qpl, qn, qnl, cnt, ws.klog, prof);
     SALZ_LAUNCH_CHECK();
+    if (prof) {
+        if (read_scalars(ws, 1600, 32, "ansv.prof") != 0)
+            return -1;
+        const uint64_t *h = ws.hscal + 200;
+        fprintf(stderr, "ansv_local: %u blocks, cycles/block build %.0f near %.0f tree %.0f; "
+                "queued %.3f per leaf\n", used_blocks, (double)h[0] / used_blocks,
+                (double)h[1] / used_blocks, (double)h[2] / used_blocks, (double)h[3] / n);
+    }
     for (uint32_t lo = nblocks / 2; lo >= 1; lo >>= 1) {
         hipLaunchKernelGGL(k_tree_level, dim3(grid_for(lo, kT)), dim3(kT), 0, st, tsa, tlcp, lo,
                            lo);

@@ -629,10 +629,15 @@ int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, ui
     int ndev = (n_devices <= 0 || n_devices > avail) ? avail : n_devices;
     // Blocks in flight per device: small blocks are dominated by per-block launch and
     // host-sync latency, so several streams (one context each) overlap them on one GPU.
-    const int per_dev = block_size >= (64u << 20) ? 1 : block_size >= (8u << 20) ? 2 : block_size >= (1u << 20) ? 4 : kMaxSlots;
     // Block count follows the reference CLI loop (programs/salzcli.c:143-179): it always
     // encodes the trailing fread() chunk, even an empty one when src_len is a multiple.
     size_t nblocks = src_len / block_size + 1;
+    // (4 slots: +38% on 16 MiB blocks, +21% on 64 MiB blocks, profiles/r01r_*; a 64 MiB
+    // workspace is ~6 GB, so 4 of them fit easily in 288 GB.)
+    int per_dev = block_size >= (256u << 20) ? 2 : block_size >= (1u << 20) ? 4 : kMaxSlots;
+    const size_t per_dev_blocks = (nblocks + ndev - 1) / ndev;
+    if ((size_t)per_dev > per_dev_blocks)
+        per_dev = (int)per_dev_blocks;
     std::vector<std::vector<uint8_t>> streams(nblocks);
     std::vector<int> rcs(nblocks, -1);
     std::atomic<size_t> next{0};

@@ -359,8 +359,10 @@ __global__ void k_dbg_heads(const uint32_t *__restrict__ hf, const uint32_t *__r
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
         return;
+    // unconditional loads (see load_u64_any): no exec-masked load next to another one
     const uint32_t g = gall[c];
-    const uint32_t prev = c ? gall[c - 1] : 0u;
+    const uint32_t pv = gall[c ? c - 1 : 0];
+    const uint32_t prev = c ? pv : 0u;
     if (g - prev != hf[c] || g == 0)
         atomicOr(err, 0x2000u);
     else if (headpos[g - 1] > c || headpos[g] <= c)
@@ -375,7 +377,8 @@ __global__ void k_dbg_gsc(const uint32_t *__restrict__ headpos, const uint64_t *
         return;
     const uint32_t size = headpos[g + 1] - headpos[g];
     const uint64_t want = size >= 2 ? (((uint64_t)size << 32) | 1ull) : 0ull;
-    const uint64_t nxt = g + 1 < G ? gsc[g + 1] : total;
+    const uint64_t nv = gsc[g + 1];  // in bounds: the scan arrays hold n + 2 entries
+    const uint64_t nxt = g + 1 < G ? nv : total;
     if (nxt - gsc[g] != want)
         atomicOr(err, 0x8000u);
 }

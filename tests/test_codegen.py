@@ -1,0 +1,45 @@
+"""Static check of the built gfx950 code objects (no GPU needed).
+
+tools/vmcnt_scan.py flags partial `s_waitcnt vmcnt(k)` waits that retire a VMEM op issued
+under one EXEC mask while an op issued under another stays outstanding: the shape that
+returned stale registers under concurrent GPU load in the suffix sorter's key kernel
+("Concurrent encodes"). Product kernels must have none.
+"""
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LLVM = "/opt/rocm/lib/llvm/bin"
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def _disassemble(obj, tmp):
+    fat = os.path.join(tmp, os.path.basename(obj) + ".fat")
+    co = os.path.join(tmp, os.path.basename(obj) + ".co")
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj], check=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--type=o",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}", f"--output={co}",
+                    "--unbundle"], check=True)
+    out = subprocess.run([f"{LLVM}/llvm-objdump", "-d", co], check=True, capture_output=True, text=True)
+    s = os.path.join(tmp, os.path.basename(obj) + ".s")
+    open(s, "w").write(out.stdout)
+    return s
+
+
+@pytest.mark.skipif(not shutil.which(f"{LLVM}/llvm-objdump"), reason="ROCm LLVM tools absent")
+def test_no_mixed_exec_partial_vmcnt(tmp_path):
+    from vmcnt_scan import scan
+
+    objs = sorted(glob.glob(os.path.join(ROOT, "salz_amd", "build", "*.o")))
+    objs = [o for o in objs if not o.endswith("salz_host.o")]
+    if not objs:
+        pytest.skip("library not built (python -c 'import __graft_entry__ as g; g.build()')")
+    hits = []
+    for o in objs:
+        hits += scan(_disassemble(o, str(tmp_path)))
+    assert hits == [], hits

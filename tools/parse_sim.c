@@ -10,6 +10,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdio.h>
 
 static uint32_t vn(uint32_t v)
 {
@@ -51,6 +52,21 @@ int parse_sim(const int32_t *psv, const int32_t *lp, const int32_t *nsv, const i
         ref[p] = best;
         refch[p] = ch;
     }
+    if (seed_mode >= 3) {
+        /* local bits-per-byte estimate, suffix-summed (x16 fixed point) */
+        uint64_t acc = 0;
+        cin[n] = 0;
+        for (int32_t q = n - 1; q >= 0; q--) {
+            uint32_t b = 9u * 16u;
+            if (q) {
+                if (lp[q] >= 3) { uint32_t c = 16u * fbits(q - psv[q], lp[q]) / (uint32_t)lp[q]; if (c < b) b = c; }
+                if (ln[q] >= 3) { uint32_t c = 16u * fbits(q - nsv[q], ln[q]) / (uint32_t)ln[q]; if (c < b) b = c; }
+            }
+            if (seed_mode == 4 && b < 16u) b = 16u;
+            acc += b;
+            cin[q] = (uint32_t)(acc / 16u);
+        }
+    } else
     for (int32_t q = 0; q <= n; q++)
         cin[q] = seed_mode == 0 ? 9u * (uint32_t)(n - q) : (seed_mode == 1 ? 0u : 3u * (uint32_t)(n - q));
     memset(chold, 0xff, n);
@@ -86,6 +102,10 @@ int parse_sim(const int32_t *psv, const int32_t *lp, const int32_t *nsv, const i
             }
         }
         uint8_t *t = chold; chold = chnew; chnew = t;
+        if (getenv("PARSE_SIM_VERBOSE")) {
+            /* changed positions: how many, and the span of chunks they fall in */
+            fprintf(stderr, "it %d changed %ld\n", it, changed);
+        }
         if (!changed)
             break;
         /* exact costs of the new decisions */
