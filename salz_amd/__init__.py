@@ -21,7 +21,8 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsalz.so")
+# SALZ_LIB_PATH: load another build of the library (A/B timing in tools/ab.sh)
+LIB_PATH = os.environ.get("SALZ_LIB_PATH") or os.path.join(_HERE, "libsalz.so")
 
 
 class SalzError(RuntimeError):

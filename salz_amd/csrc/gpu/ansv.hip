@@ -27,6 +27,7 @@ constexpr int kT = 256;
 constexpr uint32_t kB = 2048;  // leaves per workgroup block
 constexpr uint32_t kInf = 0xffffffffu;
 constexpr uint32_t kNear = 16;  // linear neighbour scan before the tree walk
+constexpr uint32_t kWQ = 1536;  // LDS walk-queue entries per block
 
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
@@ -45,6 +46,90 @@ __device__ __forceinline__ void put_nsv(uint4 *cand, uint32_t klog, uint32_t p, 
     reinterpret_cast<uint2 *>(cand)[2 * sidx(p, klog) + 1] = v;
 }
 
+// One queued query of the block (e = leaf << 1 | nsv) walks the block's LDS min-tree; a
+// query whose answer lies outside the block goes to the global queue (wave-aggregated).
+__device__ __forceinline__ void block_walk(uint32_t e, const uint32_t *vsa, const uint32_t *vlc,
+                                           uint32_t b0, uint32_t klog, uint4 *cand, uint32_t *qp,
+                                           uint32_t *qp_len, uint32_t *qn, uint32_t *qn_len,
+                                           uint32_t *qcount)
+{
+    const uint32_t l = e >> 1, r = b0 + l;
+    const uint32_t v = vsa[kB + l];
+    const bool nsv = e & 1u;
+    uint32_t lm, hit = kInf, node = kB + l;
+    if (!nsv) {
+        // PSV: nearest smaller to the left; LCP minimum over (r', r].
+        lm = vlc[kB + l];
+        while (node > 1) {
+            if (node & 1u) {
+                uint32_t s = node - 1;
+                if (vsa[s] < v) {
+                    while (s < kB) {
+                        const uint32_t rc = 2 * s + 1;
+                        if (vsa[rc] < v) {
+                            s = rc;
+                        } else {
+                            lm = umin(lm, vlc[rc]);
+                            s = 2 * s;
+                        }
+                    }
+                    hit = s - kB;
+                    break;
+                }
+                lm = umin(lm, vlc[s]);
+            }
+            node >>= 1;
+        }
+        if (hit != kInf)
+            put_psv(cand, klog, v, vsa[kB + hit], lm);
+    } else {
+        // NSV: nearest smaller to the right; LCP minimum over (r, r'].
+        lm = kInf;
+        while (node > 1) {
+            if (!(node & 1u)) {
+                uint32_t s = node + 1;
+                if (vsa[s] < v) {
+                    while (s < kB) {
+                        const uint32_t lc = 2 * s;
+                        if (vsa[lc] < v) {
+                            s = lc;
+                        } else {
+                            lm = umin(lm, vlc[lc]);
+                            s = 2 * s + 1;
+                        }
+                    }
+                    lm = umin(lm, vlc[s]);
+                    hit = s - kB;
+                    break;
+                }
+                lm = umin(lm, vlc[s]);
+            }
+            node >>= 1;
+        }
+        if (hit != kInf)
+            put_nsv(cand, klog, v, vsa[kB + hit], lm);
+    }
+    // global queue: one atomic per wave and side
+    const bool miss = hit == kInf;
+#pragma unroll
+    for (int side = 0; side < 2; side++) {
+        const bool mine = miss && (int)nsv == side;
+        const uint64_t mask = wave_ballot(mine);
+        if (!mask)
+            continue;
+        const int leader = (int)__ffsll((unsigned long long)mask) - 1;
+        uint32_t base = 0;
+        if ((int)lane_id() == leader)
+            base = atomicAdd(&qcount[side], (uint32_t)__popcll(mask));
+        base = shfl_u32(base, leader);
+        if (mine) {
+            const uint32_t q = base + count_below(mask);
+            (side ? qn : qp)[q] = r;
+            (side ? qn_len : qp_len)[q] = lm;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kT) void k_ansv_local(
     const uint32_t *__restrict__ sa, const uint32_t *__restrict__ lcp, uint32_t n, uint32_t np2,
     uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp, uint4 *__restrict__ cand,
@@ -52,34 +137,85 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     uint32_t *__restrict__ qn_len, uint32_t *__restrict__ qcount, uint32_t klog,
     unsigned long long *prof)
 {
-    __shared__ uint32_t vsa[2 * kB];
-    __shared__ uint32_t vlc[2 * kB];
+    __shared__ uint32_t vsa[2 * kB + kNear];  // heap: [1, kB) tree, [kB, 2kB) leaves, + pad
+    __shared__ uint32_t vlc[2 * kB + kNear];
     const uint32_t tid = threadIdx.x;
     const uint32_t b0 = blockIdx.x * kB;
     // SALZ_PROF_ANSV (diagnostics): per-phase cycle totals of thread 0
     const unsigned long long t0 = prof ? clock64() : 0ull;
 
-    for (uint32_t l = tid; l < kB; l += kT) {
-        uint32_t r = b0 + l;
-        vsa[kB + l] = r < n ? sa[r] : kInf;
-        vlc[kB + l] = r < n ? lcp[r] : kInf;
+    // Build the block's min-tree (heap: node k has children 2k, 2k + 1; leaves at kB + l) and
+    // publish its internal nodes into the global heap. Thread t owns leaves 8t .. 8t + 7: the
+    // three levels above them are formed in registers, the next six by butterflies within the
+    // wave, the top two by one thread: two barriers instead of one per level.
+    static_assert(kB == 8 * kT, "8 leaves per thread");
+    const uint32_t root = np2 / kB + blockIdx.x;
+    auto put = [&](uint32_t k, uint32_t a, uint32_t c) {
+        vsa[k] = a;
+        vlc[k] = c;
+        const uint32_t lev = 31u - __builtin_clz(k);
+        const uint32_t g = (root << lev) + (k - (1u << lev));
+        tsa[g] = a;
+        tlcp[g] = c;
+    };
+    uint32_t a[8], c[8];
+    {
+        const uint32_t r0 = b0 + 8 * tid;
+        if (r0 + 8 <= n) {
+            const uint4 x0 = *reinterpret_cast<const uint4 *>(sa + r0);
+            const uint4 x1 = *reinterpret_cast<const uint4 *>(sa + r0 + 4);
+            const uint4 y0 = *reinterpret_cast<const uint4 *>(lcp + r0);
+            const uint4 y1 = *reinterpret_cast<const uint4 *>(lcp + r0 + 4);
+            a[0] = x0.x; a[1] = x0.y; a[2] = x0.z; a[3] = x0.w;
+            a[4] = x1.x; a[5] = x1.y; a[6] = x1.z; a[7] = x1.w;
+            c[0] = y0.x; c[1] = y0.y; c[2] = y0.z; c[3] = y0.w;
+            c[4] = y1.x; c[5] = y1.y; c[6] = y1.z; c[7] = y1.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const bool in = r0 + j < n;
+                a[j] = in ? sa[r0 + j] : kInf;
+                c[j] = in ? lcp[r0 + j] : kInf;
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        vsa[kB + 8 * tid + j] = a[j];
+        vlc[kB + 8 * tid + j] = c[j];
+    }
+    if (tid < kNear) {
+        vsa[2 * kB + tid] = kInf;
+        vlc[2 * kB + tid] = kInf;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {  // level of kB / 2 nodes
+        a[j] = umin(a[2 * j], a[2 * j + 1]);
+        c[j] = umin(c[2 * j], c[2 * j + 1]);
+        put(kB / 2 + 4 * tid + j, a[j], c[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {  // kB / 4 nodes
+        a[j] = umin(a[2 * j], a[2 * j + 1]);
+        c[j] = umin(c[2 * j], c[2 * j + 1]);
+        put(kB / 4 + 2 * tid + j, a[j], c[j]);
+    }
+    uint32_t x = umin(a[0], a[1]), y = umin(c[0], c[1]);  // kB / 8 = kT nodes
+    put(kB / 8 + tid, x, y);
+#pragma unroll
+    for (uint32_t st = 1; st <= 6; st++) {  // kB / 16 .. kB / 512 nodes
+        x = umin(x, shfl_xor_u32(x, 1 << (st - 1)));
+        y = umin(y, shfl_xor_u32(y, 1 << (st - 1)));
+        if ((tid & ((1u << st) - 1u)) == 0)
+            put((kB >> (3 + st)) + (tid >> st), x, y);
     }
     __syncthreads();
-    for (uint32_t half = kB / 2; half >= 1; half >>= 1) {
-        for (uint32_t k = half + tid; k < 2 * half; k += kT) {
-            vsa[k] = umin(vsa[2 * k], vsa[2 * k + 1]);
-            vlc[k] = umin(vlc[2 * k], vlc[2 * k + 1]);
-        }
-        __syncthreads();
+    if (tid == 0) {  // nodes 2, 3 and the block root 1
+        put(2, umin(vsa[4], vsa[5]), umin(vlc[4], vlc[5]));
+        put(3, umin(vsa[6], vsa[7]), umin(vlc[6], vlc[7]));
+        put(1, umin(vsa[2], vsa[3]), umin(vlc[2], vlc[3]));
     }
-    // Publish this block's internal nodes into the global heap.
-    const uint32_t root = np2 / kB + blockIdx.x;
-    for (uint32_t k = 1 + tid; k < kB; k += kT) {
-        uint32_t l = 31u - __builtin_clz(k);
-        uint32_t g = (root << l) + (k - (1u << l));
-        tsa[g] = vsa[k];
-        tlcp[g] = vlc[k];
-    }
+    __syncthreads();
 
     unsigned long long t1 = 0;
     if (prof) {
@@ -88,8 +224,17 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     }
     // Phase 1: most nearest smaller values are a few ranks away. Scan up to kNear neighbours
     // on each side (lanes read consecutive LDS words: no bank conflicts); queue the rest.
-    __shared__ uint16_t wq[2 * kB];
+    // The walk queue holds kWQ entries (12% of 2 kB queries miss on text); a full queue walks
+    // in place. Kept small so 4 workgroups fit a CU's LDS.
+    __shared__ uint16_t wq[kWQ];
     __shared__ uint32_t wq_n;
+    auto enqueue = [&](uint32_t e) {
+        const uint32_t slot = atomicAdd(&wq_n, 1u);
+        if (slot < kWQ)
+            wq[slot] = (uint16_t)e;
+        else
+            block_walk(e, vsa, vlc, b0, klog, cand, qp, qp_len, qn, qn_len, qcount);
+    };
     if (tid == 0)
         wq_n = 0;
     __syncthreads();
@@ -98,33 +243,55 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
         if (r >= n)
             break;
         const uint32_t v = vsa[kB + l];
-        uint32_t lmP = vlc[kB + l], hitP = kInf;
-        for (uint32_t d = 1; d <= kNear && d <= l; d++) {
-            if (vsa[kB + l - d] < v) {
-                hitP = l - d;
-                break;
-            }
-            lmP = umin(lmP, vlc[kB + l - d]);
+        // Fully unrolled: all 4 * kNear LDS reads are independent and issue back to back
+        // (paired into ds_read2_b32 with constant offsets); the first hit is then selected
+        // in registers. Reads left of the block's first leaf land in the tree levels and
+        // right of its last leaf in the +inf pad; both are masked by the bounds tests.
+        uint32_t sL[kNear], cL[kNear], sR[kNear], cR[kNear];
+#pragma unroll
+        for (uint32_t d = 1; d <= kNear; d++) {
+            sL[d - 1] = vsa[kB + l - d];
+            cL[d - 1] = vlc[kB + l - d];
+            sR[d - 1] = vsa[kB + l + d];
+            cR[d - 1] = vlc[kB + l + d];
         }
-        uint32_t lmN = kInf, hitN = kInf;
-        for (uint32_t d = 1; d <= kNear && l + d < kB; d++) {
-            lmN = umin(lmN, vlc[kB + l + d]);
-            if (vsa[kB + l + d] < v) {
-                hitN = l + d;
-                break;
+        uint32_t lmP = vlc[kB + l], lm = lmP, hitP = kInf, pvP = 0;
+#pragma unroll
+        for (uint32_t d = 1; d <= kNear; d++) {
+            const bool live = hitP == kInf && d <= l;
+            if (live && sL[d - 1] < v) {
+                hitP = l - d;
+                pvP = sL[d - 1];
+                lmP = lm;
+            }
+            if (live)
+                lm = umin(lm, cL[d - 1]);
+        }
+        uint32_t lmN = kInf, hitN = kInf, pvN = 0;
+        lm = kInf;
+#pragma unroll
+        for (uint32_t d = 1; d <= kNear; d++) {
+            const bool live = hitN == kInf && l + d < kB;
+            if (live) {
+                lm = umin(lm, cR[d - 1]);
+                if (sR[d - 1] < v) {
+                    hitN = l + d;
+                    pvN = sR[d - 1];
+                    lmN = lm;
+                }
             }
         }
         if (hitP != kInf && hitN != kInf) {
-            cand[sidx(v, klog)] = make_uint4(v - vsa[kB + hitP], lmP, v - vsa[kB + hitN], lmN);
+            cand[sidx(v, klog)] = make_uint4(v - pvP, lmP, v - pvN, lmN);
         } else {
             if (hitP != kInf)
-                put_psv(cand, klog, v, vsa[kB + hitP], lmP);
+                put_psv(cand, klog, v, pvP, lmP);
             else
-                wq[atomicAdd(&wq_n, 1u)] = (uint16_t)(l << 1);
+                enqueue(l << 1);
             if (hitN != kInf)
-                put_nsv(cand, klog, v, vsa[kB + hitN], lmN);
+                put_nsv(cand, klog, v, pvN, lmN);
             else
-                wq[atomicAdd(&wq_n, 1u)] = (uint16_t)(l << 1 | 1u);
+                enqueue(l << 1 | 1u);
         }
     }
     __syncthreads();
@@ -134,73 +301,9 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
 
     // Phase 2: the queued queries walk the block's min-tree; answers outside the block go to
     // the global queues (k_ansv_global continues from the block root).
-    const uint32_t nw = wq_n;
-    for (uint32_t w = tid; w < nw; w += kT) {
-        const uint32_t e = wq[w], l = e >> 1, r = b0 + l;
-        const uint32_t v = vsa[kB + l];
-        if (!(e & 1u)) {
-            // PSV: nearest smaller to the left; LCP minimum over (r', r].
-            uint32_t lm = vlc[kB + l], node = kB + l, hit = kInf;
-            while (node > 1) {
-                if (node & 1u) {
-                    uint32_t s = node - 1;
-                    if (vsa[s] < v) {
-                        while (s < kB) {
-                            uint32_t rc = 2 * s + 1;
-                            if (vsa[rc] < v) {
-                                s = rc;
-                            } else {
-                                lm = umin(lm, vlc[rc]);
-                                s = 2 * s;
-                            }
-                        }
-                        hit = s - kB;
-                        break;
-                    }
-                    lm = umin(lm, vlc[s]);
-                }
-                node >>= 1;
-            }
-            if (hit != kInf) {
-                put_psv(cand, klog, v, vsa[kB + hit], lm);
-            } else {
-                uint32_t q = atomicAdd(&qcount[0], 1u);
-                qp[q] = r;
-                qp_len[q] = lm;
-            }
-        } else {
-            // NSV: nearest smaller to the right; LCP minimum over (r, r'].
-            uint32_t lm = kInf, node = kB + l, hit = kInf;
-            while (node > 1) {
-                if (!(node & 1u)) {
-                    uint32_t s = node + 1;
-                    if (vsa[s] < v) {
-                        while (s < kB) {
-                            uint32_t lc = 2 * s;
-                            if (vsa[lc] < v) {
-                                s = lc;
-                            } else {
-                                lm = umin(lm, vlc[lc]);
-                                s = 2 * s + 1;
-                            }
-                        }
-                        lm = umin(lm, vlc[s]);
-                        hit = s - kB;
-                        break;
-                    }
-                    lm = umin(lm, vlc[s]);
-                }
-                node >>= 1;
-            }
-            if (hit != kInf) {
-                put_nsv(cand, klog, v, vsa[kB + hit], lm);
-            } else {
-                uint32_t q = atomicAdd(&qcount[1], 1u);
-                qn[q] = r;
-                qn_len[q] = lm;
-            }
-        }
-    }
+    const uint32_t nw = wq_n < kWQ ? wq_n : kWQ;
+    for (uint32_t w = tid; w < nw; w += kT)
+        block_walk(wq[w], vsa, vlc, b0, klog, cand, qp, qp_len, qn, qn_len, qcount);
     if (prof) {
         __syncthreads();
         if (tid == 0) {
@@ -324,12 +427,13 @@ int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp)
                        tlcp, ws.cand, qp, qpl, qn, qnl, cnt, ws.klog, prof);
     SALZ_LAUNCH_CHECK();
     if (prof) {
-        if (read_scalars(ws, 1600, 32, "ansv.prof") != 0)
+        if (read_scalars(ws, 0, 1632, "ansv.prof") != 0)
             return -1;
         const uint64_t *h = ws.hscal + 200;
         fprintf(stderr, "ansv_local: %u blocks, cycles/block build %.0f near %.0f tree %.0f; "
-                "queued %.3f per leaf\n", used_blocks, (double)h[0] / used_blocks,
-                (double)h[1] / used_blocks, (double)h[2] / used_blocks, (double)h[3] / n);
+                "queued %.3f per leaf; global %u + %u\n", used_blocks, (double)h[0] / used_blocks,
+                (double)h[1] / used_blocks, (double)h[2] / used_blocks, (double)h[3] / n,
+                reinterpret_cast<uint32_t *>(ws.hscal)[40], reinterpret_cast<uint32_t *>(ws.hscal)[41]);
     }
     for (uint32_t lo = nblocks / 2; lo >= 1; lo >>= 1) {
         hipLaunchKernelGGL(k_tree_level, dim3(grid_for(lo, kT)), dim3(kT), 0, st, tsa, tlcp, lo,

@@ -81,10 +81,28 @@ __device__ __forceinline__ uint64_t target_state(const uint64_t *pst, const uint
     return q < b ? pst[base + ((size_t)(q - a) << 6)] : ((uint64_t)cin[sidx(q, klog)] << 32) | q;
 }
 
-// One lane per chunk, positions b-1 down to a. The loads of a step do not depend on the step
-// before it (its targets lie at p + 3 or beyond, finished at least two steps earlier), so
-// they are software-pipelined: candidates are loaded three steps ahead and target states two
-// steps ahead, and a step waits only on memory issued two steps earlier.
+// One lane per chunk, positions b-1 down to a. The states of the last kWin positions
+// (p+1 .. p+kWin) stay in registers, so a factor of length <= kWin reads its target from
+// there; a longer factor's target (p + len >= p + kWin + 1) was finished at least kWin + 1
+// steps earlier, so its load is issued kDepth = kWin steps ahead, and candidates one step
+// before that. A step then waits only on memory issued eight steps earlier (the previous
+// version, with a two-step pipeline, waited on a full HBM latency every other step).
+constexpr uint32_t kWin = 8;
+constexpr uint32_t kDepth = kWin;
+
+// target state of a long factor (len > kWin), or 0 when the window serves it
+__device__ __forceinline__ uint64_t far_state(const uint64_t *pst, const uint32_t *cin, size_t base,
+                                              uint32_t a, uint32_t b, uint32_t klog, uint32_t p,
+                                              uint32_t len, uint32_t n, uint32_t *err)
+{
+    if (len <= kWin)
+        return 0;
+    const uint32_t q = p + len;
+    if (bad_index(len > n - p, err, kErrParse))
+        return 0;
+    return q < b ? pst[base + ((size_t)(q - a) << 6)] : ((uint64_t)cin[sidx(q, klog)] << 32) | q;
+}
+
 __global__ __launch_bounds__(kT) void k_parse_chunk(
     const uint4 *__restrict__ cand, const uint32_t *__restrict__ cin, uint64_t *__restrict__ pst,
     const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, uint32_t klog,
@@ -101,61 +119,90 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         const uint32_t jn = b - a;
         auto slot = [&](uint32_t j) { return base + ((size_t)j << 6); };
         const uint4 none = make_uint4(1u, 0u, 1u, 0u);
-        // pipeline registers: c0/o0/t0 = step j, c1/o1/t1 = j-1, c2 = j-2
-        uint4 c0 = cand[slot(jn - 1)];
-        uint8_t o0 = chold[slot(jn - 1)];
-        uint4 c1 = jn >= 2 ? cand[slot(jn - 2)] : none;
-        uint8_t o1 = jn >= 2 ? chold[slot(jn - 2)] : 0;
-        uint4 c2 = jn >= 3 ? cand[slot(jn - 3)] : none;
-        uint64_t t0P = target_state(pst, cin, base, a, b, klog, a + jn - 1, c0.y, n, err);
-        uint64_t t0N = target_state(pst, cin, base, a, b, klog, a + jn - 1, c0.w, n, err);
-        uint64_t t1P = 0, t1N = 0;
-        if (jn >= 2) {
-            t1P = target_state(pst, cin, base, a, b, klog, a + jn - 2, c1.y, n, err);
-            t1N = target_state(pst, cin, base, a, b, klog, a + jn - 2, c1.w, n, err);
+        // rings, index k = position p - k for the current p
+        uint4 cr[kDepth + 1];
+        uint8_t orr[kDepth];
+        uint64_t tP[kDepth], tN[kDepth];
+        uint64_t win[kWin];  // win[k] = state of p + 1 + k
+        const uint32_t p0 = b - 1;
+#pragma unroll
+        for (uint32_t k = 0; k <= kDepth; k++)
+            cr[k] = jn > k ? cand[slot(jn - 1 - k)] : none;
+#pragma unroll
+        for (uint32_t k = 0; k < kDepth; k++) {
+            orr[k] = jn > k ? chold[slot(jn - 1 - k)] : 0;
+            tP[k] = jn > k ? far_state(pst, cin, base, a, b, klog, p0 - k, cr[k].y, n, err) : 0;
+            tN[k] = jn > k ? far_state(pst, cin, base, a, b, klog, p0 - k, cr[k].w, n, err) : 0;
         }
-        // state of p + 1: cost estimate and exit (p = b - 1 starts at the exit b)
-        uint32_t nc = cin[sidx(b, klog)], nex = b;
+#pragma unroll
+        for (uint32_t k = 0; k < kWin; k++) {  // exits b .. b + kWin - 1 (past n: never a target)
+            const uint32_t q = b + k;
+            win[k] = q <= n ? (((uint64_t)cin[sidx(q, klog)] << 32) | q) : 0;
+        }
         for (uint32_t j = jn; j-- > 0;) {
             const uint32_t p = a + j;
-            uint32_t best = 9u + nc, ex = nex;
+            const uint4 c0 = cr[0];
+            uint32_t best = 9u + (uint32_t)(win[0] >> 32), ex = (uint32_t)win[0];
             uint8_t ch = 0;
             if (p != 0) {
                 if (c0.y >= 3u) {
-                    const uint32_t alt = factor_bits(c0.x, c0.y) + (uint32_t)(t0P >> 32);
+                    uint64_t t = tP[0];
+                    if (c0.y <= kWin) {
+                        bad_index(c0.y > n - p, err, kErrParse);
+#pragma unroll
+                        for (uint32_t k = 2; k < kWin; k++)
+                            t = c0.y == k + 1 ? win[k] : t;
+                    }
+                    const uint32_t alt = factor_bits(c0.x, c0.y) + (uint32_t)(t >> 32);
                     if ((int32_t)alt < (int32_t)best) {
                         best = alt;
-                        ex = (uint32_t)t0P;
+                        ex = (uint32_t)t;
                         ch = 1;
                     }
                 }
                 if (c0.w >= 3u) {
-                    const uint32_t alt = factor_bits(c0.z, c0.w) + (uint32_t)(t0N >> 32);
+                    uint64_t t = tN[0];
+                    if (c0.w <= kWin) {
+                        bad_index(c0.w > n - p, err, kErrParse);
+#pragma unroll
+                        for (uint32_t k = 2; k < kWin; k++)
+                            t = c0.w == k + 1 ? win[k] : t;
+                    }
+                    const uint32_t alt = factor_bits(c0.z, c0.w) + (uint32_t)(t >> 32);
                     if ((int32_t)alt < (int32_t)best) {
                         best = alt;
-                        ex = (uint32_t)t0N;
+                        ex = (uint32_t)t;
                         ch = 2;
                     }
                 }
             }
-            pst[slot(j)] = ((uint64_t)best << 32) | ex;
+            const uint64_t stp = ((uint64_t)best << 32) | ex;
+            pst[slot(j)] = stp;
             chnew[slot(j)] = ch;
-            diff += ch != o0;
-            nc = best;
-            nex = ex;
-            // advance the pipeline: step j-1 becomes current, issue loads for j-2 / j-3
-            c0 = c1;
-            o0 = o1;
-            t0P = t1P;
-            t0N = t1N;
-            c1 = c2;
-            if (j >= 2) {
-                o1 = chold[slot(j - 2)];
-                t1P = target_state(pst, cin, base, a, b, klog, p - 2, c1.y, n, err);
-                t1N = target_state(pst, cin, base, a, b, klog, p - 2, c1.w, n, err);
+            diff += ch != orr[0];
+            // shift the window and the rings one position down
+#pragma unroll
+            for (uint32_t k = kWin - 1; k > 0; k--)
+                win[k] = win[k - 1];
+            win[0] = stp;
+#pragma unroll
+            for (uint32_t k = 0; k < kDepth; k++)
+                cr[k] = cr[k + 1];
+#pragma unroll
+            for (uint32_t k = 0; k + 1 < kDepth; k++) {
+                orr[k] = orr[k + 1];
+                tP[k] = tP[k + 1];
+                tN[k] = tN[k + 1];
             }
-            if (j >= 3)
-                c2 = cand[slot(j - 3)];
+            // new loads: the position kDepth below the next one (p - 1 - (kDepth - 1) = p - kDepth)
+            // and its candidate one step earlier still
+            if (j >= kDepth) {
+                const uint32_t pj = p - kDepth;
+                orr[kDepth - 1] = chold[slot(j - kDepth)];
+                tP[kDepth - 1] = far_state(pst, cin, base, a, b, klog, pj, cr[kDepth - 1].y, n, err);
+                tN[kDepth - 1] = far_state(pst, cin, base, a, b, klog, pj, cr[kDepth - 1].w, n, err);
+            }
+            cr[kDepth] = j >= kDepth + 1 ? cand[slot(j - kDepth - 1)] : none;
         }
     }
     // one atomic per wave

@@ -106,11 +106,17 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
                          const uint32_t *__restrict__ off_old, uint32_t *__restrict__ off_new,
                          uint32_t *__restrict__ nval, uint32_t *__restrict__ ngid,
                          uint32_t *__restrict__ rank, uint32_t *__restrict__ sa, GroupTab tab,
-                         uint32_t m, uint32_t n, int kb_old, int round0, uint32_t *err)
+                         uint32_t m, uint32_t n, int kb_old, int round0, uint32_t *err,
+                         uint32_t ilo, uint32_t ihi, int pass0)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
         return;
+    if (!pass0) {  // later passes only write the rank of suffixes in [ilo, ihi)
+        const uint32_t i0 = val[c];
+        if (i0 < ilo || i0 >= ihi)
+            return;
+    }
     uint32_t g = gall[c] - 1u;
     uint32_t hp = headpos[g];
     uint32_t size = headpos[g + 1] - hp;
@@ -121,8 +127,14 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     // The first subgroup of an old group keeps the old group's head, so its members' ranks
     // are unchanged; every other rank (and all of round 0) is written.
     const bool same = !round0 && (hp == 0 || (key[hp - 1] >> kb_old) != (key[hp] >> kb_old));
-    if (!same)
+    // rank[i] is a random 4-byte scatter (a read-modify-write of a whole HBM burst). Large
+    // rounds split it by text range over two passes, so the rank lines one pass writes fit
+    // in the 256 MB Infinity Cache and are merged there; pass 0 does
+    // everything else.
+    if (!same && i >= ilo && i < ihi)
         rank[i] = hp + o + 1u;
+    if (!pass0)
+        return;
     if (size == 1) {
         sa[c + o] = i;
     } else {
@@ -466,6 +478,8 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     uint64_t *KC = ws.pst;
 
     static const bool dbg_rounds = getenv("SALZ_CHECK_ROUNDS") != nullptr;
+    static const bool split_on = !getenv("SALZ_COMMIT_SPLIT") || atoi(getenv("SALZ_COMMIT_SPLIT")) > 1;
+    static const uint32_t split_ratio = getenv("SALZ_SPLIT_RATIO") ? (uint32_t)atoi(getenv("SALZ_SPLIT_RATIO")) : 4;
     SALZ_HIP(hipMemsetAsync(ws.rank + n, 0, sizeof(uint32_t), st));  // rank[n] = 0
     hipLaunchKernelGGL(k_sa_init, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, n, K, V);
     SALZ_LAUNCH_CHECK();
@@ -581,10 +595,18 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
             hipLaunchKernelGGL(k_dbg_gsc, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, gsc, G, ws.hscal[8], derr);
             SALZ_LAUNCH_CHECK();
         }
-        hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, gall, headpos,
-                           gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, kb_old,
-                           round0, derr);
-        SALZ_LAUNCH_CHECK();
+        // Large rounds: the rank scatter in two text-range passes (k_commit comment).
+        // (only where most ranks change: round 0, or a round that multiplied the groups)
+        const bool many = round0 || (uint64_t)G >= (uint64_t)split_ratio * G_act;
+        const int split = (m >= (32u << 20) && split_on && many) ? 2 : 1;
+        for (int ps = 0; ps < split; ps++) {
+            const uint32_t ilo = ps == 0 ? 0u : n / 2;
+            const uint32_t ihi = ps + 1 == split ? 0xffffffffu : n / 2;
+            hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, gall, headpos,
+                               gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, kb_old,
+                               round0, derr, ilo, ihi, ps == 0 ? 1 : 0);
+            SALZ_LAUNCH_CHECK();
+        }
         if (read_scalars(ws, 0, 256, "sa.m") != 0)
             return -1;
         if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
