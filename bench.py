@@ -214,16 +214,40 @@ def main():
         "alg_bytes_per_launch": int(bytes_rx / launches),
     }
 
+    # Whole-pipeline roofline: A(N) = 66 n + m compulsory bytes per block
+    # (each stage's int32 arrays written once and read once), over the measured block time.
+    n_pos = in_bytes - 8 * nblocks
+    alg_pipeline = 66.0 * n_pos + out_bytes
+    pipe_gbs = alg_pipeline * args.steps / dt / 1e9
+    roofline_pipeline = {"alg_bytes_per_step": int(alg_pipeline), "achieved": round(pipe_gbs, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(pipe_gbs / HBM_PEAK_GBS, 4),
+                         "definition": "A(N) = 66 n + m per block (SURVEY.md §8 d3)"}
+
     cpu = None
     parity_full = None
     if rank == 0 and not args.no_cpu_baseline and spans:
-        from tests.helpers import oracle_encode  # CPU port of the reference (baseline + checker)
+        import ctypes
+
+        import numpy as np
+
+        from tests.helpers import oracle, oracle_encode  # CPU port of the reference (baseline + checker)
 
         s, e = spans[0]
         sample = (e - s) if args.cpu_sample <= 0 else min(args.cpu_sample, e - s)
         c0 = time.perf_counter()
         rc, ref = oracle_encode(src[s:s + sample])
         c1 = time.perf_counter()
+        # SA alone (own SA-IS, standing in for libsais) so SA and post-SA time are separate
+        blk = np.ascontiguousarray(src[s:s + sample])
+        sa_buf = np.empty(max(sample - 8, 1), np.int32)
+        c2 = time.perf_counter()
+        oracle().oracle_suffix_array(blk.ctypes.data, sa_buf.ctypes.data, ctypes.c_int32(max(sample - 8, 0)))
+        c3 = time.perf_counter()
+        model = ""
+        try:
+            model = next(ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name"))
+        except (OSError, StopIteration):
+            pass
         cpu = {
             "value": round(sample / (c1 - c0) / 1e6, 3),
             "unit": "MB/s",
@@ -232,6 +256,9 @@ def main():
             "sample": f"one {sample:,}-byte block of the same {kind} input, oracle/liboracle.so "
                       f"(clean-room C restatement of lib/salz.c + own SA-IS), 1 thread, "
                       f"{c1 - c0:.2f} s",
+            "sa_s": round(c3 - c2, 3),
+            "post_sa_s": round((c1 - c0) - (c3 - c2), 3),
+            "cpu_model": model,
         }
         if sample == e - s:
             parity_full = bool(rc == 0 and ref == streams[0])
@@ -259,6 +286,7 @@ def main():
                 "parallelism": f"independent blocks over {world} GPU(s), {nslots} encoder slot(s) per GPU",
             },
             "roofline": roofline,
+            "roofline_pipeline": roofline_pipeline,
             "cpu_baseline": cpu,
             "encoded_bytes": int(out_bytes),
             "ratio": round(in_bytes / out_bytes, 4),
