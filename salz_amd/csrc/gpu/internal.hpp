@@ -52,6 +52,8 @@ struct Workspace {
     uint64_t *keyA = nullptr, *keyB = nullptr;  // n+1 each
     uint32_t *valA = nullptr, *valB = nullptr;
     uint32_t *u0 = nullptr, *u1 = nullptr, *u2 = nullptr, *u3 = nullptr;  // n+2 each
+    uint32_t *lcps = nullptr;  // LCP array in SA order, filled by the suffix sorter (n+2)
+    bool lcps_ok = false;      // lcps is complete for the current block
     uint64_t *g64 = nullptr;                                             // n+2
     uint32_t *offA = nullptr, *offB = nullptr;                           // n+2 each
     uint4 *cand = nullptr;                                               // cap_s, interleaved

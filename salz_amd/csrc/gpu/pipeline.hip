@@ -87,7 +87,7 @@ void workspace_free(Workspace &ws)
     if (ws.device >= 0)
         (void)hipSetDevice(ws.device);
     void *ptrs[] = {ws.text, ws.rank,     ws.sa,   ws.keyA, ws.keyB, ws.valA, ws.valB,
-                    ws.u0,   ws.u1,       ws.u2,   ws.u3,   ws.g64,  ws.offA, ws.offB,
+                    ws.u0,   ws.u1,       ws.u2,   ws.u3,   ws.g64,  ws.offA, ws.offB, ws.lcps,
                     ws.cand, ws.pst, ws.lsc, ws.lrec, ws.lg2g, ws.out, ws.radix_counts,  ws.scan_tmp,      ws.dscal};
     for (void *p : ptrs)
         if (p)
@@ -128,7 +128,7 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
     if (dalloc(&ws.text, N + 256) || dalloc(&ws.rank, n1) || dalloc(&ws.sa, n1) ||
         dalloc(&ws.keyA, n1) || dalloc(&ws.keyB, n1) || dalloc(&ws.valA, n1) ||
         dalloc(&ws.valB, n1) || dalloc(&ws.u0, n1) || dalloc(&ws.u1, n1) || dalloc(&ws.u2, n1) ||
-        dalloc(&ws.u3, n1) || dalloc(&ws.g64, n1) || dalloc(&ws.offA, n1) ||
+        dalloc(&ws.u3, n1) || dalloc(&ws.lcps, n1) || dalloc(&ws.g64, n1) || dalloc(&ws.offA, n1) ||
         dalloc(&ws.offB, n1) || dalloc(&ws.cand, ws.cap_s) || dalloc(&ws.pst, ws.cap_s) ||
         dalloc(&ws.lsc, n1) || dalloc(&ws.lrec, n1 / 1024 + 2) || dalloc(&ws.lg2g, n1 / 1024 + 2) || dalloc(&ws.out, ws.out_cap) ||
         dalloc(&ws.radix_counts, ws.radix_counts_elems) ||
@@ -242,7 +242,7 @@ __global__ void k_check_cand(const uint4 *cand, uint32_t n, uint32_t klog, uint3
         atomicOr(err, 0x400u);
 }
 
-static int check_stage(Workspace &ws, uint32_t n, int which)
+static int check_stage(Workspace &ws, uint32_t n, int which, const uint32_t *lcp = nullptr)
 {
     static const bool on = getenv("SALZ_CHECK_STAGES") != nullptr;
     if (!on)
@@ -253,7 +253,7 @@ static int check_stage(Workspace &ws, uint32_t n, int which)
                            ws.text, n, derr);
     else if (which == 0)
         hipLaunchKernelGGL(k_check_lcp, dim3(grid_for(n, 256)), dim3(256), 0, ws.stream, ws.sa,
-                           ws.u3, ws.text, n, derr);
+                           lcp, ws.text, n, derr);
     else
         hipLaunchKernelGGL(k_check_cand, dim3(grid_for(n, 256)), dim3(256), 0, ws.stream, ws.cand,
                            n, ws.klog, derr);
@@ -362,9 +362,13 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t N
     if (stage_suffix_array(ws, n) || guard_check(ws, "sa") || check_stage(ws, n, 2)) return -1;
     if (mark(ws, EV_SA)) return -1;
     if (dump_after_sa(ws, n, dump)) return -1;
-    if (stage_lcp(ws, n, ws.u3) || guard_check(ws, "lcp") || check_stage(ws, n, 0)) return -1;
+    // The suffix sorter usually leaves the LCP array behind (sa.hip, "LCP"); otherwise the
+    // Phi / PLCP stage computes it.
+    uint32_t *lcp = ws.lcps_ok ? ws.lcps : ws.u3;
+    if ((!ws.lcps_ok && stage_lcp(ws, n, lcp)) || guard_check(ws, "lcp") || check_stage(ws, n, 0, lcp))
+        return -1;
     if (mark(ws, EV_LCP)) return -1;
-    if (stage_candidates(ws, n, ws.u3) || guard_check(ws, "ansv") || check_stage(ws, n, 1)) return -1;
+    if (stage_candidates(ws, n, lcp) || guard_check(ws, "ansv") || check_stage(ws, n, 1)) return -1;
     if (mark(ws, EV_ANSV)) return -1;
     if (stage_parse(ws, n) || guard_check(ws, "parse")) return -1;
     if (mark(ws, EV_PARSE)) return -1;

@@ -34,6 +34,7 @@ namespace salz {
 namespace {
 
 constexpr int kT = 256;
+__device__ __forceinline__ uint32_t umin_(uint32_t a, uint32_t b) { return a < b ? a : b; }
 constexpr uint32_t kSegT = 2048;     // window of the active list per k_seg_small workgroup
 constexpr uint32_t kSmall = kSegT;   // largest group sorted in LDS (must be <= kSegT)
 constexpr uint32_t kSegCap = 4096;   // LDS slots: a window's groups span < kSegT + kSmall
@@ -154,6 +155,95 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
                 tab.lg2g[lg] = ng;
             }
         }
+    }
+}
+
+// LCP as a by-product of the sort. Every SA position r >= 1 becomes a group head exactly once,
+// in the round whose keys first tell SA[r-1] and SA[r] apart; all members of the two groups
+// then share the same LCP, so the pair at the boundary gives LCP[r] for good:
+//   round 0 (8-byte keys):   LCP = leading equal bytes of the two keys, capped by both lengths;
+//   round t (keys compare rank[i + hk] within groups sharing hk bytes): LCP = hk + the equal
+//   bytes of T[i + hk ..] and T[j + hk ..], fewer than hk. Up to kLcpLane bytes one lane
+//   compares; longer compares take the whole wave, 512 bytes per step, one head at a time.
+// The host stops (and the PLCP stage takes over, lcp.hip) once hk exceeds kLcpMaxHk.
+constexpr uint32_t kLcpLane = 16;
+constexpr uint32_t kLcpMaxHk = 4096;
+
+// k_heads with the LCP of every new head (writes hf like k_heads).
+__global__ __launch_bounds__(kT) void k_heads_lcp(
+    const uint64_t *__restrict__ K, const uint32_t *__restrict__ V, uint32_t *__restrict__ hf,
+    const uint32_t *__restrict__ off_old, uint32_t m, uint32_t n, int kb_old, uint32_t hk, int round0,
+    const uint8_t *__restrict__ T, uint32_t *__restrict__ lcps, uint32_t *err)
+{
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    const bool in = c < m;
+    // every load unconditional (clamped indices): no exec-masked load next to another
+    const size_t cc = in ? c : 0, cp = cc ? cc - 1 : 0;
+    const uint64_t k0 = K[cp], k1 = K[cc];
+    const uint32_t v0 = V[cp], v1 = V[cc];
+    bool head = c == 0 || k0 != k1;
+    if (round0 && !head)
+        head = (n - v1) < 8u || (n - v0) < 8u;
+    if (in)
+        hf[c] = head ? 1u : 0u;
+    const uint32_t g1 = round0 ? 0u : (uint32_t)(k1 >> kb_old);
+    const uint32_t o = round0 ? 0u : off_old[g1];
+    const uint32_t i = v1, j = v0, mx = i > j ? i : j;
+    bool need = false;
+    uint32_t pos = 0, lim = 0;
+    if (in && head) {
+        if (round0) {
+            uint32_t l = 0;
+            if (c > 0) {
+                const uint64_t x = k0 ^ k1;
+                l = x ? (uint32_t)__builtin_clzll(x) >> 3 : 8u;
+                l = umin_(l, n - i);
+                l = umin_(l, n - j);
+            }
+            lcps[c] = l;
+        } else if (c > 0 && (uint32_t)(k0 >> kb_old) == g1) {
+            pos = (uint32_t)c + o;
+            if (!bad_index(i >= n || j >= n || pos >= n || n - mx < hk, err, kErrCommit)) {
+                lim = umin_(hk, n - mx - hk);
+                if (hk <= kLcpLane) {
+                    uint32_t l = lim;
+                    for (uint32_t off = 0; off < lim; off += 8) {
+                        const uint64_t x = load_u64_any(T, (size_t)i + hk + off) ^
+                                           load_u64_any(T, (size_t)j + hk + off);
+                        if (x) {
+                            l = umin_(lim, off + ((uint32_t)__builtin_ctzll(x) >> 3));
+                            break;
+                        }
+                    }
+                    lcps[pos] = hk + l;
+                } else {
+                    need = true;
+                }
+            }
+        }
+    }
+    uint64_t pend = wave_ballot(need);
+    const uint32_t lane = lane_id();
+    while (pend) {
+        const int src = (int)__ffsll((unsigned long long)pend) - 1;
+        pend &= pend - 1;
+        const uint32_t si = shfl_u32(i, src) + hk, sj = shfl_u32(j, src) + hk;
+        const uint32_t sl = shfl_u32(lim, src), sp = shfl_u32(pos, src);
+        uint32_t mis = sl;
+        for (uint32_t base = 0; base < sl; base += 64 * 8) {
+            const uint32_t off = base + lane * 8;
+            uint32_t mm = 0xffffffffu;
+            const uint64_t x = load_u64_any(T, (size_t)si + off) ^ load_u64_any(T, (size_t)sj + off);
+            if (off < sl && x)
+                mm = off + ((uint32_t)__builtin_ctzll(x) >> 3);
+            mm = wave_min_u32(mm);
+            if (mm != 0xffffffffu) {
+                mis = umin_(mm, sl);
+                break;
+            }
+        }
+        if ((int)lane == src)
+            lcps[sp] = hk + mis;
     }
 }
 
@@ -478,6 +568,8 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     uint64_t *KC = ws.pst;
 
     static const bool dbg_rounds = getenv("SALZ_CHECK_ROUNDS") != nullptr;
+    static const bool lcp_in_sort = !getenv("SALZ_LCP_SA") || atoi(getenv("SALZ_LCP_SA")) != 0;
+    ws.lcps_ok = lcp_in_sort;
     static const bool split_on = !getenv("SALZ_COMMIT_SPLIT") || atoi(getenv("SALZ_COMMIT_SPLIT")) > 1;
     static const uint32_t split_ratio = getenv("SALZ_SPLIT_RATIO") ? (uint32_t)atoi(getenv("SALZ_SPLIT_RATIO")) : 4;
     SALZ_HIP(hipMemsetAsync(ws.rank + n, 0, sizeof(uint32_t), st));  // rank[n] = 0
@@ -566,8 +658,14 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
                                n, h / 2, kb, round0, derr);
             SALZ_LAUNCH_CHECK();
         }
-        hipLaunchKernelGGL(k_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m, n, round0,
-                           hf);
+        if (ws.lcps_ok && !round0 && h / 2 > kLcpMaxHk)
+            ws.lcps_ok = false;  // long repeats: the PLCP stage is cheaper than these compares
+        if (ws.lcps_ok)
+            hipLaunchKernelGGL(k_heads_lcp, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hf, offo, m, n,
+                               kb_old, round0 ? 0u : h / 2, round0, ws.text, ws.lcps, derr);
+        else
+            hipLaunchKernelGGL(k_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m, n, round0,
+                               hf);
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u32(hf, gall, m, true, d32 + 0, ws, st) != 0)
             return -1;
