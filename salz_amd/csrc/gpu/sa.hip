@@ -568,8 +568,8 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     uint64_t *KC = ws.pst;
 
     static const bool dbg_rounds = getenv("SALZ_CHECK_ROUNDS") != nullptr;
-    static const bool lcp_in_sort = !getenv("SALZ_LCP_SA") || atoi(getenv("SALZ_LCP_SA")) != 0;
-    ws.lcps_ok = lcp_in_sort;
+    const char *lcp_env = getenv("SALZ_LCP_SA");  // tests: "0" forces the Phi/PLCP stage
+    ws.lcps_ok = !lcp_env || atoi(lcp_env) != 0;
     static const bool split_on = !getenv("SALZ_COMMIT_SPLIT") || atoi(getenv("SALZ_COMMIT_SPLIT")) > 1;
     static const uint32_t split_ratio = getenv("SALZ_SPLIT_RATIO") ? (uint32_t)atoi(getenv("SALZ_SPLIT_RATIO")) : 4;
     SALZ_HIP(hipMemsetAsync(ws.rank + n, 0, sizeof(uint32_t), st));  // rank[n] = 0

@@ -238,6 +238,21 @@ def test_suffix_sort_modes(ctx, monkeypatch, mode, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
+@pytest.mark.parametrize("lcp_sa", ["1", "0"])
+@pytest.mark.parametrize("kind,n,seed,alpha", [("text", 400000, 1, 0), ("mixed", 500000, 3, 0),
+                                               ("fib", 200000, 0, 0), ("smx", 300000, 2, 4),
+                                               ("runs", 150000, 0, 0), ("zeros", 60000, 0, 0),
+                                               ("smx", 100000, 5, 256)])
+def test_lcp_paths(ctx, monkeypatch, lcp_sa, kind, n, seed, alpha):
+    """Both LCP sources give the reference stream: the LCP left behind by the suffix sort
+    (sa.hip k_heads_lcp, SALZ_LCP_SA=1, the default) and the Phi/PLCP stage (lcp.hip)."""
+    monkeypatch.setenv("SALZ_LCP_SA", lcp_sa)
+    src = _make(kind, n, seed, alpha)
+    out = ctx.encode(src)
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and out == ref
+
+
 def test_cli_roundtrip_matches_reference_container(salz, tmp_path):
     """salz_amd/salz (programs/salzcli.c mirror): -3 compresses to the reference container
     (blocks of 1 << 18, each the oracle's stream), -d restores the file, -k keeps the input."""
