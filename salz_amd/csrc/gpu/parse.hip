@@ -67,20 +67,6 @@ __global__ __launch_bounds__(kT) void k_cost_seed(uint32_t *cost, uint32_t n, ui
         cost[s] = 3u * (n - (uint32_t)p);
 }
 
-// Target state (cost estimate << 32 | exit) of a factor from p of length len: in-chunk targets
-// come from pst, targets at or past the chunk end b are exits costed by the previous pass.
-__device__ __forceinline__ uint64_t target_state(const uint64_t *pst, const uint32_t *cin,
-                                                 size_t base, uint32_t a, uint32_t b, uint32_t klog,
-                                                 uint32_t p, uint32_t len, uint32_t n, uint32_t *err)
-{
-    if (len < 3u)
-        return 0;
-    const uint32_t q = p + len;
-    if (bad_index(len > n - p, err, kErrParse))
-        return 0;
-    return q < b ? pst[base + ((size_t)(q - a) << 6)] : ((uint64_t)cin[sidx(q, klog)] << 32) | q;
-}
-
 // One lane per chunk, positions b-1 down to a. The states of the last kWin positions
 // (p+1 .. p+kWin) stay in registers, so a factor of length <= kWin reads its target from
 // there; a longer factor's target (p + len >= p + kWin + 1) was finished at least kWin + 1
@@ -106,11 +92,13 @@ __device__ __forceinline__ uint64_t far_state(const uint64_t *pst, const uint32_
 __global__ __launch_bounds__(kT) void k_parse_chunk(
     const uint4 *__restrict__ cand, const uint32_t *__restrict__ cin, uint64_t *__restrict__ pst,
     const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, uint32_t klog,
-    uint32_t *__restrict__ changed, uint32_t *err)
+    uint32_t *__restrict__ changed, uint32_t *err, uint32_t *__restrict__ eflag)
 {
     const uint32_t c = blockIdx.x * kT + threadIdx.x;  // chunk
     const uint64_t a64 = (uint64_t)c << klog;
     uint32_t diff = 0;
+    if (c == 0)
+        eflag[sidx(n, klog)] = 1u;  // the root of the exit forest
     if (a64 < n) {
         const uint32_t a = (uint32_t)a64;
         const uint32_t K = 1u << klog;
@@ -139,6 +127,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             const uint32_t q = b + k;
             win[k] = q <= n ? (((uint64_t)cin[sidx(q, klog)] << 32) | q) : 0;
         }
+        uint32_t last_ex = 0xffffffffu;
         for (uint32_t j = jn; j-- > 0;) {
             const uint32_t p = a + j;
             const uint4 c0 = cr[0];
@@ -180,6 +169,11 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             pst[slot(j)] = stp;
             chnew[slot(j)] = ch;
             diff += ch != orr[0];
+            // exit set E (every position's exit): consecutive positions mostly share one
+            if (ex != last_ex) {
+                eflag[sidx(ex, klog)] = 1u;
+                last_ex = ex;
+            }
             // shift the window and the rings one position down
 #pragma unroll
             for (uint32_t k = kWin - 1; k > 0; k--)
@@ -212,19 +206,8 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         atomicAdd(changed, diff);
 }
 
-// Exit flags and the compacted exit index live in storage (slot) order like the other parse
-// arrays: eflag[sidx(exit(p))] = 1 for every position, and for n (the root).
-__global__ void k_mark_exits(const uint64_t *__restrict__ pst, uint32_t n, uint32_t klog, size_t S,
-                             uint32_t *eflag)
-{
-    size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (s >= S)
-        return;
-    if (spos(s, klog) < n)
-        eflag[sidx((uint32_t)pst[s], klog)] = 1u;
-    if (s == 0)
-        eflag[sidx(n, klog)] = 1u;
-}
+// Exit flags (marked by the chunk pass) and the compacted exit index live in storage (slot)
+// order like the other parse arrays.
 
 // Compact E: node x = eidx[slot of q] for exit position q; parent = exit of q, weight =
 // in-chunk bit sum of q's path (estimate - cin[exit]).
@@ -251,38 +234,52 @@ __global__ void k_compact_exits(const uint32_t *__restrict__ eflag,
     }
 }
 
-__global__ void k_jump(const uint32_t *__restrict__ jt, const uint32_t *__restrict__ js,
-                       uint32_t *__restrict__ jt2, uint32_t *__restrict__ js2, uint32_t ne)
+// Pointer jumping over E, two levels per launch (the snapshot of every level is kept for
+// emission's path marking): from level k (jt, js) to k + 1 (jt1, written) and k + 2 (jt2, js2).
+// A thread derives its node's level-(k + 1) successor itself, so no other thread's result of
+// this launch is read.
+__global__ void k_jump2(const uint32_t *__restrict__ jt, const uint32_t *__restrict__ js,
+                        uint32_t *__restrict__ jt1, uint32_t *__restrict__ jt2,
+                        uint32_t *__restrict__ js2, uint32_t ne, int two)
 {
     uint32_t x = blockIdx.x * kT + threadIdx.x;
     if (x >= ne)
         return;
-    uint32_t p = jt[x];
-    js2[x] = js[x] + js[p];
-    jt2[x] = jt[p];
+    const uint32_t p = jt[x];
+    const uint32_t pp = jt[p];
+    const uint32_t s1 = js[x] + js[p];
+    if (!two) {  // last odd level
+        jt1[x] = pp;
+        js2[x] = s1;
+        return;
+    }
+    jt1[x] = pp;
+    const uint32_t q = jt[pp];
+    const uint32_t qq = jt[q];
+    jt2[x] = qq;
+    js2[x] = s1 + js[pp] + js[q];
 }
 
-__global__ void k_cost_exits(const uint32_t *__restrict__ elist, const uint32_t *__restrict__ js,
-                             uint32_t ne, uint32_t klog, uint32_t *__restrict__ cost)
-{
-    uint32_t x = blockIdx.x * kT + threadIdx.x;
-    if (x < ne)
-        cost[sidx(elist[x], klog)] = js[x];
-}
-
-// cost[p] = (in-chunk sum) + cost[exit] for every position that is not itself an exit.
-__global__ void k_cost_rest(const uint32_t *__restrict__ eflag, const uint64_t *__restrict__ pst,
+// Exact cost of every position: an exit's is its path sum (js after the jumps, through its
+// index in E), any other position adds its in-chunk bit sum to its exit's.
+__global__ void k_cost_rest(const uint32_t *__restrict__ eflag, const uint32_t *__restrict__ eidx,
+                            const uint32_t *__restrict__ js, const uint64_t *__restrict__ pst,
                             const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog, size_t S,
                             uint32_t *cost)
 {
     size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
     if (s >= S)
         return;
-    if (spos(s, klog) >= n || eflag[s])
+    const uint64_t p = spos(s, klog);
+    if (p > n)
         return;
+    if (eflag[s]) {
+        cost[s] = js[eidx[s]];
+        return;
+    }
     const uint64_t v = pst[s];
     const size_t se = sidx((uint32_t)v, klog);
-    cost[s] = (uint32_t)(v >> 32) - cin[se] + cost[se];
+    cost[s] = (uint32_t)(v >> 32) - cin[se] + js[eidx[se]];
 }
 
 }  // namespace
@@ -340,9 +337,10 @@ int stage_parse(Workspace &ws, uint32_t n)
         uint32_t *cin = cost[cur], *cout = cost[cur ^ 1];
         uint8_t *chold = choice[cur], *chnew = choice[cur ^ 1];
         SALZ_HIP(hipMemsetAsync(changed, 0, 4, st));
+        SALZ_HIP(hipMemsetAsync(eflag, 0, sizeof(uint32_t) * S, st));
         hipLaunchKernelGGL(k_parse_chunk, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
                            cin, ws.pst, chold, chnew, n, klog, changed,
-                           reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord);
+                           reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord, eflag);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 256, "parse.changed") != 0)
             return -1;
@@ -362,11 +360,7 @@ int stage_parse(Workspace &ws, uint32_t n)
             set_error("parse fixed point did not converge");
             return -1;
         }
-        // Exact costs for the new decisions.
-        SALZ_HIP(hipMemsetAsync(eflag, 0, sizeof(uint32_t) * S, st));
-        hipLaunchKernelGGL(k_mark_exits, dim3(grid_for(S, kT)), dim3(kT), 0, st, ws.pst, n, klog, S,
-                           eflag);
-        SALZ_LAUNCH_CHECK();
+        // Exact costs for the new decisions (E was marked by the chunk pass).
         if (scan_sum_u32(eflag, eidx, S, false, etotal, ws, st) != 0)
             return -1;
         if (read_scalars(ws, 0, 256, "parse.ne") != 0)
@@ -381,17 +375,16 @@ int stage_parse(Workspace &ws, uint32_t n)
                            ws.pst, cin, n, klog, S, elist, snap, js[0]);
         SALZ_LAUNCH_CHECK();
         int jc = 0;
-        for (uint32_t k = 0; k < K; k++) {
-            hipLaunchKernelGGL(k_jump, dim3(grid_for(ne, kT)), dim3(kT), 0, st, snap + (size_t)k * ne,
-                               js[jc], snap + (size_t)(k + 1) * ne, js[jc ^ 1], ne);
+        for (uint32_t k = 0; k < K; k += 2) {
+            const int two = k + 1 < K;
+            hipLaunchKernelGGL(k_jump2, dim3(grid_for(ne, kT)), dim3(kT), 0, st, snap + (size_t)k * ne,
+                               js[jc], snap + (size_t)(k + 1) * ne,
+                               two ? snap + (size_t)(k + 2) * ne : nullptr, js[jc ^ 1], ne, two);
             SALZ_LAUNCH_CHECK();
             jc ^= 1;
         }
-        hipLaunchKernelGGL(k_cost_exits, dim3(grid_for(ne, kT)), dim3(kT), 0, st, elist, js[jc], ne,
-                           klog, cout);
-        SALZ_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(S, kT)), dim3(kT), 0, st, eflag, ws.pst, cin, n,
-                           klog, S, cout);
+        hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(S, kT)), dim3(kT), 0, st, eflag, eidx, js[jc],
+                           ws.pst, cin, n, klog, S, cout);
         SALZ_LAUNCH_CHECK();
         ps.n_exit = ne;
         ps.levels = K;
