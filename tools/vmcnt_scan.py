@@ -17,22 +17,40 @@ WAIT = re.compile(r"s_waitcnt.*vmcnt\((\d+)\)")
 
 
 def scan(path):
+    """EXEC masks are modelled as a stack of regions: `s_and_saveexec` opens a region, `s_xor`,
+    `s_or_saveexec` / `s_andn2_saveexec` on EXEC switch to the sibling (else) region, `s_or_b64 exec, exec, s`
+    and `s_mov_b64 exec, s` join back to the enclosing one, and other EXEC writes (loop masks,
+    atomic optimisations) start a new region in place. Each VMEM op records its region."""
     hits = []
     kern = None
-    epoch = 0
-    pend = []
+    stack, nxt, pend = [0], 1, []
     for line in open(path):
         m = re.match(r"^[0-9a-f]+ <(.*)>:$", line)
         if m:
-            kern, epoch, pend = m.group(1), 0, []
+            kern, stack, nxt, pend = m.group(1), [0], 1, []
             continue
-        code = line.split("//")[0]
+        code = line.split("//")[0].strip()
+        if not code:
+            continue
+        op = code.split()[0]
+        args = code[len(op):].replace(" ", "")
         if VMEM.match(code):
-            pend.append(epoch)
-        elif "exec" in code and re.match(r"^\s*s_", code) and not code.strip().startswith("s_cbranch"):
-            dst = code.split()[1] if len(code.split()) > 1 else ""
-            if "saveexec" in code or dst.startswith("exec"):
-                epoch += 1
+            pend.append(stack[-1])
+        elif op.startswith("s_") and not op.startswith("s_cbranch") and (
+                "saveexec" in op or args.startswith("exec,") or args.startswith("exec")):
+            if op == "s_and_saveexec_b64":
+                stack.append(nxt)
+            elif op in ("s_andn2_saveexec_b64", "s_or_saveexec_b64") or (
+                    op == "s_xor_b64" and args.startswith("exec,exec")):
+                stack[-1] = nxt  # else-entry of an if/else: a sibling region
+            elif (op == "s_or_b64" and args.startswith("exec,exec,")) or (
+                    op == "s_mov_b64" and args.startswith("exec,")):
+                if len(stack) > 1:
+                    stack.pop()
+                nxt -= 1  # no new region opened
+            else:
+                stack[-1] = nxt
+            nxt += 1
         w = WAIT.search(code)
         if w:
             k = int(w.group(1))
@@ -41,7 +59,7 @@ def scan(path):
             elif len(pend) > k:
                 done, out = pend[:-k], pend[-k:]
                 if set(out) - set(done) and set(done) - set(out):
-                    hits.append((kern, code.strip()))
+                    hits.append((kern, code))
                 pend = out
     return hits
 
