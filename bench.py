@@ -78,7 +78,17 @@ def main():
         # tools/runtime_check.py); only gloo CPU tensors are used.
         import torch.distributed as dist
 
-        dist.init_process_group("gloo")
+        # gloo prints its mesh-connection notice on fd 1; keep stdout to the one JSON line
+        sys.stdout.flush()
+        saved, null = os.dup(1), os.open(os.devnull, os.O_WRONLY)
+        os.dup2(null, 1)
+        try:
+            dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+            os.close(null)
 
     import salz_amd
     from salz_amd.dist import block_count, my_blocks
