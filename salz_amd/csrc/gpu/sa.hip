@@ -108,16 +108,11 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
                          uint32_t *__restrict__ nval, uint32_t *__restrict__ ngid,
                          uint32_t *__restrict__ rank, uint32_t *__restrict__ sa, GroupTab tab,
                          uint32_t m, uint32_t n, int kb_old, int round0, uint32_t *err,
-                         uint32_t ilo, uint32_t ihi, int pass0)
+                         uint32_t ihi, uint32_t *__restrict__ later)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
         return;
-    if (!pass0) {  // later passes only write the rank of suffixes in [ilo, ihi)
-        const uint32_t i0 = val[c];
-        if (i0 < ilo || i0 >= ihi)
-            return;
-    }
     uint32_t g = gall[c] - 1u;
     uint32_t hp = headpos[g];
     uint32_t size = headpos[g + 1] - hp;
@@ -129,13 +124,14 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     // are unchanged; every other rank (and all of round 0) is written.
     const bool same = !round0 && (hp == 0 || (key[hp - 1] >> kb_old) != (key[hp] >> kb_old));
     // rank[i] is a random 4-byte scatter (a read-modify-write of a whole HBM burst). Large
-    // rounds split it by text range over two passes, so the rank lines one pass writes fit
-    // in the 256 MB Infinity Cache and are merged there; pass 0 does
-    // everything else.
-    if (!same && i >= ilo && i < ihi)
-        rank[i] = hp + o + 1u;
-    if (!pass0)
-        return;
+    // rounds split it by text range: this kernel writes the ranks of i < ihi and leaves the
+    // others, in list order, to k_rank_upper, so the rank lines each pass writes fit in the
+    // 256 MB Infinity Cache and are merged there.
+    const uint32_t rv = same ? 0xffffffffu : hp + o + 1u;
+    if (!same && i < ihi)
+        rank[i] = rv;
+    if (later)
+        later[c] = rv;
     if (size == 1) {
         sa[c + o] = i;
     } else {
@@ -245,6 +241,18 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
         if ((int)lane == src)
             lcps[sp] = hk + mis;
     }
+}
+
+// Second pass of a split rank scatter: ranks of suffixes i >= ilo, from k_commit's list.
+__global__ void k_rank_upper(const uint32_t *__restrict__ val, const uint32_t *__restrict__ later,
+                             uint32_t m, uint32_t ilo, uint32_t *__restrict__ rank)
+{
+    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (c >= m)
+        return;
+    const uint32_t i = val[c], rv = later[c];
+    if (i >= ilo && rv != 0xffffffffu)
+        rank[i] = rv;
 }
 
 // Window plan of the LDS sort, one thread per surviving group (groups are in list order, so
@@ -696,13 +704,15 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         // Large rounds: the rank scatter in two text-range passes (k_commit comment).
         // (only where most ranks change: round 0, or a round that multiplied the groups)
         const bool many = round0 || (uint64_t)G >= (uint64_t)split_ratio * G_act;
-        const int split = (m >= (32u << 20) && split_on && many) ? 2 : 1;
-        for (int ps = 0; ps < split; ps++) {
-            const uint32_t ilo = ps == 0 ? 0u : n / 2;
-            const uint32_t ihi = ps + 1 == split ? 0xffffffffu : n / 2;
-            hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, gall, headpos,
-                               gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, kb_old,
-                               round0, derr, ilo, ihi, ps == 0 ? 1 : 0);
+        const bool split = m >= (32u << 20) && split_on && many;
+        uint32_t *later = reinterpret_cast<uint32_t *>(Kx);  // free until k_keys
+        hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, gall, headpos,
+                           gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, kb_old,
+                           round0, derr, split ? n / 2 : 0xffffffffu, split ? later : nullptr);
+        SALZ_LAUNCH_CHECK();
+        if (split) {
+            hipLaunchKernelGGL(k_rank_upper, dim3(grid_for(m, kT)), dim3(kT), 0, st, V, later, m,
+                               n / 2, ws.rank);
             SALZ_LAUNCH_CHECK();
         }
         if (read_scalars(ws, 0, 256, "sa.m") != 0)
