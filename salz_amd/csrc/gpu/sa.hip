@@ -19,11 +19,14 @@
 //               write); large groups are extracted, radix-sorted on (large-group id, rank)
 //               and put back (k_extract / k_putback). Ties may land in any order: equal keys
 //               stay one group, so the next round re-sorts them.
-//   k_heads     group-head flags of the sorted active list
+//   k_heads_lcp group-head flags of the sorted active list, and the LCP of every new head
+//               with its predecessor (see the comment there; k_heads once the LCP is left to
+//               the Phi/PLCP stage)
 //   scan        -> group ids; k_headpos -> head index per group
 //   k_grpkeep   groups of size >= 2 survive; u64 scans pack (new gid, compact start) and
 //               (large-group id, start in the extracted array)
-//   k_commit    rank update for every active suffix, SA write for singletons, compaction
+//   k_commit    rank update for every active suffix (in large rounds the upper text half
+//               through k_rank_upper), SA write for singletons, compaction
 //   k_keys      next round's keys: gid << kb | rank[i + h]
 #include "internal.hpp"
 
