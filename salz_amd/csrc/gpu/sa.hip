@@ -246,15 +246,15 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
     }
 }
 
-// Second pass of a split rank scatter: ranks of suffixes i >= ilo, from k_commit's list.
+// Later passes of a split rank scatter: ranks of suffixes in [ilo, ihi), from k_commit's list.
 __global__ void k_rank_upper(const uint32_t *__restrict__ val, const uint32_t *__restrict__ later,
-                             uint32_t m, uint32_t ilo, uint32_t *__restrict__ rank)
+                             uint32_t m, uint32_t ilo, uint32_t ihi, uint32_t *__restrict__ rank)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
         return;
     const uint32_t i = val[c], rv = later[c];
-    if (i >= ilo && rv != 0xffffffffu)
+    if (i >= ilo && i < ihi && rv != 0xffffffffu)
         rank[i] = rv;
 }
 
@@ -704,18 +704,24 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
             hipLaunchKernelGGL(k_dbg_gsc, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, gsc, G, ws.hscal[8], derr);
             SALZ_LAUNCH_CHECK();
         }
-        // Large rounds: the rank scatter in two text-range passes (k_commit comment).
-        // (only where most ranks change: round 0, or a round that multiplied the groups)
-        const bool many = round0 || (uint64_t)G >= (uint64_t)split_ratio * G_act;
-        const bool split = m >= (32u << 20) && split_on && many;
+        // Large rounds: the rank scatter in text-range passes of at most ~200 MB of rank array
+        // each (the Infinity Cache holds 256 MB; k_commit comment). Worth it where many ranks
+        // change: round 0, a round that multiplied the groups, or any round once the rank
+        // array is past 400 MB (a scatter over 1 GB costs ~3x one over 200 MB,
+        // profiles/r01t_scatter_bench.txt; Fibonacci 256 MiB: SA 691 -> 657 ms).
+        const uint32_t parts_all = (uint32_t)(((uint64_t)n * 4 + (200u << 20) - 1) / (200u << 20));
+        const uint32_t ratio = parts_all >= 3 ? 1u : split_ratio;
+        const bool many = round0 || (uint64_t)G >= (uint64_t)ratio * G_act;
+        const uint32_t parts = (m >= (32u << 20) && split_on && many) ? (parts_all > 1 ? parts_all : 2) : 1;
+        const uint32_t span = (uint32_t)(((uint64_t)n + parts - 1) / parts);
         uint32_t *later = reinterpret_cast<uint32_t *>(Kx);  // free until k_keys
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, gall, headpos,
                            gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, kb_old,
-                           round0, derr, split ? n / 2 : 0xffffffffu, split ? later : nullptr);
+                           round0, derr, parts > 1 ? span : 0xffffffffu, parts > 1 ? later : nullptr);
         SALZ_LAUNCH_CHECK();
-        if (split) {
+        for (uint32_t q = 1; q < parts; q++) {
             hipLaunchKernelGGL(k_rank_upper, dim3(grid_for(m, kT)), dim3(kT), 0, st, V, later, m,
-                               n / 2, ws.rank);
+                               q * span, q + 1 == parts ? 0xffffffffu : (q + 1) * span, ws.rank);
             SALZ_LAUNCH_CHECK();
         }
         if (read_scalars(ws, 0, 256, "sa.m") != 0)
