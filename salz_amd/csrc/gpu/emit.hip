@@ -175,17 +175,32 @@ struct Sink {
             cnt -= take;
         }
     }
+    // A zero run: the words it covers whole are left as they are (W is zeroed beforehand; the
+    // first one's Yk is written, the others' (0 here) are filled in by a max-scan, as no raw
+    // byte is emitted inside the run),
+    // so a factor of length L costs O(1) rather than O(L / 512) (Fibonacci: runs of 10^7 bits).
     __device__ __forceinline__ void zeros(uint64_t cnt)
     {
-        while (cnt) {
-            uint64_t k = B >> 6;
-            uint32_t o = (uint32_t)(B & 63);
-            uint64_t take = cnt < (uint64_t)(64 - o) ? cnt : (uint64_t)(64 - o);
+        if (!cnt)
+            return;
+        uint64_t k = B >> 6;
+        uint32_t o = (uint32_t)(B & 63);
+        const uint64_t take = cnt < (uint64_t)(64 - o) ? cnt : (uint64_t)(64 - o);
+        enter(k);
+        if (o == 0)
+            Yk[k] = (uint32_t)Y;
+        B += take;
+        cnt -= take;
+        if (cnt >= 64) {  // whole words; B is at a word start here
+            Yk[B >> 6] = (uint32_t)Y;  // bytes may have been emitted inside the previous word
+            B += cnt & ~(uint64_t)63;
+            cnt &= 63;
+        }
+        if (cnt) {
+            k = B >> 6;
             enter(k);
-            if (o == 0)
-                Yk[k] = (uint32_t)Y;
-            B += take;
-            cnt -= take;
+            Yk[k] = (uint32_t)Y;
+            B += cnt;
         }
     }
     __device__ __forceinline__ void byte(uint8_t c)
@@ -318,10 +333,14 @@ int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap, 
     } else {
         *hdr = (1u << 24) | ((uint32_t)(L - 4) & 0xffffffu);
         SALZ_HIP(hipMemsetAsync(W, 0, sizeof(uint64_t) * (nwords + 1), st));
+        SALZ_HIP(hipMemsetAsync(Yk, 0, sizeof(uint32_t) * (nwords + 1), st));
         hipLaunchKernelGGL(k_emit_write, dim3(grid_for((size_t)nch + 1, kT)), dim3(kT), 0, st,
                            ws.text, ws.cand, ps.choice, entry, n, N, ps.chunk, nch, cbits, cbytes,
                            btotal, W, Yk, dst, ws.klog);
         SALZ_LAUNCH_CHECK();
+        // Yk of the words inside zero runs (Sink::zeros): Yk is non-decreasing in k
+        if (scan_max_u32(Yk, Yk, nwords, true, nullptr, ws, st) != 0)
+            return -1;
         hipLaunchKernelGGL(k_place_words, dim3(grid_for(nwords, kT)), dim3(kT), 0, st, W, Yk,
                            nwords, dst);
         SALZ_LAUNCH_CHECK();
