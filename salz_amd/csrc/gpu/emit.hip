@@ -71,6 +71,14 @@ __global__ void k_mark_step(const uint32_t *__restrict__ jt, uint32_t *emark, ui
         emark[jt[x]] = 1u;
 }
 
+// next pointer-jumping level of the E forest's parents (emission without stored levels)
+__global__ void k_jt_double(const uint32_t *__restrict__ jt, uint32_t *__restrict__ jt2, uint32_t ne)
+{
+    uint32_t x = blockIdx.x * kT + threadIdx.x;
+    if (x < ne)
+        jt2[x] = jt[jt[x]];
+}
+
 __global__ void k_entries(const uint32_t *__restrict__ emark, const uint32_t *__restrict__ elist,
                           uint32_t ne, uint32_t n, uint32_t chunk, uint32_t *__restrict__ entry)
 {
@@ -292,9 +300,20 @@ int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap, 
         SALZ_HIP(hipMemsetAsync(emark, 0, sizeof(uint32_t) * ne, st));
         hipLaunchKernelGGL(k_mark_start, dim3(1), dim3(1), 0, st, eidx, ps.pst, ws.klog, emark);
         SALZ_LAUNCH_CHECK();
+        const uint32_t *lev = ps.jt0;  // parents 2^k steps up (level k)
+        uint32_t *pp[2] = {ws.u2, ws.u3};  // recomputed levels when the parse kept only level 0
         for (uint32_t k = 0; k < ps.levels; k++) {
-            hipLaunchKernelGGL(k_mark_step, dim3(grid_for(ne, kT)), dim3(kT), 0, st,
-                               ps.jt0 + (size_t)k * ne, emark, ne);
+            if (k > 0) {
+                if (ps.snaps) {
+                    lev = ps.jt0 + (size_t)k * ne;
+                } else {
+                    hipLaunchKernelGGL(k_jt_double, dim3(grid_for(ne, kT)), dim3(kT), 0, st, lev,
+                                       pp[k & 1], ne);
+                    SALZ_LAUNCH_CHECK();
+                    lev = pp[k & 1];
+                }
+            }
+            hipLaunchKernelGGL(k_mark_step, dim3(grid_for(ne, kT)), dim3(kT), 0, st, lev, emark, ne);
             SALZ_LAUNCH_CHECK();
         }
         hipLaunchKernelGGL(k_entries, dim3(grid_for(ne, kT)), dim3(kT), 0, st, emark, ps.elist, ne,

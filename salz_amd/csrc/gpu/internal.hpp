@@ -36,7 +36,9 @@ struct ParseState {
     uint32_t n_exit;        // |E|
     uint32_t *elist;        // E nodes (positions), ascending; last is n
     uint32_t *jt0;          // parent (compact) per E node, snapshot level 0
-    uint32_t levels;        // pointer-jumping snapshots stored at jt0 + k*n_exit
+    uint32_t levels;        // pointer-jumping levels
+    bool snaps;             // all levels stored at jt0 + k*n_exit (else emission recomputes
+                            // them from level 0 in two ping-pong buffers)
 };
 
 struct Workspace {

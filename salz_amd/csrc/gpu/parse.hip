@@ -356,7 +356,9 @@ int stage_parse(Workspace &ws, uint32_t n)
             ps.cost = cin;
             break;
         }
-        if (it > 4096) {
+        // After t passes the last t chunks hold exact decisions (the last one sees only exact
+        // costs, then induction), so nchunks + 1 passes always suffice.
+        if ((uint32_t)it > ps.nchunks + 1) {
             set_error("parse fixed point did not converge");
             return -1;
         }
@@ -367,27 +369,44 @@ int stage_parse(Workspace &ws, uint32_t n)
             return -1;
         const uint32_t ne = reinterpret_cast<uint32_t *>(ws.hscal)[49];
         const uint32_t K = (uint32_t)bit_width(ne > 1 ? ne - 1 : 0);
-        if ((size_t)(K + 1) * ne > snap_cap) {
-            set_error("parse: exit forest too large for snapshot area (|E|=%u)", ne);
+        // Every level's parents are kept for emission's path marking when they fit (the usual
+        // case); a large E (short factors in short chunks) keeps level 0 only and jumps
+        // through two ping-pong buffers, and emission recomputes the levels.
+        const bool snaps = (size_t)(K + 1) * ne <= snap_cap;
+        if (ne > ws.cap_n + 2) {
+            set_error("parse: exit set larger than the text (|E|=%u)", ne);
             return -1;
         }
         hipLaunchKernelGGL(k_compact_exits, dim3(grid_for(S, kT)), dim3(kT), 0, st, eflag, eidx,
                            ws.pst, cin, n, klog, S, elist, snap, js[0]);
         SALZ_LAUNCH_CHECK();
         int jc = 0;
-        for (uint32_t k = 0; k < K; k += 2) {
-            const int two = k + 1 < K;
-            hipLaunchKernelGGL(k_jump2, dim3(grid_for(ne, kT)), dim3(kT), 0, st, snap + (size_t)k * ne,
-                               js[jc], snap + (size_t)(k + 1) * ne,
-                               two ? snap + (size_t)(k + 2) * ne : nullptr, js[jc ^ 1], ne, two);
-            SALZ_LAUNCH_CHECK();
-            jc ^= 1;
+        if (snaps) {
+            for (uint32_t k = 0; k < K; k += 2) {
+                const int two = k + 1 < K;
+                hipLaunchKernelGGL(k_jump2, dim3(grid_for(ne, kT)), dim3(kT), 0, st,
+                                   snap + (size_t)k * ne, js[jc], snap + (size_t)(k + 1) * ne,
+                                   two ? snap + (size_t)(k + 2) * ne : nullptr, js[jc ^ 1], ne, two);
+                SALZ_LAUNCH_CHECK();
+                jc ^= 1;
+            }
+        } else {
+            uint32_t *pp[2] = {ws.u2, ws.u3};  // free during the parse
+            const uint32_t *cur = snap;
+            for (uint32_t k = 0; k < K; k++) {
+                hipLaunchKernelGGL(k_jump2, dim3(grid_for(ne, kT)), dim3(kT), 0, st, cur, js[jc],
+                                   pp[k & 1], nullptr, js[jc ^ 1], ne, 0);
+                SALZ_LAUNCH_CHECK();
+                cur = pp[k & 1];
+                jc ^= 1;
+            }
         }
         hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(S, kT)), dim3(kT), 0, st, eflag, eidx, js[jc],
                            ws.pst, cin, n, klog, S, cout);
         SALZ_LAUNCH_CHECK();
         ps.n_exit = ne;
         ps.levels = K;
+        ps.snaps = snaps;
         ps.elist = elist;
         ps.jt0 = snap;
     }

@@ -193,6 +193,18 @@ def test_large_blocks_match_oracle(salz, kind, n):
     c.close()
 
 
+@pytest.mark.parametrize("alpha,n", [(2, 16_777_216), (4, 9_000_001)])
+def test_large_exit_set_matches_oracle(salz, alpha, n):
+    """Short factors in short chunks: the exit set E outgrows the space for every pointer-
+    jumping level (|E| ~ 2 M at 16 MiB of a binary alphabet), so the parse keeps level 0
+    only and emission recomputes the levels (parse.hip, emit.hip)."""
+    src = gen("smx", n, 5, alpha)
+    rc, ref = oracle_encode(src)
+    c = salz.Context(0, n)
+    assert rc == 0 and c.encode(src) == ref
+    c.close()
+
+
 def test_fib_256mib_golden(salz):
     """SURVEY App. C / BASELINE configs[4]: 256 MiB Fibonacci word, one block, against the
     reference's golden output hash (the oracle would take minutes at this size)."""

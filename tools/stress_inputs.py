@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Pathological inputs at large sizes: time one GPU encode, round-trip it, and (with --parity)
+compare with the CPU port.  python tools/stress_inputs.py [--size N] [--parity]"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import salz_amd  # noqa: E402
+from tests.helpers import gen, oracle_encode  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--size", type=int, default=64 << 20)
+ap.add_argument("--parity", action="store_true")
+a = ap.parse_args()
+n = a.size
+cases = {
+    "zeros": lambda: np.zeros(n, np.uint8),
+    "period3": lambda: np.resize(np.frombuffer(b"abc", np.uint8), n),
+    "period1000": lambda: np.resize(gen("smx", 1000, 7, 256), n),
+    "random": lambda: gen("smx", n, 3, 256),
+    "binary2": lambda: gen("smx", n, 5, 2),
+    "fib": lambda: gen("fib", n),
+}
+ctx = salz_amd.Context(0, n)
+for name, make in cases.items():
+    src = make()
+    ctx.encode(src[: 1 << 20])  # warm
+    t0 = time.perf_counter()
+    out = ctx.encode(src)
+    t1 = time.perf_counter()
+    ok = salz_amd.decode_safe(out, n, frame=True) == src.tobytes()
+    line = f"{name:11s} {n} B -> {len(out)} B  {(t1 - t0) * 1e3:8.1f} ms  {n / (t1 - t0) / 1e6:8.1f} MB/s  roundtrip {ok}"
+    if a.parity:
+        rc, ref = oracle_encode(src)
+        line += f"  parity {rc == 0 and ref == out}"
+    print(line, flush=True)
