@@ -206,6 +206,48 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         atomicAdd(changed, diff);
 }
 
+// Uniform-shift test of one chunk per lane (see the host loop): every target at or past the
+// chunk end b (the literal's b, and each candidate's p + len beyond it) must have moved by the
+// same delta from cold to cnew; costs at or above 2^30 fail it (int32 compares could wrap).
+// *fail counts the chunks that do not pass.
+__global__ __launch_bounds__(kT) void k_parse_check(const uint4 *__restrict__ cand,
+                                                    const uint32_t *__restrict__ cnew,
+                                                    const uint32_t *__restrict__ cold, uint32_t n,
+                                                    uint32_t klog, uint32_t *fail)
+{
+    const uint32_t c = blockIdx.x * kT + threadIdx.x;
+    const uint64_t a64 = (uint64_t)c << klog;
+    bool bad = false;
+    if (a64 < n) {
+        const uint32_t a = (uint32_t)a64, K = 1u << klog;
+        const uint32_t b = (n - a) < K ? n : a + K;
+        const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
+        const size_t sb = sidx(b, klog);
+        const uint32_t nb = cnew[sb];
+        const uint32_t d0 = nb - cold[sb];  // the literal from b - 1
+        bad = nb >= (1u << 30);
+        for (uint32_t j = 0; j < b - a && !bad; j++) {
+            const uint32_t p = a + j;
+            const uint4 cd = cand[base + ((size_t)j << 6)];
+            if (p == 0)
+                continue;
+            if (cd.y >= 3u && p + cd.y >= b) {
+                const size_t sq = sidx(p + cd.y, klog);
+                const uint32_t v = cnew[sq];
+                bad |= v - cold[sq] != d0 || v >= (1u << 30);
+            }
+            if (cd.w >= 3u && p + cd.w >= b) {
+                const size_t sq = sidx(p + cd.w, klog);
+                const uint32_t v = cnew[sq];
+                bad |= v - cold[sq] != d0 || v >= (1u << 30);
+            }
+        }
+    }
+    const uint64_t m = wave_ballot(bad);
+    if (lane_id() == 0 && m)
+        atomicAdd(fail, (uint32_t)__popcll(m));
+}
+
 // Exit flags (marked by the chunk pass) and the compacted exit index live in storage (slot)
 // order like the other parse arrays.
 
@@ -409,6 +451,25 @@ int stage_parse(Workspace &ws, uint32_t n)
         ps.snaps = snaps;
         ps.elist = elist;
         ps.jt0 = snap;
+        // Convergence without a confirming pass: if every chunk's targets beyond its end all
+        // moved by one common delta between the costs this pass used (cin) and the exact costs
+        // of its decisions (cout), every option of every position moved by that delta, so the
+        // next pass would repeat these decisions (k_parse_check). The test costs about as much
+        // as a pass, so it is tried once, after the second pass, when few decisions changed:
+        // text (3 passes) then stops one pass early; mixed data (~12 passes) never tries.
+        if (it == 1 && (uint64_t)nchanged * 64 < n) {
+            SALZ_HIP(hipMemsetAsync(changed, 0, 4, st));
+            hipLaunchKernelGGL(k_parse_check, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
+                               cout, cin, n, klog, changed);
+            SALZ_LAUNCH_CHECK();
+            if (read_scalars(ws, 0, 256, "parse.check") != 0)
+                return -1;
+            if (reinterpret_cast<uint32_t *>(ws.hscal)[48] == 0) {
+                ps.choice = chnew;
+                ps.cost = cout;
+                break;
+            }
+        }
     }
     ws.stats.parse_iters = it + 1;
     ws.stats.exit_nodes = ps.n_exit;

@@ -120,6 +120,30 @@ int parse_sim(const int32_t *psv, const int32_t *lp, const int32_t *nsv, const i
         for (int32_t q = n - 1; q >= 0; q--) /* backward: targets are exact already */
             cout[q] = sm[q] + cout[ex[q]];
         uint32_t *tc = cin; cin = cout; cout = tc;
+        if (getenv("PARSE_SIM_VERBOSE")) {
+            /* chunks whose out-of-chunk targets did not all shift by one delta (cin = new
+               exact costs, cout = the costs the pass just used) */
+            long bad = 0, nch = 0;
+            for (int32_t a = 0; a < n; a += chunk, nch++) {
+                int32_t b = a + chunk < n ? a + chunk : n;
+                int have = 0, fail = 0;
+                uint32_t d0 = 0;
+                for (int32_t p = a; p < b && !fail; p++) {
+                    uint32_t qs[3] = {(uint32_t)p + 1, p && lp[p] >= 3 ? (uint32_t)(p + lp[p]) : 0,
+                                      p && ln[p] >= 3 ? (uint32_t)(p + ln[p]) : 0};
+                    for (int k = 0; k < 3; k++) {
+                        uint32_t q = qs[k];
+                        if (q < (uint32_t)b)
+                            continue;
+                        uint32_t d = cin[q] - cout[q];
+                        if (!have) { d0 = d; have = 1; }
+                        else if (d != d0) { fail = 1; break; }
+                    }
+                }
+                bad += fail;
+            }
+            fprintf(stderr, "   after it %d: %ld of %ld chunks see non-uniform target shifts\n", it, bad, nch);
+        }
     }
     int ok = 1;
     for (int32_t p = 1; p < n; p++)
