@@ -226,20 +226,25 @@ __global__ __launch_bounds__(kT) void k_parse_check(const uint4 *__restrict__ ca
         const uint32_t nb = cnew[sb];
         const uint32_t d0 = nb - cold[sb];  // the literal from b - 1
         bad = nb >= (1u << 30);
-        for (uint32_t j = 0; j < b - a && !bad; j++) {
-            const uint32_t p = a + j;
-            const uint4 cd = cand[base + ((size_t)j << 6)];
-            if (p == 0)
-                continue;
-            if (cd.y >= 3u && p + cd.y >= b) {
-                const size_t sq = sidx(p + cd.y, klog);
-                const uint32_t v = cnew[sq];
-                bad |= v - cold[sq] != d0 || v >= (1u << 30);
+        const uint32_t jn = b - a;
+        // eight rows per step, loads first (no early exit: the loads stay in flight together)
+        for (uint32_t j0 = 0; j0 < jn; j0 += 8) {
+            uint4 cd[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) {
+                const uint32_t j = j0 + u < jn ? j0 + u : jn - 1;
+                cd[u] = cand[base + ((size_t)j << 6)];
             }
-            if (cd.w >= 3u && p + cd.w >= b) {
-                const size_t sq = sidx(p + cd.w, klog);
-                const uint32_t v = cnew[sq];
-                bad |= v - cold[sq] != d0 || v >= (1u << 30);
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) {
+                const uint32_t p = a + j0 + u;
+                const bool on = j0 + u < jn && p != 0;
+                const bool xp = on && cd[u].y >= 3u && p + cd[u].y >= b;
+                const bool xn = on && cd[u].w >= 3u && p + cd[u].w >= b;
+                const size_t sp = sidx(xp ? p + cd[u].y : b, klog), sn = sidx(xn ? p + cd[u].w : b, klog);
+                const uint32_t vp = cnew[sp], vn = cnew[sn];
+                bad |= vp - cold[sp] != d0 || vp >= (1u << 30);
+                bad |= vn - cold[sn] != d0 || vn >= (1u << 30);
             }
         }
     }

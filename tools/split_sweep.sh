@@ -1,4 +1,2 @@
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pt.log 2>&1; tail -2 gpurun_out/pt.log
 bash tools/ab.sh 2
-bash tools/ab.sh 1 --kind mixed --steps 2
-bash tools/ab.sh 1 --workload silesia --steps 2
