@@ -49,8 +49,10 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t m, int shift,
     const uint32_t *__restrict__ offs, uint32_t ntiles)
 {
+    // Keys and values are staged one after the other in the same 32 KB (4 workgroups per CU
+    // instead of 2 with a 48 KB key + value stage).
     __shared__ uint64_t skey[kTile];
-    __shared__ uint32_t sval[kTile];
+    uint32_t *sval = reinterpret_cast<uint32_t *>(skey);
     __shared__ uint32_t cnt[4][256];
     __shared__ uint32_t dstart[256];
     __shared__ uint32_t gbase[256];
@@ -128,26 +130,43 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     }
     __syncthreads();
 
+    uint32_t pos[kItems];  // tile-local sorted position of each item
 #pragma unroll
     for (int j = 0; j < kItems; j++) {
         size_t i = base + (size_t)j * 64 + lane;
-        if (i < m) {
-            unsigned d = (unsigned)(k[j] >> shift) & 255u;
-            uint32_t s = dstart[d] + cnt[wave][d] + lrank[j];
-            skey[s] = k[j];
-            sval[s] = v[j];
-        }
+        unsigned d = (unsigned)(k[j] >> shift) & 255u;
+        pos[j] = dstart[d] + cnt[wave][d] + lrank[j];
+        if (i < m)
+            skey[pos[j]] = k[j];
     }
     __syncthreads();
 
     size_t tbase = (size_t)blockIdx.x * kTile;
     uint32_t tcount = (uint32_t)((m - tbase) < (size_t)kTile ? (m - tbase) : (size_t)kTile);
-    for (uint32_t s = tid; s < tcount; s += kThreads) {
-        uint64_t key = skey[s];
-        unsigned d = (unsigned)(key >> shift) & 255u;
-        uint32_t g = gbase[d] + (s - dstart[d]);
-        kout[g] = key;
-        vout[g] = sval[s];
+    uint32_t gdst[kItems];  // global destination of staged slot tid + j * kThreads
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        const uint32_t s = tid + (uint32_t)j * kThreads;
+        if (s < tcount) {
+            uint64_t key = skey[s];
+            unsigned d = (unsigned)(key >> shift) & 255u;
+            gdst[j] = gbase[d] + (s - dstart[d]);
+            kout[gdst[j]] = key;
+        }
+    }
+    __syncthreads();  // keys out of LDS; the same bytes now stage the values
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        size_t i = base + (size_t)j * 64 + lane;
+        if (i < m)
+            sval[pos[j]] = v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        const uint32_t s = tid + (uint32_t)j * kThreads;
+        if (s < tcount)
+            vout[gdst[j]] = sval[s];
     }
 }
 
