@@ -361,8 +361,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
                                                            uint32_t *__restrict__ V, SegPlan plan,
                                                            uint32_t m, int kb, uint32_t *err)
 {
-    __shared__ uint64_t sk[kSegCap];
-    __shared__ uint32_t sv[kSegCap];
+    __shared__ uint64_t sk[kSegCap];  // keys; at the end the window's values (as u32)
     __shared__ uint32_t cnt[4][256];
     __shared__ uint32_t dstart[256];
     __shared__ uint32_t wsum[4];
@@ -387,7 +386,6 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
         if (i < count) {
             const uint64_t kk = K[lo + i];
             key = (((kk >> kb) - g0) << (kb + 12)) | ((kk & mask) << 12) | i;
-            sv[i] = V[lo + i];
         }
         sk[i] = key;
     }
@@ -398,11 +396,28 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
     default: seg_lsd<16>(sk, cnt, dstart, wsum, nbits); break;
     }
 
-    for (uint32_t i = tid; i < count; i += kSegThreads) {
-        const uint64_t key = sk[i];
-        const uint64_t g = g0 + (key >> (kb + 12));
-        K[lo + i] = (g << kb) | ((key >> 12) & mask);
-        V[lo + i] = sv[key & 0xfffu];
+    // Sorted keys to registers, then the same LDS bytes take the window's values (read only
+    // now: a separate 16 KB value stage would leave room for 3 workgroups per CU instead of 4).
+    uint64_t outk[kSegCap / kSegThreads];
+#pragma unroll
+    for (uint32_t j = 0; j < kSegCap / kSegThreads; j++) {
+        const uint32_t i = tid + j * kSegThreads;
+        outk[j] = i < count ? sk[i] : 0ull;
+    }
+    __syncthreads();
+    uint32_t *sv = reinterpret_cast<uint32_t *>(sk);
+    for (uint32_t i = tid; i < count; i += kSegThreads)
+        sv[i] = V[lo + i];
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kSegCap / kSegThreads; j++) {
+        const uint32_t i = tid + j * kSegThreads;
+        if (i < count) {
+            const uint64_t key = outk[j];
+            const uint64_t g = g0 + (key >> (kb + 12));
+            K[lo + i] = (g << kb) | ((key >> 12) & mask);
+            V[lo + i] = sv[key & 0xfffu];
+        }
     }
 }
 
