@@ -2,7 +2,8 @@
 //
 // One 8-bit digit per pass, 4096-element tiles (256 threads x 16 items), reduce-then-scan:
 //   k_radix_hist    per-tile digit counts (LDS atomics into per-wave sub-histograms)
-//   scan            digit-major exclusive scan of the counts -> global tile offsets
+//   k_radix_rowscan per-digit prefixes of the counts over the tiles (+ digit totals; the
+//                   scatter adds the digit bases)
 //   k_radix_scatter stable tile-local ranking with wave ballots (8 ballots build the peer
 //                   mask of lanes sharing a digit; mbcnt gives the rank below), then the
 //                   tile is staged in LDS in digit order and written out in contiguous runs.
@@ -44,10 +45,62 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
     counts[(size_t)tid * ntiles + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
+// Digit-major tile counts -> per-digit exclusive prefixes over the tiles (in place), one
+// workgroup per digit, plus the digit totals; k_radix_scatter adds the digit bases (an
+// exclusive scan of the 256 totals) itself. One launch instead of a three-kernel device scan.
+constexpr int kRowThreads = 1024;
+constexpr int kRowItems = 4;
+__global__ __launch_bounds__(kRowThreads) void k_radix_rowscan(uint32_t *__restrict__ counts,
+                                                               uint32_t ntiles,
+                                                               uint32_t *__restrict__ totals)
+{
+    __shared__ uint32_t wsum[kRowThreads / 64];
+    uint32_t *row = counts + (size_t)blockIdx.x * ntiles;
+    const unsigned tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < ntiles; base += kRowThreads * kRowItems) {
+        uint32_t v[kRowItems], sum = 0;
+#pragma unroll
+        for (int j = 0; j < kRowItems; j++) {
+            const uint32_t i = base + tid * kRowItems + j;
+            v[j] = i < ntiles ? row[i] : 0u;
+            sum += v[j];
+        }
+        uint32_t x = sum;
+#pragma unroll
+        for (unsigned d = 1; d < 64; d <<= 1) {
+            const uint32_t y = shfl_up_u32(x, d);
+            if (lane >= d)
+                x += y;
+        }
+        if (lane == 63)
+            wsum[wave] = x;
+        __syncthreads();
+        uint32_t pre = carry, all = 0;
+        for (unsigned w = 0; w < kRowThreads / 64; w++) {
+            const uint32_t ws = wsum[w];
+            pre += w < wave ? ws : 0u;
+            all += ws;
+        }
+        uint32_t run = pre + x - sum;
+#pragma unroll
+        for (int j = 0; j < kRowItems; j++) {
+            const uint32_t i = base + tid * kRowItems + j;
+            if (i < ntiles)
+                row[i] = run;
+            run += v[j];
+        }
+        carry += all;
+        __syncthreads();
+    }
+    if (tid == 0)
+        totals[blockIdx.x] = carry;
+}
+
 __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
     uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t m, int shift,
-    const uint32_t *__restrict__ offs, uint32_t ntiles)
+    const uint32_t *__restrict__ offs, uint32_t ntiles, const uint32_t *__restrict__ totals)
 {
     // Keys and values are staged one after the other in the same 32 KB (4 workgroups per CU
     // instead of 2 with a 48 KB key + value stage).
@@ -103,11 +156,29 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     }
     __syncthreads();
 
+    // Digit bases: exclusive scan of the 256 digit totals (thread = digit).
+    {
+        const uint32_t t = totals[tid];
+        uint32_t x = t;
+#pragma unroll
+        for (unsigned dd = 1; dd < 64; dd <<= 1) {
+            uint32_t y = shfl_up_u32(x, dd);
+            if (lane >= dd)
+                x += y;
+        }
+        if (lane == 63)
+            wsum[wave] = x;
+        __syncthreads();
+        uint32_t pre = 0;
+        for (unsigned w = 0; w < wave; w++)
+            pre += wsum[w];
+        gbase[tid] = pre + x - t + offs[(size_t)tid * ntiles + blockIdx.x];
+        __syncthreads();
+    }
     // Per digit (thread = digit): wave prefixes and tile-local digit starts.
     {
         uint32_t c0 = cnt[0][tid], c1 = cnt[1][tid], c2 = cnt[2][tid], c3 = cnt[3][tid];
         uint32_t tot = c0 + c1 + c2 + c3;
-        gbase[tid] = offs[(size_t)tid * ntiles + blockIdx.x];
         // block exclusive scan of tot over 256 digits
         uint32_t x = tot;
 #pragma unroll
@@ -179,7 +250,7 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
         return 0;
     uint32_t ntiles = (m + kTile - 1) / kTile;
     size_t ncounts = (size_t)ntiles * 256;
-    if (ncounts > ws.radix_counts_elems) {
+    if (ncounts + 256 > ws.radix_counts_elems) {  // + the digit totals
         set_error("radix: count buffer too small");
         return -1;
     }
@@ -189,13 +260,15 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
         hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(kThreads), 0, st, kin, m, shift,
                            ws.radix_counts, ntiles);
         SALZ_LAUNCH_CHECK();
-        if (scan_sum_u32(ws.radix_counts, ws.radix_counts, ncounts, false, nullptr, ws, st) != 0)
-            return -1;
+        uint32_t *totals = ws.radix_counts + ncounts;
+        hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(kRowThreads), 0, st, ws.radix_counts,
+                           ntiles, totals);
+        SALZ_LAUNCH_CHECK();
         bool timed = ws.timing && ws.rx_used + 2 <= ws.rx_pool.size();
         if (timed)
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used], st));
         hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, kout,
-                           vout, m, shift, ws.radix_counts, ntiles);
+                           vout, m, shift, ws.radix_counts, ntiles, totals);
         SALZ_LAUNCH_CHECK();
         if (timed) {
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used + 1], st));
