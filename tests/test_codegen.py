@@ -43,3 +43,36 @@ def test_no_mixed_exec_partial_vmcnt(tmp_path):
     for o in objs:
         hits += scan(_disassemble(o, str(tmp_path)))
     assert hits == [], hits
+
+
+def test_scanner_flags_the_known_hazard(tmp_path):
+    """The scanner's model on hand-written snippets: the k_sa_init shape (a load, then a load
+    under a narrower EXEC mask, then a partial wait) is flagged; loads issued under one mask,
+    or inside a completed if/else, are not."""
+    from vmcnt_scan import scan
+
+    bad = """0000000000000000 <k_bad>:
+	global_load_dwordx2 v[4:5], v0, s[10:11]
+	s_and_saveexec_b64 s[0:1], vcc
+	s_cbranch_execz 13
+	global_load_dwordx2 v[0:1], v[0:1], off offset:8
+	s_waitcnt vmcnt(1)
+	v_lshrrev_b64 v[4:5], v7, v[4:5]
+	s_or_b64 exec, exec, s[0:1]
+"""
+    good = """0000000000000100 <k_good>:
+	global_load_dwordx4 v[2:5], v2, s[2:3]
+	s_and_saveexec_b64 s[0:1], vcc
+	s_xor_b64 s[0:1], exec, s[0:1]
+	v_mov_b32 v9, 0
+	s_or_saveexec_b64 s[0:1], s[0:1]
+	s_xor_b64 exec, exec, s[0:1]
+	v_mov_b32 v9, 1
+	s_or_b64 exec, exec, s[0:1]
+	global_load_dwordx2 v[6:7], v[8:9], off
+	s_waitcnt vmcnt(1)
+"""
+    p = tmp_path / "snip.s"
+    p.write_text(bad + good)
+    hits = scan(str(p))
+    assert [k for k, _ in hits] == ["k_bad"], hits
