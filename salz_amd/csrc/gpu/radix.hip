@@ -27,22 +27,31 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
                                                          uint32_t *__restrict__ counts,
                                                          uint32_t ntiles)
 {
-    __shared__ uint32_t h[4][256];
+    // 16 sub-histograms (4 per wave, by lane & 3), 257 words apart so the copies of one digit
+    // sit in different banks: lanes of a wave adding to a hot digit (text keys' leading bytes
+    // are skewed) spread over 4 addresses instead of serialising on one.
+    constexpr int kCopies = 16, kStride = 257;
+    __shared__ uint32_t h[kCopies * kStride];
     unsigned tid = threadIdx.x, wave = tid >> 6;
-    for (int i = tid; i < 4 * 256; i += kThreads)
-        (&h[0][0])[i] = 0;
+    for (int i = tid; i < kCopies * kStride; i += kThreads)
+        h[i] = 0;
     __syncthreads();
+    uint32_t *mine = h + (wave * 4 + (tid & 3u)) * kStride;
     size_t base = (size_t)blockIdx.x * kTile;
 #pragma unroll
     for (int j = 0; j < kItems; j++) {
         size_t i = base + (size_t)j * kThreads + tid;
         if (i < m) {
             unsigned d = (unsigned)(keys[i] >> shift) & 255u;
-            atomicAdd(&h[wave][d], 1u);
+            atomicAdd(&mine[d], 1u);
         }
     }
     __syncthreads();
-    counts[(size_t)tid * ntiles + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int c = 0; c < kCopies; c++)
+        sum += h[c * kStride + tid];
+    counts[(size_t)tid * ntiles + blockIdx.x] = sum;
 }
 
 // Digit-major tile counts -> per-digit exclusive prefixes over the tiles (in place), one
