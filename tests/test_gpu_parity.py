@@ -265,6 +265,32 @@ def test_lcp_paths(ctx, monkeypatch, lcp_sa, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
+def test_concurrent_contexts_match_oracle(salz):
+    """Four contexts encoding at once on one GPU (threads, own streams): every stream must
+    equal the CPU port's. Concurrent kernels once exposed a load-ordering hazard in the
+    suffix sorter's key kernel ("Concurrent encodes")."""
+    import threading
+
+    cases = [gen("text", 1_048_575, 3), gen("mixed", 700_001, 4), gen("fib", 500_000), gen("smx", 400_000, 2, 4)]
+    refs = [oracle_encode(c)[1] for c in cases]
+    bad = []
+
+    def work(t):
+        ctx = salz.Context(0, 1_048_575)
+        for it in range(6):
+            k = (t + it) % len(cases)
+            if ctx.encode(cases[k]) != refs[k]:
+                bad.append((t, it, k))
+        ctx.close()
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert bad == []
+
+
 def test_cli_roundtrip_matches_reference_container(salz, tmp_path):
     """salz_amd/salz (programs/salzcli.c mirror): -3 compresses to the reference container
     (blocks of 1 << 18, each the oracle's stream), -d restores the file, -k keeps the input."""
