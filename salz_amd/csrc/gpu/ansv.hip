@@ -15,6 +15,13 @@
 // block's tree as a compacted LDS queue (few, full waves instead of divergent ones); queries
 // that leave the block climb the global tree from the block root (k_ansv_global).
 // Output cand[p] = {p - PSV, lenP, p - NSV, lenN}, the reference's aux layout (:555-558).
+//
+// The answers come out in rank order but cand is indexed by text position, so writing them
+// directly is a 16-byte random scatter over the whole 16n-byte array (1.6 GB at 100 MB, beyond
+// the 256 MB Infinity Cache). Instead each workgroup appends its answers to per-text-range
+// staging runs (ranges of 2^rlog positions, one global atomic per range and workgroup), and
+// k_cand_scatter moves the staged answers range by range: its concurrent writes then all fall
+// in one cache-resident window of the candidate array.
 #include "internal.hpp"
 
 #include <cstdio>
@@ -27,7 +34,11 @@ constexpr int kT = 256;
 constexpr uint32_t kB = 2048;  // leaves per workgroup block
 constexpr uint32_t kInf = 0xffffffffu;
 constexpr uint32_t kNear = 16;  // linear neighbour scan before the tree walk
-constexpr uint32_t kWQ = 1536;  // LDS walk-queue entries per block
+constexpr uint32_t kWQ = 1408;  // LDS walk-queue entries per block
+constexpr uint32_t kShards = 16;      // global-queue shards (blockIdx mod kShards)
+constexpr size_t kQCountWord = 800;   // u32 index into Workspace::dscal: 2 * kShards counters
+constexpr uint32_t kMaxRanges = 256;  // staging text ranges per block (rlog is raised to fit)
+static_assert(kMaxRanges <= kT, "one thread per range");
 
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
@@ -46,12 +57,31 @@ __device__ __forceinline__ void put_nsv(uint4 *cand, uint32_t klog, uint32_t p, 
     reinterpret_cast<uint2 *>(cand)[2 * sidx(p, klog) + 1] = v;
 }
 
+// One staged half of cand[p]: {p - pos, len}, or {p + 1, 0} for none (pos == kInf).
+__device__ __forceinline__ uint2 half(uint32_t p, uint32_t pos, uint32_t len)
+{
+    return pos == kInf ? make_uint2(p + 1u, 0u) : make_uint2(p - pos, len);
+}
+
+// First queue slot of shard s: the shards' regions hold as many entries as their blocks
+// have leaves (a leaf misses at most once per side), so they tile [0, n) exactly.
+__device__ __forceinline__ uint32_t shard_base(uint32_t s, uint32_t used_blocks, uint32_t n)
+{
+    const uint32_t last = used_blocks - 1u, short_by = used_blocks * kB - n;
+    uint32_t base = 0;
+    for (uint32_t t = 0; t < s; t++) {
+        const uint32_t nb = (used_blocks + kShards - 1u - t) / kShards;
+        base += nb * kB - (last % kShards == t ? short_by : 0u);
+    }
+    return base;
+}
+
 // One queued query of the block (e = leaf << 1 | nsv) walks the block's LDS min-tree; a
 // query whose answer lies outside the block goes to the global queue (wave-aggregated).
-__device__ __forceinline__ void block_walk(uint32_t e, const uint32_t *vsa, const uint32_t *vlc,
-                                           uint32_t b0, uint32_t klog, uint4 *cand, uint32_t *qp,
-                                           uint32_t *qp_len, uint32_t *qn, uint32_t *qn_len,
-                                           uint32_t *qcount)
+__device__ __forceinline__ void block_walk(uint32_t e, uint32_t slot, const uint32_t *vsa,
+                                           const uint32_t *vlc, uint32_t b0, uint2 *sh, uint32_t *qp, uint32_t *qp_len,
+                                           uint32_t *qn, uint32_t *qn_len, uint32_t *qcount,
+                                           uint32_t qbase)
 {
     const uint32_t l = e >> 1, r = b0 + l;
     const uint32_t v = vsa[kB + l];
@@ -81,7 +111,7 @@ __device__ __forceinline__ void block_walk(uint32_t e, const uint32_t *vsa, cons
             node >>= 1;
         }
         if (hit != kInf)
-            put_psv(cand, klog, v, vsa[kB + hit], lm);
+            sh[2 * slot] = half(v, vsa[kB + hit], lm);
     } else {
         // NSV: nearest smaller to the right; LCP minimum over (r, r'].
         lm = kInf;
@@ -107,9 +137,9 @@ __device__ __forceinline__ void block_walk(uint32_t e, const uint32_t *vsa, cons
             node >>= 1;
         }
         if (hit != kInf)
-            put_nsv(cand, klog, v, vsa[kB + hit], lm);
+            sh[2 * slot + 1] = half(v, vsa[kB + hit], lm);
     }
-    // global queue: one atomic per wave and side
+    // global queue: one atomic per wave and side on this block's shard counter
     const bool miss = hit == kInf;
 #pragma unroll
     for (int side = 0; side < 2; side++) {
@@ -120,7 +150,8 @@ __device__ __forceinline__ void block_walk(uint32_t e, const uint32_t *vsa, cons
         const int leader = (int)__ffsll((unsigned long long)mask) - 1;
         uint32_t base = 0;
         if ((int)lane_id() == leader)
-            base = atomicAdd(&qcount[side], (uint32_t)__popcll(mask));
+            base = qbase + atomicAdd(&qcount[2u * (blockIdx.x % kShards) + side],
+                                     (uint32_t)__popcll(mask));
         base = shfl_u32(base, leader);
         if (mine) {
             const uint32_t q = base + count_below(mask);
@@ -132,14 +163,20 @@ __device__ __forceinline__ void block_walk(uint32_t e, const uint32_t *vsa, cons
 
 __global__ __launch_bounds__(kT) void k_ansv_local(
     const uint32_t *__restrict__ sa, const uint32_t *__restrict__ lcp, uint32_t n, uint32_t np2,
-    uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp, uint4 *__restrict__ cand,
-    uint32_t *__restrict__ qp, uint32_t *__restrict__ qp_len, uint32_t *__restrict__ qn,
-    uint32_t *__restrict__ qn_len, uint32_t *__restrict__ qcount, uint32_t klog,
+    uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp, uint4 *__restrict__ stage,
+    uint32_t *__restrict__ sp, uint32_t *__restrict__ rfill,
+    uint32_t rlog, uint32_t *__restrict__ qp, uint32_t *__restrict__ qp_len,
+    uint32_t *__restrict__ qn, uint32_t *__restrict__ qn_len, uint32_t *__restrict__ qcount,
     unsigned long long *prof)
 {
     __shared__ uint32_t vsa[2 * kB + kNear];  // heap: [1, kB) tree, [kB, 2kB) leaves, + pad
     __shared__ uint32_t vlc[2 * kB + kNear];
+    __shared__ uint16_t loc[kB];             // leaf's index within its text range's run
+    __shared__ uint32_t rbase[kMaxRanges];   // per text range: count, then the run's first slot
+    uint2 *const sh = reinterpret_cast<uint2 *>(stage);  // halves: 2 slot (PSV), 2 slot + 1 (NSV)
     const uint32_t tid = threadIdx.x;
+    if (tid < kMaxRanges)
+        rbase[tid] = 0;
     const uint32_t b0 = blockIdx.x * kB;
     // SALZ_PROF_ANSV (diagnostics): per-phase cycle totals of thread 0
     const unsigned long long t0 = prof ? clock64() : 0ull;
@@ -215,6 +252,13 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
         put(3, umin(vsa[6], vsa[7]), umin(vlc[6], vlc[7]));
         put(1, umin(vsa[2], vsa[3]), umin(vlc[2], vlc[3]));
     }
+    // Staging slots: leaf l's answers go to slot rbase[p >> rlog] + loc[l] (one run per text
+    // range in this workgroup; the run is reserved with one global atomic per range).
+    for (uint32_t l = tid; l < kB && b0 + l < n; l += kT)
+        loc[l] = (uint16_t)atomicAdd(&rbase[vsa[kB + l] >> rlog], 1u);
+    __syncthreads();
+    if (tid < kMaxRanges && rbase[tid])
+        rbase[tid] = (tid << rlog) + atomicAdd(&rfill[tid], rbase[tid]);
     __syncthreads();
 
     unsigned long long t1 = 0;
@@ -228,12 +272,15 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     // in place. Kept small so 4 workgroups fit a CU's LDS.
     __shared__ uint16_t wq[kWQ];
     __shared__ uint32_t wq_n;
+    const uint32_t qbase = shard_base(blockIdx.x % kShards, gridDim.x, n);
+    auto slot_of = [&](uint32_t l) { return rbase[vsa[kB + l] >> rlog] + loc[l]; };
     auto enqueue = [&](uint32_t e) {
         const uint32_t slot = atomicAdd(&wq_n, 1u);
         if (slot < kWQ)
             wq[slot] = (uint16_t)e;
         else
-            block_walk(e, vsa, vlc, b0, klog, cand, qp, qp_len, qn, qn_len, qcount);
+            block_walk(e, slot_of(e >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len, qcount,
+                       qbase);
     };
     if (tid == 0)
         wq_n = 0;
@@ -281,15 +328,17 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
                 }
             }
         }
+        const uint32_t slot = slot_of(l);
+        sp[slot] = v;
         if (hitP != kInf && hitN != kInf) {
-            cand[sidx(v, klog)] = make_uint4(v - pvP, lmP, v - pvN, lmN);
+            stage[slot] = make_uint4(v - pvP, lmP, v - pvN, lmN);
         } else {
             if (hitP != kInf)
-                put_psv(cand, klog, v, pvP, lmP);
+                sh[2 * slot] = make_uint2(v - pvP, lmP);
             else
                 enqueue(l << 1);
             if (hitN != kInf)
-                put_nsv(cand, klog, v, pvN, lmN);
+                sh[2 * slot + 1] = make_uint2(v - pvN, lmN);
             else
                 enqueue(l << 1 | 1u);
         }
@@ -303,7 +352,8 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     // the global queues (k_ansv_global continues from the block root).
     const uint32_t nw = wq_n < kWQ ? wq_n : kWQ;
     for (uint32_t w = tid; w < nw; w += kT)
-        block_walk(wq[w], vsa, vlc, b0, klog, cand, qp, qp_len, qn, qn_len, qcount);
+        block_walk(wq[w], slot_of(wq[w] >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len,
+                   qcount, qbase);
     if (prof) {
         __syncthreads();
         if (tid == 0) {
@@ -314,6 +364,34 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
             atomicAdd(&prof[3], (unsigned long long)nw);
         }
     }
+}
+
+// Staged answers -> cand in the interleaved text-order layout. Slots are grouped by text
+// range, so the workgroups in flight write into one cache-resident window of cand. Halves
+// that went to the global queues are garbage here; k_ansv_global overwrites them afterwards.
+__global__ __launch_bounds__(kT) void k_cand_scatter(const uint32_t *__restrict__ sp,
+                                                     const uint4 *__restrict__ stage, uint32_t n,
+                                                     uint4 *__restrict__ cand, uint32_t klog,
+                                                     uint32_t rlog, uint32_t nranges,
+                                                     uint32_t *__restrict__ err)
+{
+    // XCD-aware: workgroups are dealt round-robin over the 8 XCDs, so workgroup g runs on
+    // XCD g mod 8; XCD x takes text ranges x, x + 8, ... in turn, and the lines of one cand
+    // window are only ever written through one XCD's L2.
+    const uint32_t g = blockIdx.x, tiles = 1u << (rlog - 8);
+    const uint32_t k = g >> 3, r = (g & 7u) + 8u * (k >> (rlog - 8));
+    if (r >= nranges)
+        return;
+    // One slot per thread: all three loads are issued under one EXEC mask (DESIGN.md,
+    // "Concurrent encodes and the unaligned text load").
+    const size_t i = ((size_t)r << rlog) + (size_t)(k & (tiles - 1u)) * kT + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t p = sp[i];
+    const uint4 c = stage[i];
+    if (bad_index(p >= n, err, kErrAnsv))
+        return;
+    cand[sidx(p, klog)] = c;
 }
 
 __global__ void k_tree_level(uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp,
@@ -346,16 +424,19 @@ struct Tree {
     }
 };
 
-// Queries that left their block: continue the climb from the block root.
+// Queries that left their block: continue the climb from the block root. blockIdx.y is the
+// queue shard.
 __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
-                              const uint32_t *__restrict__ qlen, uint32_t nq, int nsv,
+                              const uint32_t *__restrict__ qlen,
+                              const uint32_t *__restrict__ qcount, uint32_t used_blocks, int nsv,
                               uint4 *__restrict__ cand, uint32_t klog)
 {
-    uint32_t x = blockIdx.x * kT + threadIdx.x;
-    if (x >= nq)
+    const uint32_t x = blockIdx.x * kT + threadIdx.x;
+    if (x >= qcount[2u * blockIdx.y + (uint32_t)nsv])
         return;
-    const uint32_t r = q[x];
-    uint32_t lm = qlen[x];
+    const uint32_t e = shard_base(blockIdx.y, used_blocks, t.n) + x;
+    const uint32_t r = q[e];
+    uint32_t lm = qlen[e];
     const uint32_t v = t.sa[r];
     uint32_t node = t.np2 / kB + r / kB, hit = kInf;
     while (node > 1) {
@@ -405,9 +486,9 @@ int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp)
     uint32_t *tsa = reinterpret_cast<uint32_t *>(ws.keyA);
     uint32_t *tlcp = reinterpret_cast<uint32_t *>(ws.keyB);
     uint32_t *qp = ws.valA, *qpl = ws.valB, *qn = ws.offA, *qnl = ws.offB;
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(ws.dscal) + 40;
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(ws.dscal) + kQCountWord;
 
-    SALZ_HIP(hipMemsetAsync(cnt, 0, 8, st));
+    SALZ_HIP(hipMemsetAsync(cnt, 0, 2 * kShards * sizeof(uint32_t), st));
     uint32_t nblocks = np2 / kB;
     uint32_t used_blocks = (n + kB - 1) / kB;
     // Blocks past the text only hold +inf leaves: fill their subtree roots directly.
@@ -423,36 +504,71 @@ int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp)
     unsigned long long *prof = prof_on ? reinterpret_cast<unsigned long long *>(ws.dscal) + 200 : nullptr;
     if (prof)
         SALZ_HIP(hipMemsetAsync(prof, 0, 32, st));
+    // Staging: text ranges of 2^rlog positions (cand windows of 16 << rlog bytes; 64 MB by
+    // default), at most kMaxRanges of them. Slots sp / stage alias scratch that is free here.
+    static const uint32_t rlog_env = [] {
+        const char *e = getenv("SALZ_ANSV_RLOG");
+        const int v = e ? atoi(e) : 20;
+        return (uint32_t)(v < 12 ? 12 : v > 30 ? 30 : v);
+    }();
+    uint32_t rlog = rlog_env;
+    while ((((uint64_t)n - 1) >> rlog) + 1 > kMaxRanges)
+        rlog++;
+    uint32_t *rfill = ws.radix_counts;
+    uint32_t *sp = ws.u0;
+    uint4 *stage = reinterpret_cast<uint4 *>(ws.lsc);
+    uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
+    if (ws.radix_counts_elems < kMaxRanges) {
+        set_error("ansv: range counters do not fit");
+        return -1;
+    }
+    SALZ_HIP(hipMemsetAsync(rfill, 0, kMaxRanges * sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_ansv_local, dim3(used_blocks), dim3(kT), 0, st, ws.sa, lcp, n, np2, tsa,
-                       tlcp, ws.cand, qp, qpl, qn, qnl, cnt, ws.klog, prof);
+                       tlcp, stage, sp, rfill, rlog, qp, qpl, qn, qnl, cnt, prof);
+    SALZ_LAUNCH_CHECK();
+    const uint32_t nranges = (uint32_t)((((uint64_t)n - 1) >> rlog) + 1);
+    const uint32_t sgrid = 8u * ((nranges + 7u) / 8u) << (rlog - 8);
+    hipLaunchKernelGGL(k_cand_scatter, dim3(sgrid), dim3(kT), 0, st, sp, stage, n, ws.cand,
+                       ws.klog, rlog, nranges, derr);
     SALZ_LAUNCH_CHECK();
     if (prof) {
-        if (read_scalars(ws, 0, 1632, "ansv.prof") != 0)
+        if (read_scalars(ws, 0, (kQCountWord + 2 * kShards) * sizeof(uint32_t), "ansv.prof") != 0)
             return -1;
         const uint64_t *h = ws.hscal + 200;
+        uint32_t gq[2] = {0, 0};
+        for (uint32_t s = 0; s < 2 * kShards; s++)
+            gq[s & 1] += reinterpret_cast<uint32_t *>(ws.hscal)[kQCountWord + s];
         fprintf(stderr, "ansv_local: %u blocks, cycles/block build %.0f near %.0f tree %.0f; "
                 "queued %.3f per leaf; global %u + %u\n", used_blocks, (double)h[0] / used_blocks,
-                (double)h[1] / used_blocks, (double)h[2] / used_blocks, (double)h[3] / n,
-                reinterpret_cast<uint32_t *>(ws.hscal)[40], reinterpret_cast<uint32_t *>(ws.hscal)[41]);
+                (double)h[1] / used_blocks, (double)h[2] / used_blocks, (double)h[3] / n, gq[0],
+                gq[1]);
     }
     for (uint32_t lo = nblocks / 2; lo >= 1; lo >>= 1) {
         hipLaunchKernelGGL(k_tree_level, dim3(grid_for(lo, kT)), dim3(kT), 0, st, tsa, tlcp, lo,
                            lo);
         SALZ_LAUNCH_CHECK();
     }
-    if (read_scalars(ws, 0, 256, "ansv.q") != 0)
+    if (read_scalars(ws, 0, (kQCountWord + 2 * kShards) * sizeof(uint32_t), "ansv.q") != 0)
         return -1;
-    uint32_t nqp = reinterpret_cast<uint32_t *>(ws.hscal)[40];
-    uint32_t nqn = reinterpret_cast<uint32_t *>(ws.hscal)[41];
+    if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
+        set_error("ansv: device index check failed (code 0x%x): suffix array corrupt", e);
+        return -1;
+    }
+    uint32_t nqp = 0, nqn = 0;  // largest shard per side
+    for (uint32_t s = 0; s < kShards; s++) {
+        const uint32_t *h = reinterpret_cast<uint32_t *>(ws.hscal) + kQCountWord + 2 * s;
+        nqp = h[0] > nqp ? h[0] : nqp;
+        nqn = h[1] > nqn ? h[1] : nqn;
+    }
     Tree t{tsa, tlcp, ws.sa, lcp, n, np2};
     if (nqp) {
-        hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqp, kT)), dim3(kT), 0, st, t, qp, qpl,
-                           nqp, 0, ws.cand, ws.klog);
+        hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqp, kT), kShards), dim3(kT), 0, st, t,
+                           qp, qpl, cnt, used_blocks, 0, ws.cand, ws.klog);
         SALZ_LAUNCH_CHECK();
     }
     if (nqn) {
-        hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqn, kT)), dim3(kT), 0, st, t, qn, qnl,
-                           nqn, 1, ws.cand, ws.klog);
+        hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqn, kT), kShards), dim3(kT), 0, st, t,
+                           qn, qnl, cnt, used_blocks, 1, ws.cand, ws.klog);
         SALZ_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(k_cand_origin, dim3(1), dim3(1), 0, st, ws.cand);

@@ -60,7 +60,7 @@ struct Workspace {
     uint32_t *offA = nullptr, *offB = nullptr;                           // n+2 each
     uint4 *cand = nullptr;                                               // cap_s, interleaved
     uint64_t *pst = nullptr;                                             // cap_s, interleaved
-    uint64_t *lsc = nullptr;   // n1: suffix sorter's large-group scan
+    uint64_t *lsc = nullptr;   // 2 n1: suffix sorter's large-group scan; ANSV staging (uint4)
     uint64_t *lrec = nullptr;  // per large group: (start in extracted array << 32) | start
     uint32_t *lg2g = nullptr;  // per large group: its group id
     uint8_t *out = nullptr;                                              // encoded_len_max

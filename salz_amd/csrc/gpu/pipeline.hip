@@ -130,7 +130,7 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
         dalloc(&ws.valB, n1) || dalloc(&ws.u0, n1) || dalloc(&ws.u1, n1) || dalloc(&ws.u2, n1) ||
         dalloc(&ws.u3, n1) || dalloc(&ws.lcps, n1) || dalloc(&ws.g64, n1) || dalloc(&ws.offA, n1) ||
         dalloc(&ws.offB, n1) || dalloc(&ws.cand, ws.cap_s) || dalloc(&ws.pst, ws.cap_s) ||
-        dalloc(&ws.lsc, n1) || dalloc(&ws.lrec, n1 / 1024 + 2) || dalloc(&ws.lg2g, n1 / 1024 + 2) || dalloc(&ws.out, ws.out_cap) ||
+        dalloc(&ws.lsc, 2 * n1) || dalloc(&ws.lrec, n1 / 1024 + 2) || dalloc(&ws.lg2g, n1 / 1024 + 2) || dalloc(&ws.out, ws.out_cap) ||
         dalloc(&ws.radix_counts, ws.radix_counts_elems) ||
         dalloc(reinterpret_cast<uint8_t **>(&ws.scan_tmp), ws.scan_tmp_bytes) ||
         dalloc(&ws.dscal, 1024)) {
@@ -146,7 +146,7 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
         void *ptrs[] = {ws.rank, ws.sa, ws.keyA, ws.keyB, ws.valA, ws.valB, ws.u0, ws.u1, ws.u2,
                         ws.u3, ws.g64, ws.offA, ws.offB, ws.cand, ws.pst, ws.lsc};
         size_t sizes[] = {4 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1, 4 * n1, 4 * n1, 4 * n1,
-                          4 * n1, 8 * n1, 4 * n1, 4 * n1, 16 * ws.cap_s, 8 * ws.cap_s, 8 * n1};
+                          4 * n1, 8 * n1, 4 * n1, 4 * n1, 16 * ws.cap_s, 8 * ws.cap_s, 16 * n1};
         for (size_t k = 0; k < sizeof(ptrs) / sizeof(ptrs[0]); k++)
             SALZ_HIP(hipMemset(ptrs[k], v, sizes[k]));
         SALZ_HIP(hipMemset(ws.lrec, v, 8 * (n1 / 1024 + 2)));
