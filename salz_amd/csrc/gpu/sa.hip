@@ -19,10 +19,10 @@
 //               write); large groups are extracted, radix-sorted on (large-group id, rank)
 //               and put back (k_extract / k_putback). Ties may land in any order: equal keys
 //               stay one group, so the next round re-sorts them.
-//   k_heads_lcp group-head flags of the sorted active list, and the LCP of every new head
-//               with its predecessor (see the comment there; k_heads once the LCP is left to
-//               the Phi/PLCP stage)
-//   scan        -> group ids; k_headpos -> head index per group
+//   k_heads_lcp group-head flags of the sorted active list (one 64-bit ballot per wave), and
+//               the LCP of every new head with its predecessor (see the comment there; k_heads
+//               once the LCP is left to the Phi/PLCP stage)
+//   scan        of the per-wave head counts; k_headpos -> group ids and head index per group
 //   k_grpkeep   groups of size >= 2 survive; u64 scans pack (new gid, compact start) and
 //               (large-group id, start in the extracted array)
 //   k_commit    rank update for every active suffix (in large rounds the upper text half
@@ -60,28 +60,56 @@ __global__ void k_sa_init(const uint8_t *__restrict__ T, uint32_t n, uint64_t *_
     val[c] = i;
 }
 
-__global__ void k_heads(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
-                        uint32_t m, uint32_t n, int round0, uint32_t *__restrict__ hf)
+// Group-head flags travel as one 64-bit ballot per wave of the sorted list (hmask) plus its
+// popcount (wcnt): the group ids are then a scan over m / 64 wave counts, not over m flags.
+struct HeadBits {
+    uint64_t *hmask;  // ceil(m / 64) words
+    uint32_t *wcnt;   // ceil(m / 64) per-wave head counts
+    uint32_t *wpre;   // their exclusive scan
+};
+
+__device__ __forceinline__ void put_heads(HeadBits hb, size_t c, uint32_t m, bool head)
 {
-    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (c >= m)
-        return;
-    bool h = c == 0 || key[c] != key[c - 1];
-    if (round0 && !h)
-        h = (n - val[c]) < 8u || (n - val[c - 1]) < 8u;
-    hf[c] = h ? 1u : 0u;
+    const uint64_t mask = wave_ballot(head);
+    if ((c & 63u) == 0 && c < m) {  // waves wholly past the list's end own no word
+        hb.hmask[c >> 6] = mask;
+        hb.wcnt[c >> 6] = (uint32_t)__popcll(mask);
+    }
 }
 
-__global__ void k_headpos(const uint32_t *__restrict__ hf, const uint32_t *__restrict__ gall,
-                          uint32_t m, uint32_t *__restrict__ headpos)
+__global__ void k_heads(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
+                        uint32_t m, uint32_t n, int round0, HeadBits hb)
 {
-    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if ((c & ~(size_t)63) >= m)
+        return;  // whole wave past the end
+    // every load unconditional (clamped indices): no exec-masked load next to another
+    const bool in = c < m;
+    const size_t cc = in ? c : 0, cp = cc ? cc - 1 : 0;
+    const uint64_t k0 = key[cp], k1 = key[cc];
+    const uint32_t v0 = val[cp], v1 = val[cc];
+    bool h = cc == 0 || k0 != k1;
+    if (round0 && !h)
+        h = (n - v1) < 8u || (n - v0) < 8u;
+    put_heads(hb, c, m, in && h);
+}
+
+// Group ids (inclusive head count) and head positions from the per-wave head ballots.
+__global__ void k_headpos(HeadBits hb, uint32_t m, uint32_t *__restrict__ gall,
+                          uint32_t *__restrict__ headpos)
+{
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
         return;
-    if (hf[c])
-        headpos[gall[c] - 1u] = (uint32_t)c;
+    const uint64_t mask = hb.hmask[c >> 6];
+    const uint32_t lane = (uint32_t)(c & 63u);
+    const uint32_t bit = (uint32_t)(mask >> lane) & 1u;
+    const uint32_t g = hb.wpre[c >> 6] + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull)) + bit;
+    gall[c] = g;
+    if (bit)
+        headpos[g - 1u] = (uint32_t)c;
     if (c == m - 1)
-        headpos[gall[c]] = m;
+        headpos[g] = m;
 }
 
 __global__ void k_grpkeep(const uint32_t *__restrict__ headpos, uint32_t G,
@@ -168,9 +196,9 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
 constexpr uint32_t kLcpLane = 256;
 constexpr uint32_t kLcpMaxHk = 4096;
 
-// k_heads with the LCP of every new head (writes hf like k_heads).
+// k_heads with the LCP of every new head (writes the head ballots like k_heads).
 __global__ __launch_bounds__(kT) void k_heads_lcp(
-    const uint64_t *__restrict__ K, const uint32_t *__restrict__ V, uint32_t *__restrict__ hf,
+    const uint64_t *__restrict__ K, const uint32_t *__restrict__ V, HeadBits hb,
     const uint32_t *__restrict__ off_old, uint32_t m, uint32_t n, int kb_old, uint32_t hk, int round0,
     const uint8_t *__restrict__ T, uint32_t *__restrict__ lcps, uint32_t *err)
 {
@@ -183,8 +211,7 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
     bool head = c == 0 || k0 != k1;
     if (round0 && !head)
         head = (n - v1) < 8u || (n - v0) < 8u;
-    if (in)
-        hf[c] = head ? 1u : 0u;
+    put_heads(hb, c, m, in && head);
     const uint32_t g1 = round0 ? 0u : (uint32_t)(k1 >> kb_old);
     const uint32_t o = round0 ? 0u : off_old[g1];
     const uint32_t i = v1, j = v0, mx = i > j ? i : j;
@@ -481,7 +508,7 @@ __global__ void k_dbg_pairs(const uint64_t *__restrict__ K, const uint32_t *__re
     }
 }
 
-__global__ void k_dbg_heads(const uint32_t *__restrict__ hf, const uint32_t *__restrict__ gall,
+__global__ void k_dbg_heads(HeadBits hb, const uint32_t *__restrict__ gall,
                             const uint32_t *__restrict__ headpos, uint32_t m, uint32_t *err)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
@@ -491,7 +518,8 @@ __global__ void k_dbg_heads(const uint32_t *__restrict__ hf, const uint32_t *__r
     const uint32_t g = gall[c];
     const uint32_t pv = gall[c ? c - 1 : 0];
     const uint32_t prev = c ? pv : 0u;
-    if (g - prev != hf[c] || g == 0)
+    const uint32_t hfc = (uint32_t)(hb.hmask[c >> 6] >> (c & 63u)) & 1u;
+    if (g - prev != hfc || g == 0)
         atomicOr(err, 0x2000u);
     else if (headpos[g - 1] > c || headpos[g] <= c)
         atomicOr(err, 0x4000u);
@@ -579,7 +607,9 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     uint64_t *K = ws.keyA;
     uint32_t *V = ws.valA;
     uint32_t *offo = ws.offA, *offn = ws.offB;
-    uint32_t *hf = ws.u0, *gall = ws.u1, *headpos = ws.u2, *ngid = ws.u3;
+    uint32_t *gall = ws.u1, *headpos = ws.u2, *ngid = ws.u3;
+    const size_t nw_max = ((size_t)n + 63) / 64;  // head ballots of up to n list entries, in u0
+    HeadBits hb{reinterpret_cast<uint64_t *>(ws.u0), ws.u0 + 2 * nw_max, ws.u0 + 3 * nw_max};
     uint64_t *gsc = ws.g64;
     uint32_t *d32 = reinterpret_cast<uint32_t *>(ws.dscal);
     uint64_t *d64 = ws.dscal + 8;
@@ -687,22 +717,22 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         if (ws.lcps_ok && !round0 && h / 2 > kLcpMaxHk)
             ws.lcps_ok = false;  // long repeats: the PLCP stage is cheaper than these compares
         if (ws.lcps_ok)
-            hipLaunchKernelGGL(k_heads_lcp, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hf, offo, m, n,
+            hipLaunchKernelGGL(k_heads_lcp, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, offo, m, n,
                                kb_old, round0 ? 0u : h / 2, round0, ws.text, ws.lcps, derr);
         else
             hipLaunchKernelGGL(k_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m, n, round0,
-                               hf);
+                               hb);
         SALZ_LAUNCH_CHECK();
-        if (scan_sum_u32(hf, gall, m, true, d32 + 0, ws, st) != 0)
+        if (scan_sum_u32(hb.wcnt, hb.wpre, ((size_t)m + 63) / 64, false, d32 + 0, ws, st) != 0)
             return -1;
-        hipLaunchKernelGGL(k_headpos, dim3(grid_for(m, kT)), dim3(kT), 0, st, hf, gall, m,
+        hipLaunchKernelGGL(k_headpos, dim3(grid_for(m, kT)), dim3(kT), 0, st, hb, m, gall,
                            headpos);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 64, "sa.G") != 0)
             return -1;
         uint32_t G = reinterpret_cast<uint32_t *>(ws.hscal)[0];
         if (dbg_rounds) {
-            hipLaunchKernelGGL(k_dbg_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, hf, gall, headpos, m, derr);
+            hipLaunchKernelGGL(k_dbg_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, hb, gall, headpos, m, derr);
             SALZ_LAUNCH_CHECK();
         }
 
