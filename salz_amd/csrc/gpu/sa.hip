@@ -23,8 +23,8 @@
 //               the LCP of every new head with its predecessor (see the comment there; k_heads
 //               once the LCP is left to the Phi/PLCP stage)
 //   scan        of the per-wave head counts; k_headpos -> group ids and head index per group
-//   k_grpkeep   groups of size >= 2 survive; u64 scans pack (new gid, compact start) and
-//               (large-group id, start in the extracted array)
+//   k_grpsum /  groups of size >= 2 survive; exclusive scans (per-wave sums, then per group)
+//   k_grpscan   pack (compact start, new gid) and (start in the extracted array, large-group id)
 //   k_commit    rank update for every active suffix (in large rounds the upper text half
 //               through k_rank_upper), SA write for singletons, compaction
 //   k_keys      next round's keys: gid << kb | rank[i + h]
@@ -112,15 +112,72 @@ __global__ void k_headpos(HeadBits hb, uint32_t m, uint32_t *__restrict__ gall,
         headpos[g] = m;
 }
 
-__global__ void k_grpkeep(const uint32_t *__restrict__ headpos, uint32_t G,
-                          uint64_t *__restrict__ gsc, uint64_t *__restrict__ lsc)
+// Per group: (size << 32 | 1) for survivors (size >= 2) in gsc and for large groups
+// (size > kSmall) in lsc; k_commit reads their exclusive scans. Both halves sum below 2^32
+// (sizes sum to at most m, counts to at most G), so a wave sums them as two u32 lanes.
+// k_grpsum leaves one (gsc, lsc) sum per wave of groups; after a scan of those, k_grpscan
+// writes the per-group exclusive prefixes.
+__device__ __forceinline__ void grp_vals(const uint32_t *__restrict__ headpos, size_t g, uint32_t G,
+                                         uint32_t &gs, uint32_t &gc, uint32_t &ls, uint32_t &lc)
 {
-    size_t g = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (g >= G)
+    const size_t gg = g < G ? g : 0;  // unconditional loads (clamped)
+    const uint32_t size = headpos[gg + 1] - headpos[gg];
+    const bool in = g < G;
+    gc = in && size >= 2 ? 1u : 0u;
+    gs = gc ? size : 0u;
+    lc = in && size > kSmall ? 1u : 0u;
+    ls = lc ? size : 0u;
+}
+
+__global__ __launch_bounds__(kT) void k_grpsum(const uint32_t *__restrict__ headpos, uint32_t G,
+                                               uint64_t *__restrict__ wg, uint64_t *__restrict__ wl)
+{
+    const size_t g = (size_t)blockIdx.x * kT + threadIdx.x;
+    if ((g & ~(size_t)63) >= G)
+        return;  // whole wave past the end
+    uint32_t gs, gc, ls, lc;
+    grp_vals(headpos, g, G, gs, gc, ls, lc);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        gs += shfl_xor_u32(gs, d);
+        gc += shfl_xor_u32(gc, d);
+        ls += shfl_xor_u32(ls, d);
+        lc += shfl_xor_u32(lc, d);
+    }
+    if ((g & 63u) == 0) {
+        wg[g >> 6] = (uint64_t)gs << 32 | gc;
+        wl[g >> 6] = (uint64_t)ls << 32 | lc;
+    }
+}
+
+__global__ __launch_bounds__(kT) void k_grpscan(const uint32_t *__restrict__ headpos, uint32_t G,
+                                                const uint64_t *__restrict__ wg,
+                                                const uint64_t *__restrict__ wl,
+                                                uint64_t *__restrict__ gsc, uint64_t *__restrict__ lsc)
+{
+    const size_t g = (size_t)blockIdx.x * kT + threadIdx.x;
+    if ((g & ~(size_t)63) >= G)
         return;
-    uint32_t size = headpos[g + 1] - headpos[g];
-    gsc[g] = size >= 2 ? (((uint64_t)size << 32) | 1ull) : 0ull;
-    lsc[g] = size > kSmall ? (((uint64_t)size << 32) | 1ull) : 0ull;
+    uint32_t gs, gc, ls, lc;
+    grp_vals(headpos, g, G, gs, gc, ls, lc);
+    const uint32_t lane = (uint32_t)(g & 63u);
+    uint32_t xs = gs, xc = gc, ys = ls, yc = lc;  // inclusive wave scans
+#pragma unroll
+    for (unsigned d = 1; d < 64; d <<= 1) {
+        const uint32_t a = shfl_up_u32(xs, d), b = shfl_up_u32(xc, d);
+        const uint32_t e = shfl_up_u32(ys, d), f = shfl_up_u32(yc, d);
+        if (lane >= d) {
+            xs += a;
+            xc += b;
+            ys += e;
+            yc += f;
+        }
+    }
+    const uint64_t pg = wg[g >> 6], pl = wl[g >> 6];
+    if (g < G) {
+        gsc[g] = pg + ((uint64_t)(xs - gs) << 32 | (xc - gc));
+        lsc[g] = pl + ((uint64_t)(ys - ls) << 32 | (yc - lc));
+    }
 }
 
 // Next round's group table (ginfo: size << 32 | compact start, gl: large-group id) is
@@ -736,13 +793,19 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
             SALZ_LAUNCH_CHECK();
         }
 
-        hipLaunchKernelGGL(k_grpkeep, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, G, gsc,
-                           ws.lsc);
-        SALZ_LAUNCH_CHECK();
-        if (scan_sum_u64(gsc, gsc, G, false, d64, ws, st) != 0)
-            return -1;
-        if (scan_sum_u64(ws.lsc, ws.lsc, G, false, d64 + 1, ws, st) != 0)
-            return -1;
+        {
+            uint64_t *wg = reinterpret_cast<uint64_t *>(ws.u0), *wl = wg + nw_max;  // hb is spent
+            const size_t nwg = ((size_t)G + 63) / 64;
+            hipLaunchKernelGGL(k_grpsum, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, G, wg, wl);
+            SALZ_LAUNCH_CHECK();
+            if (scan_sum_u64(wg, wg, nwg, false, d64, ws, st) != 0)
+                return -1;
+            if (scan_sum_u64(wl, wl, nwg, false, d64 + 1, ws, st) != 0)
+                return -1;
+            hipLaunchKernelGGL(k_grpscan, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, G, wg, wl,
+                               gsc, ws.lsc);
+            SALZ_LAUNCH_CHECK();
+        }
         if (dbg_rounds) {
             if (read_scalars(ws, 0, 256, "sa.dbg") != 0)
                 return -1;
