@@ -27,23 +27,37 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
                                                          uint32_t *__restrict__ counts,
                                                          uint32_t ntiles)
 {
-    // 16 sub-histograms (4 per wave, by lane & 3), 257 words apart so the copies of one digit
+    // 32 sub-histograms (8 per wave, by lane & 7), 257 words apart so the copies of one digit
     // sit in different banks: lanes of a wave adding to a hot digit (text keys' leading bytes
-    // are skewed) spread over 4 addresses instead of serialising on one.
-    constexpr int kCopies = 16, kStride = 257;
+    // are skewed) spread over 8 addresses instead of serialising on one.
+    constexpr int kCopies = 32, kStride = 257;
     __shared__ uint32_t h[kCopies * kStride];
     unsigned tid = threadIdx.x, wave = tid >> 6;
     for (int i = tid; i < kCopies * kStride; i += kThreads)
         h[i] = 0;
     __syncthreads();
-    uint32_t *mine = h + (wave * 4 + (tid & 3u)) * kStride;
-    size_t base = (size_t)blockIdx.x * kTile;
+    uint32_t *mine = h + (wave * 8 + (tid & 7u)) * kStride;
+    // Two keys per 16-byte load: pair j of thread t is keys 2 (j * kThreads + t) and + 1.
+    const size_t base = (size_t)blockIdx.x * kTile;
+    const uint4 *kp = reinterpret_cast<const uint4 *>(keys + base);
+    const size_t left = m > base ? m - base : 0;
+    if (left >= (size_t)kTile) {
+        uint4 x[kItems / 2];
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
-        size_t i = base + (size_t)j * kThreads + tid;
-        if (i < m) {
-            unsigned d = (unsigned)(keys[i] >> shift) & 255u;
-            atomicAdd(&mine[d], 1u);
+        for (int j = 0; j < kItems / 2; j++)
+            x[j] = kp[j * kThreads + tid];
+#pragma unroll
+        for (int j = 0; j < kItems / 2; j++) {
+            const uint64_t k0 = (uint64_t)x[j].y << 32 | x[j].x, k1 = (uint64_t)x[j].w << 32 | x[j].z;
+            atomicAdd(&mine[(unsigned)(k0 >> shift) & 255u], 1u);
+            atomicAdd(&mine[(unsigned)(k1 >> shift) & 255u], 1u);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            const size_t i = (size_t)j * kThreads + tid;
+            if (i < left)
+                atomicAdd(&mine[(unsigned)(keys[base + i] >> shift) & 255u], 1u);
         }
     }
     __syncthreads();
