@@ -94,18 +94,24 @@ __global__ void k_heads(const uint64_t *__restrict__ key, const uint32_t *__rest
     put_heads(hb, c, m, in && h);
 }
 
-// Group ids (inclusive head count) and head positions from the per-wave head ballots.
-__global__ void k_headpos(HeadBits hb, uint32_t m, uint32_t *__restrict__ gall,
-                          uint32_t *__restrict__ headpos)
+// Group id + 1 of list entry c (the inclusive head count), from the per-wave head ballots
+// (one word per 64 entries: every lane of a wave reads the same two).
+__device__ __forceinline__ uint32_t gid1(const HeadBits &hb, size_t c, uint32_t &bit)
+{
+    const uint64_t mask = hb.hmask[c >> 6];
+    const uint32_t lane = (uint32_t)(c & 63u);
+    bit = (uint32_t)(mask >> lane) & 1u;
+    return hb.wpre[c >> 6] + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull)) + bit;
+}
+
+// Head position per group (plus the sentinel headpos[G] = m).
+__global__ void k_headpos(HeadBits hb, uint32_t m, uint32_t *__restrict__ headpos)
 {
     const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
         return;
-    const uint64_t mask = hb.hmask[c >> 6];
-    const uint32_t lane = (uint32_t)(c & 63u);
-    const uint32_t bit = (uint32_t)(mask >> lane) & 1u;
-    const uint32_t g = hb.wpre[c >> 6] + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull)) + bit;
-    gall[c] = g;
+    uint32_t bit;
+    const uint32_t g = gid1(hb, c, bit);
     if (bit)
         headpos[g - 1u] = (uint32_t)c;
     if (c == m - 1)
@@ -190,7 +196,7 @@ struct GroupTab {
 };
 
 __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
-                         const uint32_t *__restrict__ gall, const uint32_t *__restrict__ headpos,
+                         HeadBits hb, const uint32_t *__restrict__ headpos,
                          const uint64_t *__restrict__ gsc, const uint64_t *__restrict__ lsc,
                          const uint32_t *__restrict__ off_old, uint32_t *__restrict__ off_new,
                          uint32_t *__restrict__ nval, uint32_t *__restrict__ ngid,
@@ -201,7 +207,8 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
         return;
-    uint32_t g = gall[c] - 1u;
+    uint32_t bit;
+    const uint32_t g = gid1(hb, c, bit) - 1u;
     uint32_t hp = headpos[g];
     uint32_t size = headpos[g + 1] - hp;
     uint32_t o = round0 ? 0u : off_old[(uint32_t)(key[c] >> kb_old)];
@@ -565,15 +572,16 @@ __global__ void k_dbg_pairs(const uint64_t *__restrict__ K, const uint32_t *__re
     }
 }
 
-__global__ void k_dbg_heads(HeadBits hb, const uint32_t *__restrict__ gall,
-                            const uint32_t *__restrict__ headpos, uint32_t m, uint32_t *err)
+__global__ void k_dbg_heads(HeadBits hb, const uint32_t *__restrict__ headpos, uint32_t m,
+                            uint32_t *err)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
         return;
     // unconditional loads (see load_u64_any): no exec-masked load next to another one
-    const uint32_t g = gall[c];
-    const uint32_t pv = gall[c ? c - 1 : 0];
+    uint32_t bit, pbit;
+    const uint32_t g = gid1(hb, c, bit);
+    const uint32_t pv = gid1(hb, c ? c - 1 : 0, pbit);
     const uint32_t prev = c ? pv : 0u;
     const uint32_t hfc = (uint32_t)(hb.hmask[c >> 6] >> (c & 63u)) & 1u;
     if (g - prev != hfc || g == 0)
@@ -664,7 +672,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     uint64_t *K = ws.keyA;
     uint32_t *V = ws.valA;
     uint32_t *offo = ws.offA, *offn = ws.offB;
-    uint32_t *gall = ws.u1, *headpos = ws.u2, *ngid = ws.u3;
+    uint32_t *headpos = ws.u2, *ngid = ws.u3;
     const size_t nw_max = ((size_t)n + 63) / 64;  // head ballots of up to n list entries, in u0
     HeadBits hb{reinterpret_cast<uint64_t *>(ws.u0), ws.u0 + 2 * nw_max, ws.u0 + 3 * nw_max};
     uint64_t *gsc = ws.g64;
@@ -782,19 +790,19 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u32(hb.wcnt, hb.wpre, ((size_t)m + 63) / 64, false, d32 + 0, ws, st) != 0)
             return -1;
-        hipLaunchKernelGGL(k_headpos, dim3(grid_for(m, kT)), dim3(kT), 0, st, hb, m, gall,
-                           headpos);
+        hipLaunchKernelGGL(k_headpos, dim3(grid_for(m, kT)), dim3(kT), 0, st, hb, m, headpos);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 64, "sa.G") != 0)
             return -1;
         uint32_t G = reinterpret_cast<uint32_t *>(ws.hscal)[0];
         if (dbg_rounds) {
-            hipLaunchKernelGGL(k_dbg_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, hb, gall, headpos, m, derr);
+            hipLaunchKernelGGL(k_dbg_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, hb, headpos, m, derr);
             SALZ_LAUNCH_CHECK();
         }
 
         {
-            uint64_t *wg = reinterpret_cast<uint64_t *>(ws.u0), *wl = wg + nw_max;  // hb is spent
+            // per-wave group sums in u1 (u0 holds the head ballots until k_commit)
+            uint64_t *wg = reinterpret_cast<uint64_t *>(ws.u1), *wl = wg + nw_max;
             const size_t nwg = ((size_t)G + 63) / 64;
             hipLaunchKernelGGL(k_grpsum, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, G, wg, wl);
             SALZ_LAUNCH_CHECK();
@@ -823,7 +831,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         const uint32_t parts = (m >= (32u << 20) && split_on && many) ? (parts_all > 1 ? parts_all : 2) : 1;
         const uint32_t span = (uint32_t)(((uint64_t)n + parts - 1) / parts);
         uint32_t *later = reinterpret_cast<uint32_t *>(Kx);  // free until k_keys
-        hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, gall, headpos,
+        hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, headpos,
                            gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, kb_old,
                            round0, derr, parts > 1 ? span : 0xffffffffu, parts > 1 ? later : nullptr);
         SALZ_LAUNCH_CHECK();
