@@ -135,54 +135,64 @@ __device__ __forceinline__ void grp_vals(const uint32_t *__restrict__ headpos, s
     ls = lc ? size : 0u;
 }
 
-__global__ __launch_bounds__(kT) void k_grpsum(const uint32_t *__restrict__ headpos, uint32_t G,
+// G is read on the device (the host does not wait for it in most rounds); both kernels loop
+// over waves of groups, nwv waves at most (the scan runs over all nwv wave sums).
+__global__ __launch_bounds__(kT) void k_grpsum(const uint32_t *__restrict__ headpos,
+                                               const uint32_t *__restrict__ Gp, uint32_t nwv,
                                                uint64_t *__restrict__ wg, uint64_t *__restrict__ wl)
 {
-    const size_t g = (size_t)blockIdx.x * kT + threadIdx.x;
-    if ((g & ~(size_t)63) >= G)
-        return;  // whole wave past the end
-    uint32_t gs, gc, ls, lc;
-    grp_vals(headpos, g, G, gs, gc, ls, lc);
+    const uint32_t G = *Gp, lane = threadIdx.x & 63u;
+    for (uint32_t w = blockIdx.x * (kT / 64) + (threadIdx.x >> 6); w < nwv;
+         w += gridDim.x * (kT / 64)) {
+        const size_t g = (size_t)w * 64 + lane;
+        uint32_t gs = 0, gc = 0, ls = 0, lc = 0;
+        if ((size_t)w * 64 < G) {  // wave-uniform
+            grp_vals(headpos, g, G, gs, gc, ls, lc);
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        gs += shfl_xor_u32(gs, d);
-        gc += shfl_xor_u32(gc, d);
-        ls += shfl_xor_u32(ls, d);
-        lc += shfl_xor_u32(lc, d);
-    }
-    if ((g & 63u) == 0) {
-        wg[g >> 6] = (uint64_t)gs << 32 | gc;
-        wl[g >> 6] = (uint64_t)ls << 32 | lc;
+            for (int d = 32; d >= 1; d >>= 1) {
+                gs += shfl_xor_u32(gs, d);
+                gc += shfl_xor_u32(gc, d);
+                ls += shfl_xor_u32(ls, d);
+                lc += shfl_xor_u32(lc, d);
+            }
+        }
+        if (lane == 0) {
+            wg[w] = (uint64_t)gs << 32 | gc;
+            wl[w] = (uint64_t)ls << 32 | lc;
+        }
     }
 }
 
-__global__ __launch_bounds__(kT) void k_grpscan(const uint32_t *__restrict__ headpos, uint32_t G,
+__global__ __launch_bounds__(kT) void k_grpscan(const uint32_t *__restrict__ headpos,
+                                                const uint32_t *__restrict__ Gp, uint32_t nwv,
                                                 const uint64_t *__restrict__ wg,
                                                 const uint64_t *__restrict__ wl,
                                                 uint64_t *__restrict__ gsc, uint64_t *__restrict__ lsc)
 {
-    const size_t g = (size_t)blockIdx.x * kT + threadIdx.x;
-    if ((g & ~(size_t)63) >= G)
-        return;
-    uint32_t gs, gc, ls, lc;
-    grp_vals(headpos, g, G, gs, gc, ls, lc);
-    const uint32_t lane = (uint32_t)(g & 63u);
-    uint32_t xs = gs, xc = gc, ys = ls, yc = lc;  // inclusive wave scans
+    const uint32_t G = *Gp, lane = threadIdx.x & 63u;
+    const uint32_t nw = (uint32_t)(((uint64_t)G + 63) / 64) < nwv ? (uint32_t)(((uint64_t)G + 63) / 64) : nwv;
+    for (uint32_t w = blockIdx.x * (kT / 64) + (threadIdx.x >> 6); w < nw;
+         w += gridDim.x * (kT / 64)) {
+        const size_t g = (size_t)w * 64 + lane;
+        uint32_t gs, gc, ls, lc;
+        grp_vals(headpos, g, G, gs, gc, ls, lc);
+        uint32_t xs = gs, xc = gc, ys = ls, yc = lc;  // inclusive wave scans
 #pragma unroll
-    for (unsigned d = 1; d < 64; d <<= 1) {
-        const uint32_t a = shfl_up_u32(xs, d), b = shfl_up_u32(xc, d);
-        const uint32_t e = shfl_up_u32(ys, d), f = shfl_up_u32(yc, d);
-        if (lane >= d) {
-            xs += a;
-            xc += b;
-            ys += e;
-            yc += f;
+        for (unsigned d = 1; d < 64; d <<= 1) {
+            const uint32_t a = shfl_up_u32(xs, d), b = shfl_up_u32(xc, d);
+            const uint32_t e = shfl_up_u32(ys, d), f = shfl_up_u32(yc, d);
+            if (lane >= d) {
+                xs += a;
+                xc += b;
+                ys += e;
+                yc += f;
+            }
         }
-    }
-    const uint64_t pg = wg[g >> 6], pl = wl[g >> 6];
-    if (g < G) {
-        gsc[g] = pg + ((uint64_t)(xs - gs) << 32 | (xc - gc));
-        lsc[g] = pl + ((uint64_t)(ys - ls) << 32 | (yc - lc));
+        const uint64_t pg = wg[w], pl = wl[w];
+        if (g < G) {
+            gsc[g] = pg + ((uint64_t)(xs - gs) << 32 | (xc - gc));
+            lsc[g] = pl + ((uint64_t)(ys - ls) << 32 | (yc - lc));
+        }
     }
 }
 
@@ -792,9 +802,15 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
             return -1;
         hipLaunchKernelGGL(k_headpos, dim3(grid_for(m, kT)), dim3(kT), 0, st, hb, m, headpos);
         SALZ_LAUNCH_CHECK();
-        if (read_scalars(ws, 0, 64, "sa.G") != 0)
-            return -1;
-        uint32_t G = reinterpret_cast<uint32_t *>(ws.hscal)[0];
+        // The host needs G only to choose the split rank scatter (large rounds) and for the
+        // debug checks; other rounds do not wait for it.
+        const bool need_G = dbg_rounds || verbose || (m >= (32u << 20) && split_on);
+        uint32_t G = 0;
+        if (need_G) {
+            if (read_scalars(ws, 0, 64, "sa.G") != 0)
+                return -1;
+            G = reinterpret_cast<uint32_t *>(ws.hscal)[0];
+        }
         if (dbg_rounds) {
             hipLaunchKernelGGL(k_dbg_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, hb, headpos, m, derr);
             SALZ_LAUNCH_CHECK();
@@ -803,15 +819,16 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         {
             // per-wave group sums in u1 (u0 holds the head ballots until k_commit)
             uint64_t *wg = reinterpret_cast<uint64_t *>(ws.u1), *wl = wg + nw_max;
-            const size_t nwg = ((size_t)G + 63) / 64;
-            hipLaunchKernelGGL(k_grpsum, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, G, wg, wl);
+            const uint32_t nwg = (uint32_t)(((uint64_t)(need_G ? G : m) + 63) / 64);
+            const unsigned ggrid = grid_for((size_t)nwg * 64, kT) < 8192u ? grid_for((size_t)nwg * 64, kT) : 8192u;
+            hipLaunchKernelGGL(k_grpsum, dim3(ggrid), dim3(kT), 0, st, headpos, d32 + 0, nwg, wg, wl);
             SALZ_LAUNCH_CHECK();
             if (scan_sum_u64(wg, wg, nwg, false, d64, ws, st) != 0)
                 return -1;
             if (scan_sum_u64(wl, wl, nwg, false, d64 + 1, ws, st) != 0)
                 return -1;
-            hipLaunchKernelGGL(k_grpscan, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, G, wg, wl,
-                               gsc, ws.lsc);
+            hipLaunchKernelGGL(k_grpscan, dim3(ggrid), dim3(kT), 0, st, headpos, d32 + 0, nwg, wg,
+                               wl, gsc, ws.lsc);
             SALZ_LAUNCH_CHECK();
         }
         if (dbg_rounds) {
