@@ -101,8 +101,11 @@ int scan_sum_u64(const uint64_t *in, uint64_t *out, size_t n, bool inclusive,
 // radix sort of (u64 key, u32 value) pairs on key bits [bit_lo, bit_hi) (radix.hip).
 // On return *keys / *vals point at whichever buffer holds the sorted result.
 constexpr int kRadixTile = 4096;
+// With `text` set, the first pass builds the round-0 suffix keys from the text itself (m = n
+// suffixes; *keys / *vals are not read).
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
-                     uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st);
+                     uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
+                     const uint8_t *text = nullptr);
 
 // stages
 int stage_suffix_array(Workspace &ws, uint32_t n);                 // sa.hip   -> ws.sa

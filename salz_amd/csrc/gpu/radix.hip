@@ -18,14 +18,39 @@ namespace salz {
 namespace {
 
 constexpr int kThreads = 256;
+
+// Round 0 of the suffix sorter (sa.hip) can start straight from the text: list entry c is
+// suffix i (the < 8 suffixes with fewer than 8 bytes left first, shortest first, then the rest
+// in text order) with the big-endian key of its first 8 bytes (missing bytes zero). The
+// first pass then builds (key, value) itself instead of reading an initial key/value array.
+struct TextSrc {
+    const uint8_t *T;  // padded text
+    uint32_t n;        // suffixes
+};
+
+__device__ __forceinline__ uint32_t init_suffix(size_t c, uint32_t n)
+{
+    const uint32_t s = n < 7 ? n : 7;
+    return c < s ? (n - 1u - (uint32_t)c) : ((uint32_t)c - s);
+}
+
+__device__ __forceinline__ uint64_t init_key(const TextSrc &t, uint32_t i)
+{
+    uint64_t w = load_u64_any(t.T, i);
+    const uint32_t left = t.n - i;
+    if (left < 8)
+        w &= (1ull << (8u * left)) - 1ull;
+    return __builtin_bswap64(w);
+}
 constexpr int kItems = 16;
 constexpr int kTile = kThreads * kItems;
 static_assert(kTile == kRadixTile, "tile size mismatch");
 
+template <bool kText>
 __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restrict__ keys,
                                                          uint32_t m, int shift,
                                                          uint32_t *__restrict__ counts,
-                                                         uint32_t ntiles)
+                                                         uint32_t ntiles, TextSrc txt)
 {
     // 32 sub-histograms (8 per wave, by lane & 7), 257 words apart so the copies of one digit
     // sit in different banks: lanes of a wave adding to a hot digit (text keys' leading bytes
@@ -41,7 +66,19 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
     const size_t base = (size_t)blockIdx.x * kTile;
     const uint4 *kp = reinterpret_cast<const uint4 *>(keys + base);
     const size_t left = m > base ? m - base : 0;
-    if (left >= (size_t)kTile) {
+    if (kText) {
+        // text loads unconditional (clamped entry), so none is issued under a narrower mask
+        uint64_t kk[kItems];
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            const size_t i = (size_t)j * kThreads + tid;
+            kk[j] = init_key(txt, init_suffix(i < left ? base + i : 0, txt.n));
+        }
+#pragma unroll
+        for (int j = 0; j < kItems; j++)
+            if ((size_t)j * kThreads + tid < left)
+                atomicAdd(&mine[(unsigned)(kk[j] >> shift) & 255u], 1u);
+    } else if (left >= (size_t)kTile) {
         uint4 x[kItems / 2];
 #pragma unroll
         for (int j = 0; j < kItems / 2; j++)
@@ -120,10 +157,12 @@ __global__ __launch_bounds__(kRowThreads) void k_radix_rowscan(uint32_t *__restr
         totals[blockIdx.x] = carry;
 }
 
+template <bool kText>
 __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
     uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t m, int shift,
-    const uint32_t *__restrict__ offs, uint32_t ntiles, const uint32_t *__restrict__ totals)
+    const uint32_t *__restrict__ offs, uint32_t ntiles, const uint32_t *__restrict__ totals,
+    TextSrc txt)
 {
     // Keys and values are staged one after the other in the same 32 KB (4 workgroups per CU
     // instead of 2 with a 48 KB key + value stage).
@@ -148,8 +187,15 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     for (int j = 0; j < kItems; j++) {
         size_t i = base + (size_t)j * 64 + lane;
         bool ok = i < m;
-        k[j] = ok ? kin[i] : 0ull;
-        v[j] = ok ? vin[i] : 0u;
+        if (kText) {  // unconditional text loads (clamped entry)
+            const uint32_t sfx = init_suffix(ok ? i : 0, txt.n);
+            const uint64_t kk = init_key(txt, sfx);
+            k[j] = ok ? kk : 0ull;
+            v[j] = sfx;
+        } else {
+            k[j] = ok ? kin[i] : 0ull;
+            v[j] = ok ? vin[i] : 0u;
+        }
     }
 
 #pragma unroll
@@ -267,7 +313,8 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
 }  // namespace
 
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
-                     uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st)
+                     uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
+                     const uint8_t *text)
 {
     if (m <= 1 || bit_hi <= bit_lo)
         return 0;
@@ -280,8 +327,15 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     uint64_t *kin = *keys, *kout = keys_alt;
     uint32_t *vin = *vals, *vout = vals_alt;
     for (int shift = bit_lo; shift < bit_hi; shift += 8) {
-        hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(kThreads), 0, st, kin, m, shift,
-                           ws.radix_counts, ntiles);
+        // first pass from the text (round 0 of the suffix sorter): no initial key/value read
+        const bool from_text = text && shift == bit_lo;
+        const TextSrc txt{text, m};
+        if (from_text)
+            hipLaunchKernelGGL(k_radix_hist<true>, dim3(ntiles), dim3(kThreads), 0, st, kin, m,
+                               shift, ws.radix_counts, ntiles, txt);
+        else
+            hipLaunchKernelGGL(k_radix_hist<false>, dim3(ntiles), dim3(kThreads), 0, st, kin, m,
+                               shift, ws.radix_counts, ntiles, txt);
         SALZ_LAUNCH_CHECK();
         uint32_t *totals = ws.radix_counts + ncounts;
         hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(kRowThreads), 0, st, ws.radix_counts,
@@ -290,8 +344,12 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
         bool timed = ws.timing && ws.rx_used + 2 <= ws.rx_pool.size();
         if (timed)
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used], st));
-        hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, kout,
-                           vout, m, shift, ws.radix_counts, ntiles, totals);
+        if (from_text)
+            hipLaunchKernelGGL(k_radix_scatter<true>, dim3(ntiles), dim3(kThreads), 0, st, kin,
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt);
+        else
+            hipLaunchKernelGGL(k_radix_scatter<false>, dim3(ntiles), dim3(kThreads), 0, st, kin,
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt);
         SALZ_LAUNCH_CHECK();
         if (timed) {
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used + 1], st));

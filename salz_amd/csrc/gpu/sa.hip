@@ -704,8 +704,14 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     static const bool split_on = !getenv("SALZ_COMMIT_SPLIT") || atoi(getenv("SALZ_COMMIT_SPLIT")) > 1;
     static const uint32_t split_ratio = getenv("SALZ_SPLIT_RATIO") ? (uint32_t)atoi(getenv("SALZ_SPLIT_RATIO")) : 4;
     SALZ_HIP(hipMemsetAsync(ws.rank + n, 0, sizeof(uint32_t), st));  // rank[n] = 0
-    hipLaunchKernelGGL(k_sa_init, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, n, K, V);
-    SALZ_LAUNCH_CHECK();
+    // Round 0's first radix pass reads the text itself (radix.hip, TextSrc); the initial
+    // key/value arrays are only materialised for the per-round checks, and for n = 1 (the
+    // sort has nothing to do and would leave them unwritten).
+    const bool text_first = !dbg_rounds && n > 1;
+    if (!text_first) {
+        hipLaunchKernelGGL(k_sa_init, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, n, K, V);
+        SALZ_LAUNCH_CHECK();
+    }
     if (dbg_rounds) {
         hipLaunchKernelGGL(k_dbg_pairs, dim3(grid_for(n, kT)), dim3(kT), 0, st, K, V, ws.rank, ws.text, n, n,
                            0u, 0, 1, derr);
@@ -735,7 +741,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         const char *how = "global";
         bool seg_round = false;
         if (round0) {
-            if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, 64, ws, st) != 0)
+            if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, 64, ws, st, text_first ? ws.text : nullptr) != 0)
                 return -1;
         } else {
             // Global sort of every active suffix on (group, rank) vs. LDS sort of the small
