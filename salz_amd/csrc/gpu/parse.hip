@@ -89,10 +89,14 @@ __device__ __forceinline__ uint64_t far_state(const uint64_t *pst, const uint32_
     return q < b ? pst[base + ((size_t)(q - a) << 6)] : ((uint64_t)cin[sidx(q, klog)] << 32) | q;
 }
 
+// wdirty (from the third pass on): one flag per wave of 64 chunks; a clean wave's chunks
+// would repeat their decisions (k_parse_mark), so they only carry their choices over, and
+// their states stay valid through dsum (the uniform cost shift added since their last pass).
 __global__ __launch_bounds__(kT) void k_parse_chunk(
     const uint4 *__restrict__ cand, const uint32_t *__restrict__ cin, uint64_t *__restrict__ pst,
     const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, uint32_t klog,
-    uint32_t *__restrict__ changed, uint32_t *err, uint32_t *__restrict__ eflag)
+    uint32_t *__restrict__ changed, uint32_t *err, uint32_t *__restrict__ eflag,
+    const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum)
 {
     const uint32_t c = blockIdx.x * kT + threadIdx.x;  // chunk
     const uint64_t a64 = (uint64_t)c << klog;
@@ -106,6 +110,13 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
         const uint32_t jn = b - a;
         auto slot = [&](uint32_t j) { return base + ((size_t)j << 6); };
+        if (wdirty && !wdirty[c >> 6]) {  // wave-uniform: a clean wave
+            for (uint32_t j = 0; j < jn; j++)
+                chnew[slot(j)] = chold[slot(j)];
+            return;
+        }
+        if (dsum)
+            dsum[c] = 0;  // this pass's states are computed from cin itself
         const uint4 none = make_uint4(1u, 0u, 1u, 0u);
         // rings, index k = position p - k for the current p
         uint4 cr[kDepth + 1];
@@ -206,28 +217,36 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         atomicAdd(changed, diff);
 }
 
-// Uniform-shift test of one chunk per lane (see the host loop): every target at or past the
-// chunk end b (the literal's b, and each candidate's p + len beyond it) must have moved by the
-// same delta from cold to cnew; costs at or above 2^30 fail it (int32 compares could wrap).
-// *fail counts the chunks that do not pass.
-__global__ __launch_bounds__(kT) void k_parse_check(const uint4 *__restrict__ cand,
-                                                    const uint32_t *__restrict__ cnew,
-                                                    const uint32_t *__restrict__ cold, uint32_t n,
-                                                    uint32_t klog, uint32_t *fail)
+// Uniform-shift test, one chunk per lane, before every pass from the third on: every target
+// at or past the chunk end b (the literal's b, and each candidate's p + len beyond it) must
+// have moved by the same delta from cold (the costs the chunk's decisions are consistent
+// with) to cnew (the exact costs of the current decisions); costs at or above 2^30 fail it
+// (int32 compares could wrap). Then every option of every position moved by that delta, so the
+// argmins repeat. A wave of 64 chunks that all pass is clean (wdirty = 0) and skips the pass;
+// its chunks' states then lag cin by the delta, which dsum accumulates. ndirty counts the
+// dirty waves; none left means the fixed point.
+__global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ cand,
+                                                   const uint32_t *__restrict__ cnew,
+                                                   const uint32_t *__restrict__ cold, uint32_t n,
+                                                   uint32_t klog, uint8_t *__restrict__ wdirty,
+                                                   uint32_t *__restrict__ dsum,
+                                                   uint32_t *__restrict__ ndirty)
 {
     const uint32_t c = blockIdx.x * kT + threadIdx.x;
     const uint64_t a64 = (uint64_t)c << klog;
+    if ((a64 & ~(((uint64_t)64 << klog) - 1)) >= n)
+        return;  // whole wave past the end
     bool bad = false;
+    uint32_t d0 = 0;
     if (a64 < n) {
         const uint32_t a = (uint32_t)a64, K = 1u << klog;
         const uint32_t b = (n - a) < K ? n : a + K;
         const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
         const size_t sb = sidx(b, klog);
         const uint32_t nb = cnew[sb];
-        const uint32_t d0 = nb - cold[sb];  // the literal from b - 1
+        d0 = nb - cold[sb];
         bad = nb >= (1u << 30);
         const uint32_t jn = b - a;
-        // eight rows per step, loads first (no early exit: the loads stay in flight together)
         for (uint32_t j0 = 0; j0 < jn; j0 += 8) {
             uint4 cd[8];
 #pragma unroll
@@ -249,20 +268,25 @@ __global__ __launch_bounds__(kT) void k_parse_check(const uint4 *__restrict__ ca
         }
     }
     const uint64_t m = wave_ballot(bad);
-    if (lane_id() == 0 && m)
-        atomicAdd(fail, (uint32_t)__popcll(m));
+    if (lane_id() == 0) {
+        wdirty[c >> 6] = m ? 1u : 0u;
+        if (m)
+            atomicAdd(ndirty, 1u);
+    }
+    if (!m && a64 < n)
+        dsum[c] += d0;
 }
 
 // Exit flags (marked by the chunk pass) and the compacted exit index live in storage (slot)
 // order like the other parse arrays.
 
 // Compact E: node x = eidx[slot of q] for exit position q; parent = exit of q, weight =
-// in-chunk bit sum of q's path (estimate - cin[exit]).
+// in-chunk bit sum of q's path (estimate + dsum of q's chunk - cin[exit]).
 __global__ void k_compact_exits(const uint32_t *__restrict__ eflag,
                                 const uint32_t *__restrict__ eidx, const uint64_t *__restrict__ pst,
                                 const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog, size_t S,
                                 uint32_t *__restrict__ elist, uint32_t *__restrict__ jt0,
-                                uint32_t *__restrict__ js)
+                                uint32_t *__restrict__ js, const uint32_t *__restrict__ dsum)
 {
     size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
     if (s >= S || !eflag[s])
@@ -277,7 +301,7 @@ __global__ void k_compact_exits(const uint32_t *__restrict__ eflag,
         const uint64_t v = pst[s];
         const size_t se = sidx((uint32_t)v, klog);
         jt0[x] = eidx[se];
-        js[x] = (uint32_t)(v >> 32) - cin[se];
+        js[x] = (uint32_t)(v >> 32) + dsum[q >> klog] - cin[se];
     }
 }
 
@@ -312,7 +336,7 @@ __global__ void k_jump2(const uint32_t *__restrict__ jt, const uint32_t *__restr
 __global__ void k_cost_rest(const uint32_t *__restrict__ eflag, const uint32_t *__restrict__ eidx,
                             const uint32_t *__restrict__ js, const uint64_t *__restrict__ pst,
                             const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog, size_t S,
-                            uint32_t *cost)
+                            uint32_t *cost, const uint32_t *__restrict__ dsum)
 {
     size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
     if (s >= S)
@@ -326,7 +350,7 @@ __global__ void k_cost_rest(const uint32_t *__restrict__ eflag, const uint32_t *
     }
     const uint64_t v = pst[s];
     const size_t se = sidx((uint32_t)v, klog);
-    cost[s] = (uint32_t)(v >> 32) - cin[se] + js[eidx[se]];
+    cost[s] = (uint32_t)(v >> 32) + dsum[(uint32_t)p >> klog] - cin[se] + js[eidx[se]];
 }
 
 }  // namespace
@@ -369,7 +393,15 @@ int stage_parse(Workspace &ws, uint32_t n)
     const size_t snap_cap = 2 * (ws.cap_n + 1);
     uint32_t *changed = reinterpret_cast<uint32_t *>(ws.dscal) + 48;
     uint32_t *etotal = reinterpret_cast<uint32_t *>(ws.dscal) + 49;
+    uint32_t *ndirty = reinterpret_cast<uint32_t *>(ws.dscal) + 50;
     static const bool verbose = getenv("SALZ_DEBUG_PARSE") != nullptr;
+    // Wave skipping from the third pass on (k_parse_mark); SALZ_PARSE_SKIP=0 runs every chunk
+    // every pass (tests compare both).
+    const bool skip_on = !getenv("SALZ_PARSE_SKIP") || atoi(getenv("SALZ_PARSE_SKIP")) != 0;
+    // per chunk: uniform cost shift since its last pass; per wave: dirty flag (lsc is free here)
+    uint32_t *dsum = reinterpret_cast<uint32_t *>(ws.lsc);
+    uint8_t *wdirty = reinterpret_cast<uint8_t *>(dsum + ps.nchunks);
+    SALZ_HIP(hipMemsetAsync(dsum, 0, sizeof(uint32_t) * ps.nchunks, st));
 
     hipLaunchKernelGGL(k_cost_seed, dim3(grid_for(S, kT)), dim3(kT), 0, st, cost[0], n, klog, S);
     SALZ_LAUNCH_CHECK();
@@ -379,15 +411,47 @@ int stage_parse(Workspace &ws, uint32_t n)
     ps.n_exit = 0;
     ps.levels = 0;
     int it = 0;
+    uint32_t prev_changed = 0xffffffffu;
     for (;; it++) {
         const int cur = it & 1;
         uint32_t *cin = cost[cur], *cout = cost[cur ^ 1];
         uint8_t *chold = choice[cur], *chnew = choice[cur ^ 1];
+        // From the third pass on, waves of chunks whose decisions would repeat skip the pass,
+        // and a pass with no dirty wave left is not run at all: the previous decisions are the
+        // fixed point and cin their exact costs (k_parse_mark, DESIGN.md "Parse"). The test
+        // costs about a third of a pass. A large block's pass is latency-bound (its duration is
+        // one lane's walk, however few waves run), so there it pays only as the stopping test:
+        // before the third pass when the second changed few decisions (text stops there), later
+        // once almost none change. Smaller blocks, encoded several at a time, where skipped waves
+        // save throughput, run it before every pass from the third.
+        const bool late = (uint64_t)prev_changed * 64 < n &&
+                          (it == 2 || (uint64_t)prev_changed * 4096 < n);
+        const bool skipping = it >= 2 && (n < (1u << 25) || late);
+        if (skipping) {
+            SALZ_HIP(hipMemsetAsync(ndirty, 0, 4, st));
+            hipLaunchKernelGGL(k_parse_mark, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st,
+                               ws.cand, cin, cout, n, klog, wdirty, dsum, ndirty);
+            SALZ_LAUNCH_CHECK();
+            if (read_scalars(ws, 0, 256, "parse.mark") != 0)
+                return -1;
+            const uint32_t nd = reinterpret_cast<uint32_t *>(ws.hscal)[50];
+            if (verbose)
+                fprintf(stderr, "parse it=%d dirty waves %u of %u\n", it, nd, (ps.nchunks + 63) / 64);
+            if (nd == 0) {
+                ps.choice = chold;
+                ps.cost = cin;
+                break;
+            }
+        }
         SALZ_HIP(hipMemsetAsync(changed, 0, 4, st));
-        SALZ_HIP(hipMemsetAsync(eflag, 0, sizeof(uint32_t) * S, st));
+        // Exit flags accumulate once waves skip passes: a skipped chunk's exits stay marked
+        // from the pass that chose them (stale exits only add nodes to the forest).
+        if (!skipping)
+            SALZ_HIP(hipMemsetAsync(eflag, 0, sizeof(uint32_t) * S, st));
         hipLaunchKernelGGL(k_parse_chunk, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
                            cin, ws.pst, chold, chnew, n, klog, changed,
-                           reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord, eflag);
+                           reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord, eflag,
+                           skipping && skip_on ? wdirty : nullptr, dsum);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 256, "parse.changed") != 0)
             return -1;
@@ -403,6 +467,7 @@ int stage_parse(Workspace &ws, uint32_t n)
             ps.cost = cin;
             break;
         }
+        prev_changed = nchanged;
         // After t passes the last t chunks hold exact decisions (the last one sees only exact
         // costs, then induction), so nchunks + 1 passes always suffice.
         if ((uint32_t)it > ps.nchunks + 1) {
@@ -425,7 +490,7 @@ int stage_parse(Workspace &ws, uint32_t n)
             return -1;
         }
         hipLaunchKernelGGL(k_compact_exits, dim3(grid_for(S, kT)), dim3(kT), 0, st, eflag, eidx,
-                           ws.pst, cin, n, klog, S, elist, snap, js[0]);
+                           ws.pst, cin, n, klog, S, elist, snap, js[0], dsum);
         SALZ_LAUNCH_CHECK();
         int jc = 0;
         if (snaps) {
@@ -449,32 +514,13 @@ int stage_parse(Workspace &ws, uint32_t n)
             }
         }
         hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(S, kT)), dim3(kT), 0, st, eflag, eidx, js[jc],
-                           ws.pst, cin, n, klog, S, cout);
+                           ws.pst, cin, n, klog, S, cout, dsum);
         SALZ_LAUNCH_CHECK();
         ps.n_exit = ne;
         ps.levels = K;
         ps.snaps = snaps;
         ps.elist = elist;
         ps.jt0 = snap;
-        // Convergence without a confirming pass: if every chunk's targets beyond its end all
-        // moved by one common delta between the costs this pass used (cin) and the exact costs
-        // of its decisions (cout), every option of every position moved by that delta, so the
-        // next pass would repeat these decisions (k_parse_check). The test costs about as much
-        // as a pass, so it is tried once, after the second pass, when few decisions changed:
-        // text (3 passes) then stops one pass early; mixed data (~12 passes) never tries.
-        if (it == 1 && (uint64_t)nchanged * 64 < n) {
-            SALZ_HIP(hipMemsetAsync(changed, 0, 4, st));
-            hipLaunchKernelGGL(k_parse_check, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
-                               cout, cin, n, klog, changed);
-            SALZ_LAUNCH_CHECK();
-            if (read_scalars(ws, 0, 256, "parse.check") != 0)
-                return -1;
-            if (reinterpret_cast<uint32_t *>(ws.hscal)[48] == 0) {
-                ps.choice = chnew;
-                ps.cost = cout;
-                break;
-            }
-        }
     }
     ws.stats.parse_iters = it + 1;
     ws.stats.exit_nodes = ps.n_exit;

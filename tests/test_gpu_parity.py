@@ -265,6 +265,30 @@ def test_lcp_paths(ctx, monkeypatch, lcp_sa, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
+@pytest.mark.parametrize("skip", ["1", "0"])
+@pytest.mark.parametrize("kind,n,seed,alpha,klog", [("mixed", 3_000_000, 3, 0, "6"),
+                                                    ("mixed", 2_000_001, 7, 0, "9"),
+                                                    ("text", 1_500_000, 2, 0, "7"),
+                                                    ("smx", 1_000_000, 4, 4, "6"),
+                                                    ("runs", 400_000, 0, 0, "6")])
+def test_parse_wave_skip(ctx, monkeypatch, skip, kind, n, seed, alpha, klog):
+    """From the third pass on, waves of chunks whose decisions would repeat skip the pass
+    (parse.hip k_parse_mark, SALZ_PARSE_SKIP=1, the default): decisions, the exact suffix
+    costs and the stream match the oracle with and without skipping."""
+    monkeypatch.setenv("SALZ_PARSE_SKIP", skip)
+    monkeypatch.setenv("SALZ_PARSE_KLOG", klog)
+    src = _make(kind, n, seed, alpha)
+    out, d = ctx.encode_dump(src)
+    o = oracle_stages(src)
+    for k in ("dlen", "doff"):
+        i = _first_diff(d[k], o[k])
+        assert i < 0, f"{k} differs at {i}: gpu {d[k][i]} oracle {o[k][i]}"
+    i = _first_diff(d["cost"][1:], o["cost"][1:])
+    assert i < 0, f"cost differs at {i + 1}"
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and out == ref
+
+
 def test_concurrent_contexts_match_oracle(salz):
     """Four contexts encoding at once on one GPU (threads, own streams): every stream must
     equal the CPU port's. Concurrent kernels once exposed a load-ordering hazard in the
