@@ -70,23 +70,40 @@ __global__ __launch_bounds__(kT) void k_cost_seed(uint32_t *cost, uint32_t n, ui
 // One lane per chunk, positions b-1 down to a. The states of the last kWin positions
 // (p+1 .. p+kWin) stay in registers, so a factor of length <= kWin reads its target from
 // there; a longer factor's target (p + len >= p + kWin + 1) was finished at least kWin + 1
-// steps earlier, so its load is issued kDepth = kWin steps ahead, and candidates one step
-// before that. A step then waits only on memory issued eight steps earlier (the previous
-// version, with a two-step pipeline, waited on a full HBM latency every other step).
+// steps earlier, so its load can be issued early: kDepth = 4 steps ahead, from a candidate
+// loaded kCDepth = 7 steps ahead. Every step issues the same memory operations at clamped,
+// always-valid addresses, no loaded value is examined before the step that needs it, and the
+// loop is unrolled by the rings' lengths (8 candidates, 4 far states), so the rings rotate by
+// register renaming: the compiler's waits are s_waitcnt vmcnt(k) for the load in use. The
+// previous form (conditional loads, selects on just-loaded values, rings shifted with moves
+// of in-flight registers) drained every outstanding load each step: one HBM latency per step.
 constexpr uint32_t kWin = 8;
-constexpr uint32_t kDepth = kWin;
+constexpr uint32_t kDepth = 4;
+constexpr uint32_t kCDepth = 7;
 
-// target state of a long factor (len > kWin), or 0 when the window serves it
-__device__ __forceinline__ uint64_t far_state(const uint64_t *pst, const uint32_t *cin, size_t base,
-                                              uint32_t a, uint32_t b, uint32_t klog, uint32_t p,
-                                              uint32_t len, uint32_t n, uint32_t *err)
+// Raw target state of a long factor: one 8-byte load. Inside the chunk it is the target's
+// state in pst; past it, the aligned pair of cin words holding cin[sidx(q)] (far_decode picks
+// the half). A factor that is not long (or runs past the end) loads its own chunk's first
+// state, pst[base]: the 64 lanes then read 512 contiguous bytes instead of 64 lines.
+__device__ __forceinline__ uint64_t far_load(const uint64_t *pst, const uint32_t *cin, size_t base,
+                                             uint32_t a, uint32_t b, uint32_t klog, uint32_t p,
+                                             uint32_t len, uint32_t n)
 {
-    if (len <= kWin)
-        return 0;
-    const uint32_t q = p + len;
-    if (bad_index(len > n - p, err, kErrParse))
-        return 0;
-    return q < b ? pst[base + ((size_t)(q - a) << 6)] : ((uint64_t)cin[sidx(q, klog)] << 32) | q;
+    const bool far = len > kWin && len <= n - p;
+    const uint32_t q = far ? p + len : a;
+    const uint64_t *addr = q < b ? pst + base + ((size_t)(q - a) << 6)
+                                 : reinterpret_cast<const uint64_t *>(cin) + (sidx(q, klog) >> 1);
+    return *addr;
+}
+
+// (cost << 32 | exit) of target q = p + len from its raw load; sidx(q) is odd iff its chunk
+// q >> klog is (the lane bit of the interleaved layout).
+__device__ __forceinline__ uint64_t far_decode(uint64_t raw, uint32_t q, uint32_t b, uint32_t klog)
+{
+    if (q < b)
+        return raw;
+    const uint32_t v = ((q >> klog) & 1u) ? (uint32_t)(raw >> 32) : (uint32_t)raw;
+    return ((uint64_t)v << 32) | q;
 }
 
 // wdirty (from the third pass on): one flag per wave of 64 chunks; a clean wave's chunks
@@ -100,7 +117,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
 {
     const uint32_t c = blockIdx.x * kT + threadIdx.x;  // chunk
     const uint64_t a64 = (uint64_t)c << klog;
-    uint32_t diff = 0;
+    uint32_t diff = 0, errw = 0;
     if (c == 0)
         eflag[sidx(n, klog)] = 1u;  // the root of the exit forest
     if (a64 < n) {
@@ -108,50 +125,58 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         const uint32_t K = 1u << klog;
         const uint32_t b = (n - a) < K ? n : a + K;
         const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
-        const uint32_t jn = b - a;
         auto slot = [&](uint32_t j) { return base + ((size_t)j << 6); };
         if (wdirty && !wdirty[c >> 6]) {  // wave-uniform: a clean wave
-            for (uint32_t j = 0; j < jn; j++)
+            for (uint32_t j = 0; j < b - a; j++)
                 chnew[slot(j)] = chold[slot(j)];
             return;
         }
         if (dsum)
             dsum[c] = 0;  // this pass's states are computed from cin itself
-        const uint4 none = make_uint4(1u, 0u, 1u, 0u);
-        // rings, index k = position p - k for the current p
-        uint4 cr[kDepth + 1];
+        // Every lane walks K steps, a + K - 1 down to a: the text's last chunk starts past the
+        // end (those steps are inert, below), so the loop count is wave-uniform (a scalar
+        // counter, no EXEC change inside the loop) and the loop is unrolled by the rings'
+        // length. Positions past n lie inside the layout's last tile; their slots are never read.
+        // Rings, index k = position p - k for the current p.
+        uint4 cr[kCDepth + 1];
         uint8_t orr[kDepth];
-        uint64_t tP[kDepth], tN[kDepth];
+        uint64_t fP[kDepth], fN[kDepth];
         uint64_t win[kWin];  // win[k] = state of p + 1 + k
-        const uint32_t p0 = b - 1;
+        const uint32_t pK = a + K - 1;
 #pragma unroll
-        for (uint32_t k = 0; k <= kDepth; k++)
-            cr[k] = jn > k ? cand[slot(jn - 1 - k)] : none;
+        for (uint32_t k = 0; k <= kCDepth; k++)
+            cr[k] = cand[slot(K - 1 - k)];
 #pragma unroll
         for (uint32_t k = 0; k < kDepth; k++) {
-            orr[k] = jn > k ? chold[slot(jn - 1 - k)] : 0;
-            tP[k] = jn > k ? far_state(pst, cin, base, a, b, klog, p0 - k, cr[k].y, n, err) : 0;
-            tN[k] = jn > k ? far_state(pst, cin, base, a, b, klog, p0 - k, cr[k].w, n, err) : 0;
+            orr[k] = chold[slot(K - 1 - k)];
+            fP[k] = far_load(pst, cin, base, a, b, klog, pK - k, cr[k].y, n);
+            fN[k] = far_load(pst, cin, base, a, b, klog, pK - k, cr[k].w, n);
         }
 #pragma unroll
-        for (uint32_t k = 0; k < kWin; k++) {  // exits b .. b + kWin - 1 (past n: never a target)
-            const uint32_t q = b + k;
-            win[k] = q <= n ? (((uint64_t)cin[sidx(q, klog)] << 32) | q) : 0;
+        for (uint32_t k = 0; k < kWin; k++) {  // states a + K .. a + K + kWin - 1 (past n: unused)
+            const uint32_t q = a + K + k;
+            const uint32_t v = cin[sidx(q <= n ? q : n, klog)];
+            win[k] = q <= n ? (((uint64_t)v << 32) | q) : 0;
         }
         uint32_t last_ex = 0xffffffffu;
-        for (uint32_t j = jn; j-- > 0;) {
+#pragma unroll 8
+        for (uint32_t j = K; j-- > 0;) {
             const uint32_t p = a + j;
+            const bool live = p < b;
             const uint4 c0 = cr[0];
             uint32_t best = 9u + (uint32_t)(win[0] >> 32), ex = (uint32_t)win[0];
             uint8_t ch = 0;
             if (p != 0) {
                 if (c0.y >= 3u) {
-                    uint64_t t = tP[0];
+                    errw |= live && c0.y > n - p ? kErrParse : 0u;
+                    uint64_t t;
                     if (c0.y <= kWin) {
-                        bad_index(c0.y > n - p, err, kErrParse);
+                        t = win[1];
 #pragma unroll
                         for (uint32_t k = 2; k < kWin; k++)
                             t = c0.y == k + 1 ? win[k] : t;
+                    } else {
+                        t = far_decode(fP[0], p + c0.y, b, klog);
                     }
                     const uint32_t alt = factor_bits(c0.x, c0.y) + (uint32_t)(t >> 32);
                     if ((int32_t)alt < (int32_t)best) {
@@ -161,12 +186,15 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
                     }
                 }
                 if (c0.w >= 3u) {
-                    uint64_t t = tN[0];
+                    errw |= live && c0.w > n - p ? kErrParse : 0u;
+                    uint64_t t;
                     if (c0.w <= kWin) {
-                        bad_index(c0.w > n - p, err, kErrParse);
+                        t = win[1];
 #pragma unroll
                         for (uint32_t k = 2; k < kWin; k++)
                             t = c0.w == k + 1 ? win[k] : t;
+                    } else {
+                        t = far_decode(fN[0], p + c0.w, b, klog);
                     }
                     const uint32_t alt = factor_bits(c0.z, c0.w) + (uint32_t)(t >> 32);
                     if ((int32_t)alt < (int32_t)best) {
@@ -176,40 +204,48 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
                     }
                 }
             }
-            const uint64_t stp = ((uint64_t)best << 32) | ex;
+            // An inert step (past the end) leaves the state of a position no live one reads,
+            // except n itself: (cost 0, exit n).
+            if (!live)
+                ex = n;
+            const uint64_t stp = live ? ((uint64_t)best << 32) | ex : (uint64_t)n;
             pst[slot(j)] = stp;
             chnew[slot(j)] = ch;
-            diff += ch != orr[0];
-            // exit set E (every position's exit): consecutive positions mostly share one
-            if (ex != last_ex) {
-                eflag[sidx(ex, klog)] = 1u;
-                last_ex = ex;
-            }
+            diff += live && ch != orr[0];
+            // Exit set E (every position's exit; consecutive positions mostly share one). The
+            // store is issued every step, as a store under a narrower EXEC mask would leave
+            // partial vmcnt waits depending on whether it ran (tests/test_codegen.py); a lane
+            // whose exit did not change writes the root's flag (set anyway), so those lanes
+            // share one line instead of each touching its own.
+            eflag[sidx(ex != last_ex ? ex : n, klog)] = 1u;
+            last_ex = ex;
             // shift the window and the rings one position down
 #pragma unroll
             for (uint32_t k = kWin - 1; k > 0; k--)
                 win[k] = win[k - 1];
             win[0] = stp;
 #pragma unroll
-            for (uint32_t k = 0; k < kDepth; k++)
+            for (uint32_t k = 0; k < kCDepth; k++)
                 cr[k] = cr[k + 1];
 #pragma unroll
             for (uint32_t k = 0; k + 1 < kDepth; k++) {
                 orr[k] = orr[k + 1];
-                tP[k] = tP[k + 1];
-                tN[k] = tN[k + 1];
+                fP[k] = fP[k + 1];
+                fN[k] = fN[k + 1];
             }
-            // new loads: the position kDepth below the next one (p - 1 - (kDepth - 1) = p - kDepth)
-            // and its candidate one step earlier still
-            if (j >= kDepth) {
-                const uint32_t pj = p - kDepth;
-                orr[kDepth - 1] = chold[slot(j - kDepth)];
-                tP[kDepth - 1] = far_state(pst, cin, base, a, b, klog, pj, cr[kDepth - 1].y, n, err);
-                tN[kDepth - 1] = far_state(pst, cin, base, a, b, klog, pj, cr[kDepth - 1].w, n, err);
-            }
-            cr[kDepth] = j >= kDepth + 1 ? cand[slot(j - kDepth - 1)] : none;
+            // new loads (unconditional, clamped): position p - kDepth's old choice and far
+            // targets (its candidate, cr[kDepth - 1], was loaded four steps ago), and position
+            // p - 1 - kCDepth's candidate
+            const uint32_t jd = j >= kDepth ? j - kDepth : 0u;
+            const uint4 cd = cr[kDepth - 1];
+            orr[kDepth - 1] = chold[slot(jd)];
+            fP[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, cd.y, n);
+            fN[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, cd.w, n);
+            cr[kCDepth] = cand[slot(j >= kCDepth + 1 ? j - kCDepth - 1 : 0u)];
         }
     }
+    if (errw)
+        atomicOr(err, errw);  // a candidate past the end (reported once per lane)
     // one atomic per wave
     for (int m = 32; m >= 1; m >>= 1)
         diff += shfl_xor_u32(diff, m);
