@@ -97,12 +97,11 @@ struct Token {
 __device__ __forceinline__ Token token_at(const uint4 *cand, const uint8_t *choice, uint32_t p,
                                           uint32_t klog)
 {
+    // both loads issued together (one memory latency per token of the path walk, not two)
     const size_t s = sidx(p, klog);
-    uint8_t ch = choice[s];
-    if (ch == 0)
-        return {1u, 0u};
-    uint4 c = cand[s];
-    return ch == 1 ? Token{c.y, c.x} : Token{c.w, c.z};
+    const uint8_t ch = choice[s];
+    const uint4 c = cand[s];
+    return ch == 0 ? Token{1u, 0u} : ch == 1 ? Token{c.y, c.x} : Token{c.w, c.z};
 }
 
 __global__ void k_emit_count(const uint4 *__restrict__ cand, const uint8_t *__restrict__ choice,

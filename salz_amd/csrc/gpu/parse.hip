@@ -283,13 +283,18 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
         d0 = nb - cold[sb];
         bad = nb >= (1u << 30);
         const uint32_t jn = b - a;
-        for (uint32_t j0 = 0; j0 < jn; j0 += 8) {
-            uint4 cd[8];
+        // K rows for every lane (rows past jn test b itself, which always passes), in batches
+        // of 8: a batch's candidates are loaded while the previous batch's costs are checked
+        // (two register sets, so no in-flight register is moved), and the loop count is
+        // wave-uniform.
+        auto load = [&](uint4(&cd)[8], uint32_t j0) {
 #pragma unroll
             for (uint32_t u = 0; u < 8; u++) {
                 const uint32_t j = j0 + u < jn ? j0 + u : jn - 1;
                 cd[u] = cand[base + ((size_t)j << 6)];
             }
+        };
+        auto check = [&](const uint4(&cd)[8], uint32_t j0) {
 #pragma unroll
             for (uint32_t u = 0; u < 8; u++) {
                 const uint32_t p = a + j0 + u;
@@ -301,6 +306,14 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
                 bad |= vp - cold[sp] != d0 || vp >= (1u << 30);
                 bad |= vn - cold[sn] != d0 || vn >= (1u << 30);
             }
+        };
+        uint4 A[8], B[8];
+        load(A, 0);
+        for (uint32_t j0 = 0; j0 < K; j0 += 16) {
+            load(B, j0 + 8);
+            check(A, j0);
+            load(A, j0 + 16);
+            check(B, j0 + 8);
         }
     }
     const uint64_t m = wave_ballot(bad);
