@@ -28,6 +28,8 @@ def load(path):
         name = m.group(1) if m else r["Kernel_Name"][:40]
         if "unsigned long" in r["Kernel_Name"] and name.startswith("k_scan"):
             name += "<u64>"
+        if name.startswith("k_radix") and ("ILb1E" in r["Kernel_Name"] or "<true>" in r["Kernel_Name"]):
+            name += "<text>"  # round 0's first pass (keys from the text): not the priced kernel
         per[name].append((int(r["Dispatch_Id"]), float(r["Counter_Value"]), int(r["Grid_Size"])))
     return per
 

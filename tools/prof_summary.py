@@ -11,7 +11,9 @@ for r in rows:
     name = r["Name"]
     m = re.search(r"(k_[a-z0-9_]+|__amd_rocclr_[A-Za-z]+)", name)
     short = m.group(1) if m else name[:34]
-    if "<unsigned long" in name:
+    if "k_radix" in short and ("ILb1E" in name or "<true>" in name):
+        short += "<text>"  # round 0's first pass, keys built from the text
+    elif "<unsigned long" in name:
         short += "<u64>"
     elif "MaxOp" in name:
         short += "<max>"
