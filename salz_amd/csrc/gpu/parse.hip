@@ -381,25 +381,47 @@ __global__ void k_jump2(const uint32_t *__restrict__ jt, const uint32_t *__restr
 }
 
 // Exact cost of every position: an exit's is its path sum (js after the jumps, through its
-// index in E), any other position adds its in-chunk bit sum to its exit's.
-__global__ void k_cost_rest(const uint32_t *__restrict__ eflag, const uint32_t *__restrict__ eidx,
-                            const uint32_t *__restrict__ js, const uint64_t *__restrict__ pst,
-                            const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog, size_t S,
-                            uint32_t *cost, const uint32_t *__restrict__ dsum)
+// index in E), any other position adds its in-chunk bit sum to its exit's. A thread takes
+// kRows consecutive positions of one chunk (the 64 lanes of a wave: 64 neighbouring chunks, so
+// every row is one contiguous run); consecutive positions mostly share their exit, whose cost
+// (cin, eidx, js: a dependent pair of gathers) is then loaded once.
+constexpr uint32_t kRows = 8;
+__global__ __launch_bounds__(kT) void k_cost_rest(const uint32_t *__restrict__ eflag,
+                                                  const uint32_t *__restrict__ eidx,
+                                                  const uint32_t *__restrict__ js,
+                                                  const uint64_t *__restrict__ pst,
+                                                  const uint32_t *__restrict__ cin, uint32_t n,
+                                                  uint32_t klog, size_t S, uint32_t *cost,
+                                                  const uint32_t *__restrict__ dsum)
 {
-    size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (s >= S)
+    const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
+    const uint32_t lane = (uint32_t)(x & 63u);
+    const size_t rest = x >> 6;
+    const uint32_t groups = (1u << klog) / kRows;
+    const size_t t = rest / groups;
+    const uint32_t g = (uint32_t)(rest % groups);
+    if ((t << (klog + 6)) >= S)
         return;
-    const uint64_t p = spos(s, klog);
-    if (p > n)
-        return;
-    if (eflag[s]) {
-        cost[s] = js[eidx[s]];
-        return;
+    const uint32_t c = (uint32_t)(t * 64 + lane);  // chunk
+    const uint32_t shift = (uint64_t)c << klog < n ? dsum[c] : 0u;
+    uint32_t last_se = 0xffffffffu, base_cost = 0;
+    for (uint32_t r = 0; r < kRows; r++) {
+        const size_t s = (t << (klog + 6)) | ((size_t)(g * kRows + r) << 6) | lane;
+        const uint64_t p = spos(s, klog);
+        if (p > n)
+            break;
+        if (eflag[s]) {
+            cost[s] = js[eidx[s]];
+            continue;
+        }
+        const uint64_t v = pst[s];
+        const uint32_t se = (uint32_t)sidx((uint32_t)v, klog);
+        if (se != last_se) {
+            base_cost = js[eidx[se]] - cin[se];
+            last_se = se;
+        }
+        cost[s] = (uint32_t)(v >> 32) + shift + base_cost;
     }
-    const uint64_t v = pst[s];
-    const size_t se = sidx((uint32_t)v, klog);
-    cost[s] = (uint32_t)(v >> 32) + dsum[(uint32_t)p >> klog] - cin[se] + js[eidx[se]];
 }
 
 }  // namespace
@@ -562,7 +584,7 @@ int stage_parse(Workspace &ws, uint32_t n)
                 jc ^= 1;
             }
         }
-        hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(S, kT)), dim3(kT), 0, st, eflag, eidx, js[jc],
+        hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(S / kRows, kT)), dim3(kT), 0, st, eflag, eidx, js[jc],
                            ws.pst, cin, n, klog, S, cout, dsum);
         SALZ_LAUNCH_CHECK();
         ps.n_exit = ne;
