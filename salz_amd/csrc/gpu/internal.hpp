@@ -95,6 +95,9 @@ int scan_sum_u32(const uint32_t *in, uint32_t *out, size_t n, bool inclusive,
                  uint32_t *total_out, Workspace &ws, hipStream_t st);
 int scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, bool inclusive,
                  uint32_t *total_out, Workspace &ws, hipStream_t st);
+// u8 flags -> u32 prefix sums
+int scan_sum_u8(const uint8_t *in, uint32_t *out, size_t n, bool inclusive, uint32_t *total_out,
+                Workspace &ws, hipStream_t st);
 int scan_sum_u64(const uint64_t *in, uint64_t *out, size_t n, bool inclusive,
                  uint64_t *total_out, Workspace &ws, hipStream_t st);
 

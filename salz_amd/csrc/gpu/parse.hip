@@ -112,7 +112,7 @@ __device__ __forceinline__ uint64_t far_decode(uint64_t raw, uint32_t q, uint32_
 __global__ __launch_bounds__(kT) void k_parse_chunk(
     const uint4 *__restrict__ cand, const uint32_t *__restrict__ cin, uint64_t *__restrict__ pst,
     const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, uint32_t klog,
-    uint32_t *__restrict__ changed, uint32_t *err, uint32_t *__restrict__ eflag,
+    uint32_t *__restrict__ changed, uint32_t *err, uint8_t *__restrict__ eflag,
     const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum)
 {
     const uint32_t c = blockIdx.x * kT + threadIdx.x;  // chunk
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
 
 // Compact E: node x = eidx[slot of q] for exit position q; parent = exit of q, weight =
 // in-chunk bit sum of q's path (estimate + dsum of q's chunk - cin[exit]).
-__global__ void k_compact_exits(const uint32_t *__restrict__ eflag,
+__global__ void k_compact_exits(const uint8_t *__restrict__ eflag,
                                 const uint32_t *__restrict__ eidx, const uint64_t *__restrict__ pst,
                                 const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog, size_t S,
                                 uint32_t *__restrict__ elist, uint32_t *__restrict__ jt0,
@@ -386,7 +386,7 @@ __global__ void k_jump2(const uint32_t *__restrict__ jt, const uint32_t *__restr
 // every row is one contiguous run); consecutive positions mostly share their exit, whose cost
 // (cin, eidx, js: a dependent pair of gathers) is then loaded once.
 constexpr uint32_t kRows = 8;
-__global__ __launch_bounds__(kT) void k_cost_rest(const uint32_t *__restrict__ eflag,
+__global__ __launch_bounds__(kT) void k_cost_rest(const uint8_t *__restrict__ eflag,
                                                   const uint32_t *__restrict__ eidx,
                                                   const uint32_t *__restrict__ js,
                                                   const uint64_t *__restrict__ pst,
@@ -456,7 +456,8 @@ int stage_parse(Workspace &ws, uint32_t n)
     }
     uint32_t *cost[2] = {ws.u0, ws.u1};
     uint8_t *choice[2] = {reinterpret_cast<uint8_t *>(ws.valA), reinterpret_cast<uint8_t *>(ws.valB)};
-    uint32_t *eflag = ws.offA, *eidx = ws.offB;
+    uint8_t *eflag = reinterpret_cast<uint8_t *>(ws.offA);  // exit flags, one byte per slot
+    uint32_t *eidx = ws.offB;
     uint32_t *elist = ws.rank;
     uint32_t *js[2] = {reinterpret_cast<uint32_t *>(ws.keyA),
                        reinterpret_cast<uint32_t *>(ws.keyA) + (ws.cap_n + 1)};
@@ -518,7 +519,7 @@ int stage_parse(Workspace &ws, uint32_t n)
         // Exit flags accumulate once waves skip passes: a skipped chunk's exits stay marked
         // from the pass that chose them (stale exits only add nodes to the forest).
         if (!skipping)
-            SALZ_HIP(hipMemsetAsync(eflag, 0, sizeof(uint32_t) * S, st));
+            SALZ_HIP(hipMemsetAsync(eflag, 0, S, st));
         hipLaunchKernelGGL(k_parse_chunk, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
                            cin, ws.pst, chold, chnew, n, klog, changed,
                            reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord, eflag,
@@ -546,7 +547,7 @@ int stage_parse(Workspace &ws, uint32_t n)
             return -1;
         }
         // Exact costs for the new decisions (E was marked by the chunk pass).
-        if (scan_sum_u32(eflag, eidx, S, false, etotal, ws, st) != 0)
+        if (scan_sum_u8(eflag, eidx, S, false, etotal, ws, st) != 0)
             return -1;
         if (read_scalars(ws, 0, 256, "parse.ne") != 0)
             return -1;

@@ -53,8 +53,8 @@ __device__ __forceinline__ T block_excl(T v, T *wsum, T &total, Op op)
     return op(wpre, ex);
 }
 
-template <typename T, typename Op>
-__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const T *__restrict__ in, size_t n,
+template <typename T, typename Op, typename TI = T>
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const TI *__restrict__ in, size_t n,
                                                               T *__restrict__ partial)
 {
     __shared__ T wsum[4];
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const T *__restric
     for (int j = 0; j < kScanItems; j++) {
         size_t i = base + (size_t)j * kScanThreads + threadIdx.x;
         if (i < n)
-            acc = op(acc, in[i]);
+            acc = op(acc, (T)in[i]);
     }
     T total;
     block_excl<T, Op>(acc, wsum, total, op);
@@ -73,8 +73,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const T *__restric
         partial[blockIdx.x] = total;
 }
 
-template <typename T, typename Op>
-__global__ __launch_bounds__(kScanThreads) void k_scan_tiles(const T *__restrict__ in, T *out,
+template <typename T, typename Op, typename TI = T>
+__global__ __launch_bounds__(kScanThreads) void k_scan_tiles(const TI *__restrict__ in, T *out,
                                                              size_t n, const T *__restrict__ carry,
                                                              int inclusive, T *total_out)
 {
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_tiles(const T *__restrict
     for (int j = 0; j < kScanItems; j++) {
         int l = j * kScanThreads + threadIdx.x;
         size_t i = base + l;
-        s[pidx(l)] = i < n ? in[i] : Op::id();
+        s[pidx(l)] = i < n ? (T)in[i] : Op::id();
     }
     __syncthreads();
     T loc[kScanItems];
@@ -118,15 +118,15 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_tiles(const T *__restrict
     }
 }
 
-template <typename T, typename Op>
-int scan_impl(const T *in, T *out, size_t n, bool inclusive, T *total_out, T *tmp,
+template <typename T, typename Op, typename TI = T>
+int scan_impl(const TI *in, T *out, size_t n, bool inclusive, T *total_out, T *tmp,
               size_t tmp_elems, hipStream_t st)
 {
     if (n == 0)
         return 0;
     size_t tiles = (n + kScanTile - 1) / kScanTile;
     if (tiles == 1) {
-        hipLaunchKernelGGL((k_scan_tiles<T, Op>), dim3(1), dim3(kScanThreads), 0, st, in, out,
+        hipLaunchKernelGGL((k_scan_tiles<T, Op, TI>), dim3(1), dim3(kScanThreads), 0, st, in, out,
                            n, (const T *)nullptr, inclusive ? 1 : 0, total_out);
         SALZ_LAUNCH_CHECK();
         return 0;
@@ -136,13 +136,13 @@ int scan_impl(const T *in, T *out, size_t n, bool inclusive, T *total_out, T *tm
         return -1;
     }
     T *partial = tmp;
-    hipLaunchKernelGGL((k_scan_reduce<T, Op>), dim3((unsigned)tiles), dim3(kScanThreads), 0,
+    hipLaunchKernelGGL((k_scan_reduce<T, Op, TI>), dim3((unsigned)tiles), dim3(kScanThreads), 0,
                        st, in, n, partial);
     SALZ_LAUNCH_CHECK();
     if (scan_impl<T, Op>(partial, partial, tiles, false, nullptr, tmp + tiles,
                          tmp_elems - tiles, st) != 0)
         return -1;
-    hipLaunchKernelGGL((k_scan_tiles<T, Op>), dim3((unsigned)tiles), dim3(kScanThreads), 0, st,
+    hipLaunchKernelGGL((k_scan_tiles<T, Op, TI>), dim3((unsigned)tiles), dim3(kScanThreads), 0, st,
                        in, out, n, (const T *)partial, inclusive ? 1 : 0, total_out);
     SALZ_LAUNCH_CHECK();
     return 0;
@@ -172,6 +172,14 @@ int scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, bool inclusive,
 {
     return scan_impl<uint32_t, MaxOp<uint32_t>>(in, out, n, inclusive, total_out,
                                                 (uint32_t *)ws.scan_tmp, ws.scan_tmp_bytes / 4, st);
+}
+
+int scan_sum_u8(const uint8_t *in, uint32_t *out, size_t n, bool inclusive, uint32_t *total_out,
+                Workspace &ws, hipStream_t st)
+{
+    return scan_impl<uint32_t, SumOp<uint32_t>, uint8_t>(in, out, n, inclusive, total_out,
+                                                         (uint32_t *)ws.scan_tmp,
+                                                         ws.scan_tmp_bytes / 4, st);
 }
 
 int scan_sum_u64(const uint64_t *in, uint64_t *out, size_t n, bool inclusive,
