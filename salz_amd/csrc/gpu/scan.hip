@@ -118,6 +118,56 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_tiles(const TI *__restric
     }
 }
 
+// Byte flags (u8 -> u32 sums), whole tiles: a thread's 16 consecutive elements are one 16-byte
+// load, so the input needs no LDS transpose and a wave reads 1 KB per instruction.
+__device__ __forceinline__ uint32_t bsum4(uint32_t w)
+{
+    const uint32_t x = (w & 0x00ff00ffu) + ((w >> 8) & 0x00ff00ffu);
+    return (x & 0xffffu) + (x >> 16);
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_flag_reduce(const uint4 *__restrict__ in,
+                                                              uint32_t *__restrict__ partial)
+{
+    __shared__ uint32_t wsum[4];
+    const uint4 v = in[(size_t)blockIdx.x * kScanThreads + threadIdx.x];
+    uint32_t total;
+    block_excl<uint32_t, SumOp<uint32_t>>(bsum4(v.x) + bsum4(v.y) + bsum4(v.z) + bsum4(v.w), wsum,
+                                          total, SumOp<uint32_t>());
+    if (threadIdx.x == 0)
+        partial[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_flag_scan(const uint4 *__restrict__ in,
+                                                            uint32_t *__restrict__ out,
+                                                            const uint32_t *__restrict__ carry,
+                                                            int inclusive, uint32_t ntiles,
+                                                            uint32_t *total_out)
+{
+    __shared__ uint32_t wsum[4];
+    const size_t i = (size_t)blockIdx.x * kScanThreads + threadIdx.x;
+    const uint4 v = in[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t total;
+    uint32_t run = block_excl<uint32_t, SumOp<uint32_t>>(
+        bsum4(v.x) + bsum4(v.y) + bsum4(v.z) + bsum4(v.w), wsum, total, SumOp<uint32_t>());
+    run += carry ? carry[blockIdx.x] : 0u;
+    uint4 *o = reinterpret_cast<uint4 *>(out) + i * 4;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        uint32_t r[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t e = (w[q] >> (8 * k)) & 0xffu;
+            r[k] = inclusive ? run + e : run;
+            run += e;
+        }
+        o[q] = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+    if (total_out && threadIdx.x == kScanThreads - 1 && blockIdx.x == ntiles - 1)
+        *total_out = run;
+}
+
 template <typename T, typename Op, typename TI = T>
 int scan_impl(const TI *in, T *out, size_t n, bool inclusive, T *total_out, T *tmp,
               size_t tmp_elems, hipStream_t st)
@@ -177,6 +227,23 @@ int scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, bool inclusive,
 int scan_sum_u8(const uint8_t *in, uint32_t *out, size_t n, bool inclusive, uint32_t *total_out,
                 Workspace &ws, hipStream_t st)
 {
+    const size_t tiles = n / kScanTile;
+    if (n % kScanTile == 0 && tiles > 1 && ((uintptr_t)in & 15u) == 0 && ((uintptr_t)out & 15u) == 0 &&
+        ws.scan_tmp_bytes / 4 >= tiles) {
+        uint32_t *partial = (uint32_t *)ws.scan_tmp;
+        hipLaunchKernelGGL(k_flag_reduce, dim3((unsigned)tiles), dim3(kScanThreads), 0, st,
+                           reinterpret_cast<const uint4 *>(in), partial);
+        SALZ_LAUNCH_CHECK();
+        if (scan_impl<uint32_t, SumOp<uint32_t>>(partial, partial, tiles, false, nullptr,
+                                                 partial + tiles, ws.scan_tmp_bytes / 4 - tiles,
+                                                 st) != 0)
+            return -1;
+        hipLaunchKernelGGL(k_flag_scan, dim3((unsigned)tiles), dim3(kScanThreads), 0, st,
+                           reinterpret_cast<const uint4 *>(in), out, (const uint32_t *)partial,
+                           inclusive ? 1 : 0, (uint32_t)tiles, total_out);
+        SALZ_LAUNCH_CHECK();
+        return 0;
+    }
     return scan_impl<uint32_t, SumOp<uint32_t>, uint8_t>(in, out, n, inclusive, total_out,
                                                          (uint32_t *)ws.scan_tmp,
                                                          ws.scan_tmp_bytes / 4, st);
