@@ -504,8 +504,9 @@ int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp)
     unsigned long long *prof = prof_on ? reinterpret_cast<unsigned long long *>(ws.dscal) + 200 : nullptr;
     if (prof)
         SALZ_HIP(hipMemsetAsync(prof, 0, 32, st));
-    // Staging: text ranges of 2^rlog positions (cand windows of 16 << rlog bytes; 64 MB by
-    // default), at most kMaxRanges of them. Slots sp / stage alias scratch that is free here.
+    // Staging: text ranges of 2^rlog positions (cand windows of 16 << rlog bytes; 16 MB by
+    // default: 2^19 and 2^21 measured slower), at most kMaxRanges of them. Slots sp / stage
+    // alias scratch that is free here.
     static const uint32_t rlog_env = [] {
         const char *e = getenv("SALZ_ANSV_RLOG");
         const int v = e ? atoi(e) : 20;
