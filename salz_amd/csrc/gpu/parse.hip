@@ -435,8 +435,12 @@ uint32_t parse_chunk_log(uint32_t n)
         if (k >= 6 && k <= (int)kMaxChunkLog)
             return (uint32_t)k;
     }
+    // At least 2^17 chunks (two waves per SIMD) for blocks under 32 MiB; from 32 MiB, 2^16
+    // suffice for the longest chunks (64 MiB text blocks: 3 passes instead of 4, C4 +7.7%,
+    // while 16 MiB mixed blocks measured slower with longer chunks).
+    const uint32_t min_chunks = n >= (1u << 25) ? (1u << 16) : (1u << 17);
     uint32_t klog = kMaxChunkLog;
-    while (klog > 6 && ((uint64_t)n >> klog) < (1u << 17))
+    while (klog > 6 && ((uint64_t)n >> klog) < min_chunks)
         klog--;
     return klog;
 }
