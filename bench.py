@@ -61,21 +61,67 @@ def parse_args():
                     help="bytes of one block timed on the CPU port (0 = the whole first block)")
     ap.add_argument("--profile-steps", action="store_true",
                     help="per-stage HIP-event timing on every timed step (adds small overhead)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the host-buffer (salz_encode_safe-style) end-to-end timing")
+    ap.add_argument("--cpu-child", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--slots", type=int, default=0,
                     help="concurrent encoder contexts per GPU for the sharded workloads "
                          "(0 = auto: 4; one block per GPU: 1)")
     return ap.parse_args()
 
 
+def cpu_child(spec: str) -> None:
+    """CPU baseline in a process of its own, pinned to one core before it touches anything:
+    the CPU port of the reference (oracle/liboracle.so) on `sample` bytes of the workload's
+    first block. Prints one JSON line; the parent compares the stream hash with the GPU's."""
+    import ctypes
+    import hashlib
+
+    import numpy as np
+
+    kind, total, start, sample, core = spec.split(",")
+    total, start, sample, core = int(total), int(start), int(sample), int(core)
+    os.sched_setaffinity(0, {core})
+    from tests.helpers import gen, oracle, oracle_encode  # CPU port of the reference (baseline + checker)
+
+    src = gen(kind, total, 1, 16 if kind == "smx" else 256)
+    blk = np.ascontiguousarray(src[start:start + sample])
+    c0 = time.perf_counter()
+    rc, ref = oracle_encode(blk)
+    c1 = time.perf_counter()
+    sa_buf = np.empty(max(sample - 8, 1), np.int32)
+    c2 = time.perf_counter()
+    oracle().oracle_suffix_array(blk.ctypes.data, sa_buf.ctypes.data, ctypes.c_int32(max(sample - 8, 0)))
+    c3 = time.perf_counter()
+    print(json.dumps({"rc": rc, "enc_s": c1 - c0, "sa_s": c3 - c2, "core": core,
+                      "affinity": sorted(os.sched_getaffinity(0)),
+                      "sha256": hashlib.sha256(ref).hexdigest() if rc == 0 else None}), flush=True)
+
+
+def start_cpu_child(kind, total, start, sample):
+    """Start the pinned CPU-baseline child before this process makes any GPU call (it runs
+    beside the GPU timing on a core of its own and is collected at the end)."""
+    import subprocess
+
+    cores = sorted(os.sched_getaffinity(0))
+    core = cores[-1]
+    spec = f"{kind},{total},{start},{sample},{core}"
+    return subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-child", spec],
+                            stdout=subprocess.PIPE, text=True), core
+
+
 def main():
     args = parse_args()
+    if args.cpu_child:
+        cpu_child(args.cpu_child)
+        return
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     dist = None
     if world > 1:
         # torch first: libsalz then shares torch's HIP runtime (one runtime per process,
-        # tools/runtime_check.py); only gloo CPU tensors are used.
+        # one HIP runtime per process); only gloo CPU tensors are used.
         import torch.distributed as dist
 
         # gloo prints its mesh-connection notice on fd 1; keep stdout to the one JSON line
@@ -89,6 +135,16 @@ def main():
             os.dup2(saved, 1)
             os.close(saved)
             os.close(null)
+
+    config, kind, total, block = WORKLOADS[args.workload]
+    kind = args.kind or kind
+    total = args.size or total
+    sharded = block is not None
+    child = None
+    if rank == 0 and not args.no_cpu_baseline:
+        first = min(block, total) if sharded else total
+        sample = first if args.cpu_sample <= 0 else min(args.cpu_sample, first)
+        child, _ = start_cpu_child(kind, total, 0, sample)
 
     import salz_amd
     from salz_amd.dist import block_count, my_blocks
@@ -110,10 +166,6 @@ def main():
     SUM = dist.ReduceOp.SUM if dist else None
     MAX = dist.ReduceOp.MAX if dist else None
 
-    config, kind, total, block = WORKLOADS[args.workload]
-    kind = args.kind or kind
-    total = args.size or total
-    sharded = block is not None
     ndev = salz_amd.device_count()
     if ndev == 0:
         raise SystemExit("bench.py: no HIP device visible")
@@ -233,45 +285,63 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(pipe_gbs / HBM_PEAK_GBS, 4),
                          "definition": "A(N) = 66 n + m per block (SURVEY.md §8 d3)"}
 
+    # End to end from host buffers (the salz_encode_safe path: H2D, encode, D2H of the
+    # stream), same blocks and slots; never `value`.
+    e2e = None
+    if not args.no_e2e:
+        host_blocks = [src[s:e] for s, e in spans]
+
+        def run_slot_host(k):
+            return [ctxs[k].encode(host_blocks[j]) for j in range(k, len(spans), nslots)]
+
+        def step_host():
+            if pool is None:
+                return [ctx.encode(b) for b in host_blocks]
+            return list(pool.map(run_slot_host, range(nslots)))
+
+        step_host()
+        barrier()
+        h0 = time.perf_counter()
+        for _ in range(args.steps):
+            step_host()
+        h1 = time.perf_counter()
+        barrier()
+        dth = allreduce([h1 - h0], MAX)[0]
+        e2e = {"value": round(in_bytes * args.steps / dth / 1e6, 3), "unit": "MB/s",
+               "ms_per_step": round(dth / args.steps * 1e3, 3),
+               "what": "host buffers in and out (pageable numpy memory): H2D of each block, "
+                       "encode, D2H of each stream; same blocks and slots as value"}
+
     cpu = None
     parity_full = None
-    if rank == 0 and not args.no_cpu_baseline and spans:
-        import ctypes
+    if child is not None:
+        import hashlib
 
-        import numpy as np
-
-        from tests.helpers import oracle, oracle_encode  # CPU port of the reference (baseline + checker)
-
-        s, e = spans[0]
-        sample = (e - s) if args.cpu_sample <= 0 else min(args.cpu_sample, e - s)
-        c0 = time.perf_counter()
-        rc, ref = oracle_encode(src[s:s + sample])
-        c1 = time.perf_counter()
-        # SA alone (own SA-IS, standing in for libsais) so SA and post-SA time are separate
-        blk = np.ascontiguousarray(src[s:s + sample])
-        sa_buf = np.empty(max(sample - 8, 1), np.int32)
-        c2 = time.perf_counter()
-        oracle().oracle_suffix_array(blk.ctypes.data, sa_buf.ctypes.data, ctypes.c_int32(max(sample - 8, 0)))
-        c3 = time.perf_counter()
+        out_txt, _ = child.communicate(timeout=900)
+        r = json.loads(out_txt.strip().splitlines()[-1])
+        first = spans[0][1] - spans[0][0]
+        sample = first if args.cpu_sample <= 0 else min(args.cpu_sample, first)
         model = ""
         try:
             model = next(ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name"))
         except (OSError, StopIteration):
             pass
         cpu = {
-            "value": round(sample / (c1 - c0) / 1e6, 3),
+            "value": round(sample / r["enc_s"] / 1e6, 3),
             "unit": "MB/s",
             "cores": 1,
             "kind": "port",
             "sample": f"one {sample:,}-byte block of the same {kind} input, oracle/liboracle.so "
-                      f"(clean-room C restatement of lib/salz.c + own SA-IS), 1 thread, "
-                      f"{c1 - c0:.2f} s",
-            "sa_s": round(c3 - c2, 3),
-            "post_sa_s": round((c1 - c0) - (c3 - c2), 3),
+                      f"(clean-room C restatement of lib/salz.c + own SA-IS), 1 thread pinned to "
+                      f"core {r['core']} (sched_setaffinity in a child started before any GPU call), "
+                      f"{r['enc_s']:.2f} s",
+            "pinned_core": r["core"],
+            "sa_s": round(r["sa_s"], 3),
+            "post_sa_s": round(r["enc_s"] - r["sa_s"], 3),
             "cpu_model": model,
         }
-        if sample == e - s:
-            parity_full = bool(rc == 0 and ref == streams[0])
+        if sample == first and r["sha256"] is not None:
+            parity_full = r["sha256"] == hashlib.sha256(streams[0]).hexdigest()
 
     if rank == 0:
         line = {
@@ -298,6 +368,8 @@ def main():
             "roofline": roofline,
             "roofline_pipeline": roofline_pipeline,
             "cpu_baseline": cpu,
+            "value_e2e": e2e["value"] if e2e else None,
+            "e2e": e2e,
             "encoded_bytes": int(out_bytes),
             "ratio": round(in_bytes / out_bytes, 4),
             "roundtrip_ok": bool(roundtrip_ok),

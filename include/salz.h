@@ -13,12 +13,20 @@
  * the reference encoder's. With no usable GPU, salz_encode_safe fails (-1) and reports why
  * on stderr and in salz_gpu_last_error() (salz_gpu.h); there is no silent CPU fallback.
  * Decoding is host C.
+ *
+ * Like the reference (lib/salz.h:16), this header includes common.h, so includers get its
+ * min/divup/roundup/unlikely/unused/get_time_ns. Code that cannot take a function-like `min`
+ * macro (C++ translation units of the library itself) defines SALZ_NO_COMMON_H first.
  */
 #ifndef SALZ_H
 #define SALZ_H
 
 #include <stddef.h>
 #include <stdint.h>
+
+#ifndef SALZ_NO_COMMON_H
+#include "common.h"
+#endif
 
 #ifdef __cplusplus
 extern "C" {

@@ -24,6 +24,10 @@ typedef struct salz_gpu_ctx salz_gpu_ctx;
 /* Number of visible HIP devices; 0 when no GPU is usable. */
 int salz_gpu_device_count(void);
 
+/* log2 of the parse chunk length chosen for a block of block_len bytes (host-only helper;
+ * no device call; SALZ_PARSE_KLOG overrides it for tests). */
+uint32_t salz_gpu_parse_chunk_log(size_t block_len);
+
 /* Message of the last failure on this thread ("" if none). */
 const char *salz_gpu_last_error(void);
 

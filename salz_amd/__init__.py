@@ -55,6 +55,8 @@ lib.vnibble_size.argtypes = [ctypes.c_uint32]
 lib.vnibble_size.restype = _sz
 lib.salz_gpu_device_count.argtypes = []
 lib.salz_gpu_device_count.restype = ctypes.c_int
+lib.salz_gpu_parse_chunk_log.argtypes = [_sz]
+lib.salz_gpu_parse_chunk_log.restype = ctypes.c_uint32
 lib.salz_gpu_last_error.argtypes = []
 lib.salz_gpu_last_error.restype = ctypes.c_char_p
 lib.salz_gpu_malloc.argtypes = [ctypes.c_int, _sz]

@@ -115,7 +115,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n);                 // sa.hip   -
 int stage_lcp(Workspace &ws, uint32_t n, uint32_t *lcp_out);       // lcp.hip  -> lcp[r]
 int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp);  // ansv.hip -> ws.cand
 int stage_parse(Workspace &ws, uint32_t n);                        // parse.hip
-uint32_t parse_chunk_log(uint32_t n);                              // parse.hip: klog for n
+uint32_t parse_chunk_log(size_t N);                                // parse.hip: klog for a block of N bytes
 int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap,
                size_t *out_len);                                   // emit.hip -> dst
 

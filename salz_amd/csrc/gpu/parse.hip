@@ -426,21 +426,22 @@ __global__ __launch_bounds__(kT) void k_cost_rest(const uint8_t *__restrict__ ef
 
 }  // namespace
 
-// Chunk length: the largest K <= 512 that still gives every SIMD of the chip a few waves
-// (parse lanes = chunks); small blocks get short chunks.
-uint32_t parse_chunk_log(uint32_t n)
+// Chunk length from the block length N (bytes; n = N - 8 positions): the largest K <= 512
+// that leaves MORE than 2^17 chunks (two waves per SIMD) for blocks up to 32 MiB, and more
+// than 2^16 for larger blocks, whose longest chunks need fewer passes (64 MiB text blocks: 3
+// passes instead of 4 at K = 512, C4 +7.7%), while 16 MiB mixed blocks measured slower with
+// longer chunks. So: 1 MiB and 16 MiB blocks -> K = 64, 24 MB -> 128, 32 MiB -> 128,
+// 32 MiB + 8 -> 256, 64 MiB / 100 MB / 256 MiB -> 512 (tests/test_abi.py pins these).
+uint32_t parse_chunk_log(size_t N)
 {
     if (const char *e = getenv("SALZ_PARSE_KLOG")) {  // tests: force a chunk length
         int k = atoi(e);
         if (k >= 6 && k <= (int)kMaxChunkLog)
             return (uint32_t)k;
     }
-    // At least 2^17 chunks (two waves per SIMD) for blocks under 32 MiB; from 32 MiB, 2^16
-    // suffice for the longest chunks (64 MiB text blocks: 3 passes instead of 4, C4 +7.7%,
-    // while 16 MiB mixed blocks measured slower with longer chunks).
-    const uint32_t min_chunks = n >= (1u << 25) ? (1u << 16) : (1u << 17);
+    const uint64_t min_chunks = N > (1ull << 25) ? (1ull << 16) : (1ull << 17);
     uint32_t klog = kMaxChunkLog;
-    while (klog > 6 && ((uint64_t)n >> klog) < min_chunks)
+    while (klog > 6 && ((uint64_t)N >> klog) <= min_chunks)
         klog--;
     return klog;
 }

@@ -11,6 +11,7 @@
 // One Workspace per context, reused across calls; a mutex per context keeps the reference
 // API's reentrancy (concurrent callers serialise per device).
 #include "internal.hpp"
+#define SALZ_NO_COMMON_H  // std headers below use min(); the C API does not need common.h here
 #include "../../../include/salz.h"
 #include "../../../include/salz_gpu.h"
 
@@ -357,7 +358,7 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t N
     SALZ_HIP(hipMemcpyAsync(ws.text, src, N, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                             st));
     SALZ_HIP(hipMemsetAsync(ws.text + N, 0, 128, st));
-    ws.klog = parse_chunk_log(n);
+    ws.klog = parse_chunk_log(N);
     if (mark(ws, EV_UP)) return -1;
     if (stage_suffix_array(ws, n) || guard_check(ws, "sa") || check_stage(ws, n, 2)) return -1;
     if (mark(ws, EV_SA)) return -1;
@@ -407,6 +408,8 @@ struct salz_gpu_ctx {
 extern "C" {
 
 const char *salz_gpu_last_error(void) { return g_err; }
+
+uint32_t salz_gpu_parse_chunk_log(size_t block_len) { return parse_chunk_log(block_len); }
 
 int salz_gpu_device_count(void)
 {

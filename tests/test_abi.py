@@ -132,3 +132,20 @@ def test_encode_fails_loudly_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(salz_amd.SalzError, match="no usable HIP device"):
         salz_amd.encode_safe(gen("text", 10000, 1))
+
+
+def test_parse_chunk_log_boundaries(monkeypatch):
+    """Parse chunk length K = 2^klog per block length (parse.hip parse_chunk_log): more than
+    2^17 chunks up to 32 MiB, more than 2^16 above. Pins the boundaries the bench configs sit
+    on (C1/C3: K = 64, C2/C4/C5: K = 512) and the 32 MiB edge."""
+    import salz_amd
+
+    monkeypatch.delenv("SALZ_PARSE_KLOG", raising=False)
+    f = salz_amd.lib.salz_gpu_parse_chunk_log
+    MiB = 1 << 20
+    want = {9: 6, 1 * MiB - 1: 6, 16 * MiB: 6, 16 * MiB + 1: 6, 24_000_000: 7, 32 * MiB: 7,
+            32 * MiB + 8: 8, 40 * MiB: 9, 64 * MiB: 9, 100_000_000: 9, 256 * MiB: 9}
+    for N, k in want.items():
+        assert f(N) == k, (N, f(N), k)
+    monkeypatch.setenv("SALZ_PARSE_KLOG", "8")
+    assert f(16 * MiB) == 8
