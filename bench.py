@@ -8,15 +8,17 @@ A step is one full salz_gpu_encode_device call per block: suffix array, LCP, PSV
 candidates, optimal parse and emission of the bit-exact reference stream into HBM.
 
 Other BASELINE configs (--workload):
-  enwik9   configs[3]: 10^9 bytes of the text surrogate in 64 MiB blocks, blocks sharded
-           round-robin over the ranks (salz_amd/dist.py); a step encodes every block once
+  enwik9   configs[3]: 10^9 bytes of the text surrogate in 64 MiB blocks, contiguous block
+           ranges sharded over the ranks (salz_amd/dist.py); a step encodes every block once
   silesia  configs[2]: 211,957,760 bytes of the mixed surrogate in 16 MiB blocks, sharded
   fib256   configs[4]: the 268,435,456-byte Fibonacci word as one block per GPU
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload enwik8|enwik9|silesia|fib256]
   (N > 1: launched by torch.distributed.run, one rank per GPU; weak scaling for the one-block
-   workloads, strong for the sharded ones. The only exchange is the per-block encoded length,
-   all-reduced over gloo: no data-path collective.)
+   workloads, strong for the sharded ones. A step is encode + the exchange step of
+   salz_amd/dist.py: RCCL all-gather of each rank's packed frame bytes, then every rank's run of
+   frames straight into rank 0's container in HBM over xGMI (point-to-point). No collective
+   touches the encode itself.)
 
 Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel (the suffix sorter's
 radix scatter) by algorithmic bytes / HIP-event-measured launch time on the library's own
@@ -118,23 +120,6 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    dist = None
-    if world > 1:
-        # torch first: libsalz then shares torch's HIP runtime (one runtime per process,
-        # one HIP runtime per process); only gloo CPU tensors are used.
-        import torch.distributed as dist
-
-        # gloo prints its mesh-connection notice on fd 1; keep stdout to the one JSON line
-        sys.stdout.flush()
-        saved, null = os.dup(1), os.open(os.devnull, os.O_WRONLY)
-        os.dup2(null, 1)
-        try:
-            dist.init_process_group("gloo")
-            dist.barrier()
-        finally:
-            os.dup2(saved, 1)
-            os.close(saved)
-            os.close(null)
 
     config, kind, total, block = WORKLOADS[args.workload]
     kind = args.kind or kind
@@ -146,21 +131,44 @@ def main():
         sample = first if args.cpu_sample <= 0 else min(args.cpu_sample, first)
         child, _ = start_cpu_child(kind, total, 0, sample)
 
+    # torch first: libsalz then shares torch's HIP runtime (one runtime per process), and
+    # torch owns the HBM buffers the encoder reads and writes and RCCL moves.
+    import torch
+
+    dist = None
+    cpu_group = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+        # gloo prints its mesh-connection notice on fd 1; keep stdout to the one JSON line
+        sys.stdout.flush()
+        saved, null = os.dup(1), os.open(os.devnull, os.O_WRONLY)
+        os.dup2(null, 1)
+        try:
+            # nccl = RCCL over xGMI for the exchange step (lengths + payload runs, HBM to HBM);
+            # a gloo side group carries the host-side barrier and timing reductions.
+            dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+            cpu_group = dist.new_group(backend="gloo")
+            dist.barrier(group=cpu_group)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+            os.close(null)
+
     import salz_amd
-    from salz_amd.dist import block_count, my_blocks
+    from salz_amd.dist import block_count, gather_container, my_blocks, pack_frames, packed_len
     from tests.helpers import gen  # workload generator (tools/libdatagen.so)
 
     def barrier():
         if dist is not None:
-            dist.barrier()
+            dist.barrier(group=cpu_group)
 
     def allreduce(vals, op):
         if dist is None:
             return vals
-        import torch
-
         t = torch.tensor(vals, dtype=torch.float64)
-        dist.all_reduce(t, op=op)
+        dist.all_reduce(t, op=op, group=cpu_group)
         return t.tolist()
 
     SUM = dist.ReduceOp.SUM if dist else None
@@ -170,6 +178,8 @@ def main():
     if ndev == 0:
         raise SystemExit("bench.py: no HIP device visible")
     device = local % ndev
+    torch.cuda.set_device(device)
+    dev = torch.device("cuda", device)
 
     src = gen(kind, total, 1, 16 if kind == "smx" else 256)
     if sharded:
@@ -180,69 +190,86 @@ def main():
     else:
         nblocks = world
         spans = [(0, total)]
+    block_field = block or total
     max_block = max([e - s for s, e in spans] + [9])
     # Several blocks per GPU: independent encoder contexts (own stream + workspace each) on
     # host threads, so one block's host round trips overlap another block's kernels.
     nslots = args.slots or (1 if not sharded else 4)
-    nslots = max(1, min(nslots, len(spans)))
+    nslots = max(1, min(nslots, max(len(spans), 1)))
     ctxs = [salz_amd.Context(device, max_block) for _ in range(nslots)]
     ctx = ctxs[0]
+    streams_t = [torch.cuda.Stream(device=dev) for _ in range(nslots)]
     cap = salz_amd.encoded_len_max(max_block) + 4096
-    d_src = [salz_amd.DeviceBuffer(e - s, device).upload(src[s:e]) for s, e in spans]
-    d_dst = [salz_amd.DeviceBuffer(cap, device) for _ in spans]
+    d_src = [torch.from_numpy(src[s:e].copy()).to(dev) for s, e in spans]
+    d_dst = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in spans]
+    d_packed = torch.empty(max(packed_len([cap] * len(spans)), 1), dtype=torch.uint8, device=dev)
+    d_container = torch.empty(8 + nblocks * (cap + 4), dtype=torch.uint8, device=dev) if rank == 0 else None
+    torch.cuda.synchronize()
     pool = None
     if nslots > 1:
         from concurrent.futures import ThreadPoolExecutor
 
         pool = ThreadPoolExecutor(nslots)
 
+    def enc(k, j):
+        s, e = spans[j]
+        return ctxs[k].encode_device(d_src[j].data_ptr(), e - s, d_dst[j].data_ptr(), cap,
+                                     streams_t[k].cuda_stream)
+
     def run_slot(k):  # slot k encodes blocks k, k + nslots, ... (ctypes drops the GIL)
-        return [(j, ctxs[k].encode_device(d_src[j].ptr, spans[j][1] - spans[j][0], d_dst[j].ptr, cap))
-                for j in range(k, len(spans), nslots)]
+        return [(j, enc(k, j)) for j in range(k, len(spans), nslots)]
 
     def step():
+        """One step: encode this rank's blocks into HBM, pack their frames, and the exchange
+        step that assembles the whole container in rank 0's HBM (RCCL for N > 1)."""
         if pool is None:
-            return [ctx.encode_device(d.ptr, e - s, o.ptr, cap) for d, o, (s, e) in zip(d_src, d_dst, spans)]
-        out = [0] * len(spans)
-        for part in pool.map(run_slot, range(nslots)):
-            for j, v in part:
-                out[j] = v
-        return out
+            lens = [enc(0, j) for j in range(len(spans))]
+        else:
+            lens = [0] * len(spans)
+            for part in pool.map(run_slot, range(nslots)):
+                for j, v in part:
+                    lens[j] = v
+        nb = pack_frames(d_dst, lens, d_packed)
+        cont = gather_container(d_packed, nb, block_field, rank, world, None, d_container)
+        torch.cuda.synchronize()
+        return lens, cont
 
     # Warmup (untimed), then one instrumented pass for the kernel-level numbers (slot 0 alone,
     # so the HIP-event launch times are not inflated by a concurrent slot).
     for _ in range(args.warmup):
         step()
     ctx.set_timing(True)
-    ctx.encode_device(d_src[-1].ptr, spans[-1][1] - spans[-1][0], d_dst[-1].ptr, cap)
+    enc(0, len(spans) - 1)
     st = ctx.stats()  # stats of the last block of this rank
     ctx.set_timing(bool(args.profile_steps))
-    lens = step()
+    lens, cont = step()
 
     # Timed region: exactly K steps bracketed by barrier + device sync on both sides.
     barrier()
-    salz_amd.synchronize(device)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        lens = step()
-        if sharded and dist is not None:  # the exchange step: per-block lengths -> offsets
-            v = [0.0] * nblocks
-            for b, x in zip(my_blocks(nblocks, rank, world), lens):
-                v[b] = float(x)
-            allreduce(v, SUM)
-    salz_amd.synchronize(device)
+        lens, cont = step()
+    torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
     dt = allreduce([t1 - t0], MAX)[0]
     if args.profile_steps:
         st = ctx.stats()
 
-    streams = [o.download(n) for o, n in zip(d_dst, lens)]
+    streams = [d.narrow(0, 0, n).cpu().numpy().tobytes() for d, n in zip(d_dst, lens)]
     in_bytes, out_bytes = allreduce([float(sum(e - s for s, e in spans)), float(sum(lens))], SUM)
 
-    # Round trip of every local block through the product decoder (frame rule > 16 MiB).
+    # Round trip of every local block through the product decoder (frame rule > 16 MiB), and on
+    # rank 0 the assembled container (every rank's blocks) through the threaded decoder.
     ok = all(salz_amd.decode_safe(s_, e - s, frame=True) == src[s:e].tobytes()
              for s_, (s, e) in zip(streams, spans))
+    container_ok = None
+    if rank == 0:
+        cbytes = cont.cpu().numpy().tobytes()
+        want_len = total * world if not sharded else total
+        back = salz_amd.decode_blocks(cbytes, want_len)
+        container_ok = back == (src.tobytes() * world if not sharded else src.tobytes())
     roundtrip_ok = allreduce([0.0 if ok else 1.0], SUM)[0] == 0
 
     value = in_bytes * args.steps / dt / 1e6
@@ -310,7 +337,7 @@ def main():
         e2e = {"value": round(in_bytes * args.steps / dth / 1e6, 3), "unit": "MB/s",
                "ms_per_step": round(dth / args.steps * 1e3, 3),
                "what": "host buffers in and out (pageable numpy memory): H2D of each block, "
-                       "encode, D2H of each stream; same blocks and slots as value"}
+                       "encode, D2H of each stream; same blocks and slots as value, no exchange"}
 
     cpu = None
     parity_full = None
@@ -360,10 +387,13 @@ def main():
             "config": {
                 "workload": config,
                 "input_bytes_total": int(in_bytes),
-                "block_bytes": block or total,
+                "block_bytes": block_field,
                 "blocks": nblocks,
                 "input": kind,
-                "parallelism": f"independent blocks over {world} GPU(s), {nslots} encoder slot(s) per GPU",
+                "parallelism": f"independent blocks over {world} GPU(s), {nslots} encoder slot(s) per GPU; "
+                               f"step = encode + frame packing + exchange ("
+                               f"{'RCCL all-gather of run lengths + xGMI point-to-point payload runs' if world > 1 else 'local'}"
+                               f") + container assembly in rank 0's HBM",
             },
             "roofline": roofline,
             "roofline_pipeline": roofline_pipeline,
@@ -371,8 +401,10 @@ def main():
             "value_e2e": e2e["value"] if e2e else None,
             "e2e": e2e,
             "encoded_bytes": int(out_bytes),
+            "container_bytes": int(cont.numel()),
             "ratio": round(in_bytes / out_bytes, 4),
             "roundtrip_ok": bool(roundtrip_ok),
+            "container_roundtrip_ok": container_ok,
             "parity_vs_cpu_port": parity_full,
             "stages_ms_last_block": {k: round(st[k], 3) for k in
                                      ("ms_sa", "ms_lcp", "ms_ansv", "ms_parse", "ms_emit", "ms_total")},

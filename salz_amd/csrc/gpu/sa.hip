@@ -30,6 +30,7 @@
 //   k_keys      next round's keys: gid << kb | rank[i + h]
 #include "internal.hpp"
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 
@@ -733,6 +734,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     ws.stats.sa_sorted_elems = 0;
     static const bool verbose = getenv("SALZ_DEBUG_SA") != nullptr;
     const char *mode_env = getenv("SALZ_SA_MODE");  // tests: "global" or "segmented"
+    auto t_round = std::chrono::steady_clock::now();
     for (;;) {
         ws.stats.sa_rounds++;
         ws.stats.sa_sorted_elems += m;
@@ -872,10 +874,13 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         }
         const uint64_t tot = ws.hscal[8], ltot = ws.hscal[9];
         const uint32_t Gnew = (uint32_t)tot, mnew = (uint32_t)(tot >> 32);
-        if (verbose)
+        if (verbose) {  // the round's wall time (this round synchronised with the host twice)
+            const auto now = std::chrono::steady_clock::now();
             fprintf(stderr, "sa round %d (%s) h=%u m=%u (large %u in %u groups) groups=%u -> "
-                    "survivors %u in %u groups\n", ws.stats.sa_rounds, how, h, m, mL, GL, G, mnew,
-                    Gnew);
+                    "survivors %u in %u groups  %.3f ms\n", ws.stats.sa_rounds, how, h, m, mL, GL, G,
+                    mnew, Gnew, std::chrono::duration<double, std::milli>(now - t_round).count());
+            t_round = now;
+        }
         if (mnew == 0)
             break;
         if (h >= n || Gnew == 0) {

@@ -1,18 +1,20 @@
 """Block-sharded container encode over processes, one per GPU.
 
 The reference CLI encodes a file as consecutive independent blocks and frames them as
-"ZLAS" + u32 block size, then u32 length + stream per block (programs/salzcli.c:102-185).
-Blocks share nothing (lib/salz.c:777-823), so the path shards by block:
+"ZLAS" + u32 block size, then u32 length + stream per block (programs/salzcli.c:102-185,
+the loop at :143-179). Blocks share nothing (lib/salz.c:777-823), so the path shards by block:
 
-  1. rank r encodes blocks b with b % world == r on its own GPU (no data-path collective);
-  2. ranks exchange the per-block encoded lengths: an all-reduce of a zero-filled length
-     vector, which is an all-gather for disjoint block sets (the one exchange step);
-  3. every rank derives the container offsets from the lengths (exclusive scan in block
-     order), and rank 0 gathers the payloads and writes them at those offsets.
+  1. rank r encodes a CONTIGUOUS range of blocks on its own GPU (no data-path collective);
+     its frames (u32 length + stream, in block order) are packed into one byte buffer, so in
+     the container they form one contiguous run;
+  2. the one exchange step: an all-gather of each rank's packed byte count, from which every
+     rank knows where its run starts in the container (exclusive scan in rank order);
+  3. rank 0 receives every other rank's run straight into its place in the container
+     (point-to-point, all receives in flight together), after the 8-byte header and its own run.
 
-The exchange runs on a torch.distributed process group (gloo: lengths are a few hundred
-bytes, payloads are at most the input size). `encode_block` is the per-block encoder: the
-GPU path (`gpu_block_encoder`) in production, the CPU oracle in the gloo tests.
+With the nccl backend (RCCL on ROCm) the buffers are HBM tensors: the lengths are all-gathered
+and the payload runs travel GPU to GPU over xGMI, and the container is assembled in rank 0's
+HBM. The same code runs on gloo with CPU tensors (tests/test_dist.py, world 2 and 3).
 """
 from __future__ import annotations
 
@@ -30,7 +32,10 @@ def block_count(src_len: int, block_size: int) -> int:
 
 
 def my_blocks(nblocks: int, rank: int, world: int) -> list[int]:
-    return list(range(rank, nblocks, world))
+    """Rank r's blocks: a contiguous range, sizes differing by at most one across ranks."""
+    base, extra = divmod(nblocks, world)
+    lo = rank * base + min(rank, extra)
+    return list(range(lo, lo + base + (1 if rank < extra else 0)))
 
 
 def container_offsets(lengths: Sequence[int]) -> tuple[np.ndarray, int]:
@@ -40,15 +45,80 @@ def container_offsets(lengths: Sequence[int]) -> tuple[np.ndarray, int]:
     return offs.astype(np.int64), int(8 + frame.sum())
 
 
+def header(block_size: int) -> bytes:
+    return MAGIC.to_bytes(4, "little") + int(block_size).to_bytes(4, "little")
+
+
 def assemble(block_size: int, streams: Sequence[bytes]) -> bytes:
     offs, total = container_offsets([len(s) for s in streams])
     out = bytearray(total)
-    out[0:4] = MAGIC.to_bytes(4, "little")
-    out[4:8] = int(block_size).to_bytes(4, "little")
+    out[0:8] = header(block_size)
     for o, s in zip(offs, streams):
         out[o:o + 4] = len(s).to_bytes(4, "little")
         out[o + 4:o + 4 + len(s)] = s
     return bytes(out)
+
+
+def packed_len(lengths: Sequence[int]) -> int:
+    return int(sum(int(L) + 4 for L in lengths))
+
+
+def pack_frames(streams, lengths: Sequence[int], out):
+    """Write u32 length + stream for each block into the byte tensor `out` (same device as the
+    streams: HBM for the GPU path). Returns the number of bytes written."""
+    import torch
+
+    lens = [int(L) for L in lengths]
+    hdr = torch.tensor(np.frombuffer(np.asarray(lens, dtype="<u4").tobytes(), np.uint8).copy())
+    hdr = hdr.to(out.device, non_blocking=False)
+    o = 0
+    for k, (s, L) in enumerate(zip(streams, lens)):
+        out[o:o + 4].copy_(hdr[4 * k:4 * k + 4])
+        out[o + 4:o + 4 + L].copy_(s[:L])
+        o += 4 + L
+    return o
+
+
+def gather_container(packed, nbytes: int, block_size: int, rank: int = 0, world: int = 1,
+                     group=None, out=None):
+    """The exchange step. `packed` holds this rank's `nbytes` of frames. Returns the container
+    tensor on rank 0 (on packed's device; `out` may supply its storage), None elsewhere."""
+    import torch
+
+    dev = packed.device
+    if world > 1:
+        import torch.distributed as dist
+
+        cnt = torch.tensor([nbytes], dtype=torch.int64, device=dev)
+        allc = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(allc, cnt, group=group)
+        counts = [int(c.item()) for c in allc]
+    else:
+        counts = [nbytes]
+    total = 8 + sum(counts)
+    if rank != 0:
+        import torch.distributed as dist
+
+        if nbytes:
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, packed[:nbytes], 0, group=group)]):
+                req.wait()
+        return None
+    if out is None or out.numel() < total:
+        out = torch.empty(total, dtype=torch.uint8, device=dev)
+    out[:8].copy_(torch.tensor(list(header(block_size)), dtype=torch.uint8).to(dev))
+    out[8:8 + counts[0]].copy_(packed[:counts[0]])
+    if world > 1:
+        import torch.distributed as dist
+
+        ops, off = [], 8 + counts[0]
+        for r in range(1, world):
+            if counts[r]:
+                ops.append(dist.P2POp(dist.irecv, out[off:off + counts[r]], r, group=group))
+            off += counts[r]
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+    return out[:total]
 
 
 def gpu_block_encoder(device: int, max_block: int) -> Callable[[np.ndarray], bytes]:
@@ -61,40 +131,18 @@ def gpu_block_encoder(device: int, max_block: int) -> Callable[[np.ndarray], byt
 
 def encode_container(src: np.ndarray, block_size: int, encode_block: Callable[[np.ndarray], bytes],
                      rank: int = 0, world: int = 1, group=None) -> Optional[bytes]:
-    """Encode src as the reference container with blocks sharded over `world` ranks.
-    Returns the container on rank 0, None elsewhere. Raises on any block failure (the
-    reference CLI aborts the whole file, programs/salzcli.c:156-161)."""
+    """Encode src as the reference container with blocks sharded over `world` ranks (host
+    buffers; gloo or any backend that moves CPU tensors). Returns the container on rank 0,
+    None elsewhere. Raises on any block failure (the reference CLI aborts the whole file,
+    programs/salzcli.c:156-161)."""
     import torch
-    import torch.distributed as dist
 
     nblocks = block_count(len(src), block_size)
     mine = my_blocks(nblocks, rank, world)
-    streams = {b: encode_block(src[b * block_size:(b + 1) * block_size]) for b in mine}
-
-    lengths = torch.zeros(nblocks, dtype=torch.int64)
-    for b, s in streams.items():
-        lengths[b] = len(s)
-    if world > 1:
-        dist.all_reduce(lengths, op=dist.ReduceOp.SUM, group=group)
-    lens = lengths.tolist()
-
-    if world == 1:
-        return assemble(block_size, [streams[b] for b in range(nblocks)])
-    if rank != 0:
-        if mine:
-            payload = torch.from_numpy(np.frombuffer(b"".join(streams[b] for b in mine), np.uint8).copy())
-            dist.send(payload, dst=0, group=group)
-        return None
-    got = dict(streams)
-    for r in range(1, world):
-        theirs = my_blocks(nblocks, r, world)
-        if not theirs:
-            continue
-        buf = torch.empty(sum(lens[b] for b in theirs), dtype=torch.uint8)
-        dist.recv(buf, src=r, group=group)
-        data = buf.numpy().tobytes()
-        o = 0
-        for b in theirs:
-            got[b] = data[o:o + lens[b]]
-            o += lens[b]
-    return assemble(block_size, [got[b] for b in range(nblocks)])
+    streams = [encode_block(src[b * block_size:(b + 1) * block_size]) for b in mine]
+    lens = [len(s) for s in streams]
+    packed = torch.empty(max(packed_len(lens), 1), dtype=torch.uint8)
+    n = pack_frames([torch.frombuffer(bytearray(s), dtype=torch.uint8) if s else torch.empty(0, dtype=torch.uint8)
+                     for s in streams], lens, packed)
+    out = gather_container(packed, n, block_size, rank, world, group)
+    return None if out is None else out.numpy().tobytes()

@@ -63,7 +63,8 @@ def _run(world, kind, size, block):
 
 @pytest.mark.parametrize("world,kind,size,block", [(2, "text", 300_000 + 123, 65536),
                                                    (3, "mixed", 250_000 + 77, 32768),
-                                                   (2, "fib", 40_000, 65536)])
+                                                   (2, "fib", 40_000, 65536),
+                                                   (3, "text", 40_000, 32768)])
 def test_sharded_container_matches_single_process(world, kind, size, block):
     from salz_amd.dist import assemble, block_count
 
