@@ -90,6 +90,21 @@ int salz_gpu_get_stats(const salz_gpu_ctx *ctx, salz_gpu_stats *out);
 int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, uint8_t *dst,
                        size_t *dst_len, int n_devices);
 
+/*
+ * Streaming form of salz_encode_blocks for inputs of any size (the CLI pipeline,
+ * programs/salzcli.c:102-185): blocks are pulled through `rd` (fread-like: returns bytes read,
+ * 0 at end of input, < 0 on error), encoded on the GPUs with reads, transfers, encodes and
+ * writes overlapped, and the container is pushed through `wr` (0 on success) in block order.
+ * Host memory is bounded by a ring of (encoder slots + 2) pinned block buffers. As in the
+ * reference loop, the trailing short (possibly empty) block is always encoded, so inputs whose
+ * size mod block_size is in [0, 8] fail. *in_total / *out_total (may be NULL) receive the
+ * byte counts. Returns 0 / -1.
+ */
+typedef long long (*salz_read_fn)(void *user, uint8_t *buf, size_t cap);
+typedef int (*salz_write_fn)(void *user, const uint8_t *buf, size_t len);
+int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *wr_user,
+                       size_t block_size, int n_devices, uint64_t *in_total, uint64_t *out_total);
+
 /* Upper bound of salz_encode_blocks output for (src_len, block_size). */
 size_t salz_blocks_len_max(size_t src_len, size_t block_size);
 
@@ -105,6 +120,12 @@ int salz_decode_frame(const uint8_t *src, size_t frame_len, uint8_t *dst, size_t
  * (<= 0: one per core). *dst_len: [in] capacity, [out] bytes. Returns 0 / -1. */
 int salz_decode_blocks(const uint8_t *src, size_t src_len, uint8_t *dst, size_t *dst_len,
                        int threads);
+
+/* Streaming container decode (host threads): frames are pulled through `rd`, decoded `threads`
+ * at a time (<= 0: one per core, at most 8; at most 32) and the plain bytes pushed through `wr` in order.
+ * Host memory: threads x (block + encoded_len_max(block)). Returns 0 / -1. */
+int salz_decode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *wr_user, int threads,
+                       uint64_t *in_total, uint64_t *out_total);
 
 #ifdef __cplusplus
 }

@@ -16,8 +16,10 @@
 #include "../../../include/salz_gpu.h"
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -167,10 +169,7 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
     ws.own_stream = true;
     for (hipEvent_t &e : ws.ev)
         SALZ_HIP(hipEventCreate(&e));
-    ws.rx_pool.resize(2048);
-    for (hipEvent_t &e : ws.rx_pool)
-        SALZ_HIP(hipEventCreate(&e));
-    return 0;
+    return 0;  // rx_pool (radix-scatter timing events) is created on the first timed call
 }
 
 __global__ void k_read_scalars(const uint32_t *__restrict__ d, uint32_t *h, uint32_t words)
@@ -353,6 +352,11 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t N
     const uint32_t n = (uint32_t)(N - 8);
     ws.stats = StageStats{};
     ws.rx_used = 0;
+    if (ws.timing && ws.rx_pool.empty()) {
+        ws.rx_pool.resize(2048);
+        for (hipEvent_t &e : ws.rx_pool)
+            SALZ_HIP(hipEventCreate(&e));
+    }
 
     if (mark(ws, EV_START)) return -1;
     SALZ_HIP(hipMemcpyAsync(ws.text, src, N, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
@@ -713,6 +717,201 @@ int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, ui
         o += 4 + L;
     }
     *dst_len = o;
+    return 0;
+}
+
+
+// ---- streaming container encode (the CLI pipeline, programs/salzcli.c:102-185) ------------
+//
+// One reader (this call's thread pool entry), the encoder slots of salz_encode_blocks, and the
+// caller's thread as the in-order writer. A ring of R pinned block buffers (R = slots + 2)
+// bounds host memory to R x (block + encoded_len_max(block)) whatever the input size; reads,
+// H2D/encode/D2H of several blocks and writes overlap. The block loop is the reference's:
+// blocks are read until a short read, and that last (possibly empty) block is encoded too, so
+// inputs with size mod block in [0, 8] fail exactly as the reference CLI does.
+
+namespace {
+struct RingSlot {
+    uint8_t *in = nullptr, *out = nullptr;
+    size_t in_len = 0, out_len = 0;
+    size_t block = 0;    // block index held
+    bool last = false;
+    int state = 0;       // 0 free, 1 read (queued for encode), 2 encoded, 3 failed
+};
+}  // namespace
+
+int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *wr_user,
+                       size_t block_size, int n_devices, uint64_t *in_total, uint64_t *out_total)
+{
+    if (!rd || !wr || block_size == 0 || block_size > 0xffffffffu) {
+        set_error("invalid argument");
+        return -1;
+    }
+    const int avail = salz_gpu_device_count();
+    if (avail <= 0) {
+        set_error("no usable HIP device");
+        return -1;
+    }
+    const int ndev = (n_devices <= 0 || n_devices > avail) ? avail : n_devices;
+    const int per_dev = block_size >= (256u << 20) ? 2 : block_size >= (1u << 20) ? 4 : kMaxSlots;
+    const int W = ndev * per_dev;
+    const size_t R = (size_t)W + 2;
+    const size_t cap = (size_t)salz_encoded_len_max(block_size);
+    std::vector<RingSlot> ring(R);
+    auto free_ring = [&]() {
+        for (RingSlot &r : ring) {
+            if (r.in) (void)hipHostFree(r.in);
+            if (r.out) (void)hipHostFree(r.out);
+        }
+    };
+    for (RingSlot &r : ring) {
+        if (hipHostMalloc(reinterpret_cast<void **>(&r.in), block_size ? block_size : 1) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void **>(&r.out), cap) != hipSuccess) {
+            free_ring();
+            set_error("pinned host buffers for the block ring (%zu x %zu bytes)", R, block_size + cap);
+            return -1;
+        }
+    }
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<size_t> todo;       // ring indices waiting for an encoder, in block order
+    bool stop = false, reader_done = false;
+    std::string err;
+    uint64_t nin = 0, nout = 0;
+
+    auto fail = [&](const std::string &e) {  // with mu held
+        if (err.empty())
+            err = e;
+        stop = true;
+        cv.notify_all();
+    };
+    auto reader = [&]() {
+        size_t b = 0;
+        for (;;) {
+            size_t k;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || ring[b % R].state == 0; });
+                if (stop)
+                    break;
+                k = b % R;
+            }
+            RingSlot &r = ring[k];
+            size_t got = 0;
+            bool eof = false, bad = false;
+            while (got < block_size) {  // fill the block like fread (short only at EOF)
+                const long long n = rd(rd_user, r.in + got, block_size - got);
+                if (n < 0) { bad = true; break; }
+                if (n == 0) { eof = true; break; }
+                got += (size_t)n;
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            if (bad) {
+                fail("read error on the input stream");
+                break;
+            }
+            r.in_len = got;
+            r.block = b;
+            r.last = eof;  // a full block at EOF is followed by the (empty) trailing block
+            r.state = 1;
+            nin += got;
+            todo.push_back(k);
+            cv.notify_all();
+            b++;
+            if (r.last)
+                break;
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        reader_done = true;
+        cv.notify_all();
+    };
+    auto worker = [&](int dev, int slot) {
+        salz_gpu_ctx *c = default_ctx(dev, block_size < 9 ? 9 : block_size, slot);
+        if (!c) {
+            std::lock_guard<std::mutex> lk(mu);
+            fail(g_err);
+            return;
+        }
+        for (;;) {
+            size_t k;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || !todo.empty() || reader_done; });
+                if (stop || (todo.empty() && reader_done))
+                    break;
+                k = todo.front();
+                todo.pop_front();
+            }
+            RingSlot &r = ring[k];
+            size_t out = cap;
+            int rc;
+            {
+                std::lock_guard<std::mutex> lk(c->mu);
+                rc = encode_host_locked(c, r.in, r.in_len, r.out, &out, nullptr);
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            if (rc != 0) {
+                r.state = 3;
+                fail(std::string("block ") + std::to_string(r.block) + ": " + g_err);
+                break;
+            }
+            r.out_len = out;
+            r.state = 2;
+            cv.notify_all();
+        }
+    };
+
+    const uint32_t hdr[2] = {0x53414C5Au, (uint32_t)block_size};
+    int rc = wr(wr_user, reinterpret_cast<const uint8_t *>(hdr), 8) == 0 ? 0 : -1;
+    if (rc != 0) {
+        free_ring();
+        set_error("write error on the output stream");
+        return -1;
+    }
+    nout = 8;
+    std::thread rth(reader);
+    std::vector<std::thread> th;
+    for (int d = 0; d < ndev; d++)
+        for (int k = 0; k < per_dev; k++)
+            th.emplace_back(worker, d, k);
+    // in-order writer
+    for (size_t b = 0;; b++) {
+        RingSlot &r = ring[b % R];
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return stop || (r.state == 2 && r.block == b); });
+            if (stop)
+                break;
+        }
+        const uint32_t L = (uint32_t)r.out_len;
+        const bool last = r.last;
+        if (wr(wr_user, reinterpret_cast<const uint8_t *>(&L), 4) != 0 || wr(wr_user, r.out, r.out_len) != 0) {
+            std::lock_guard<std::mutex> lk(mu);
+            fail("write error on the output stream");
+            break;
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        nout += 4 + r.out_len;
+        r.state = 0;
+        cv.notify_all();
+        if (last) {
+            stop = true;  // done: release the reader (it has already finished) and the workers
+            cv.notify_all();
+            break;
+        }
+    }
+    rth.join();
+    for (auto &t : th)
+        t.join();
+    free_ring();
+    if (!err.empty()) {
+        set_error("%s", err.c_str());
+        return -1;
+    }
+    if (in_total)
+        *in_total = nin;
+    if (out_total)
+        *out_total = nout;
     return 0;
 }
 

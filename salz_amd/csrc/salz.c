@@ -346,3 +346,120 @@ int salz_decode_blocks(const uint8_t *src, size_t src_len, uint8_t *dst, size_t 
         *dst_len = total;
     return rc;
 }
+
+/* ---- streaming container decode ---------------------------------------------------------- */
+
+typedef struct {
+    uint8_t *frame;
+    size_t frame_len;
+    uint8_t *plain;
+    size_t plain_cap, plain_len;
+    int rc;
+} stream_job;
+
+static void *stream_decode_worker(void *arg)
+{
+    stream_job *j = arg;
+    size_t cap = j->plain_cap;
+    j->rc = salz_decode_frame(j->frame, j->frame_len, j->plain, &cap);
+    j->plain_len = cap;
+    return NULL;
+}
+
+static int read_full(salz_read_fn rd, void *user, uint8_t *buf, size_t len, size_t *got)
+{
+    *got = 0;
+    while (*got < len) {
+        long long n = rd(user, buf + *got, len - *got);
+        if (n < 0)
+            return -1;
+        if (n == 0)
+            break;
+        *got += (size_t)n;
+    }
+    return 0;
+}
+
+int salz_decode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *wr_user, int threads,
+                       uint64_t *in_total, uint64_t *out_total)
+{
+    if (!rd || !wr)
+        return -1;
+    uint8_t hdr[8];
+    size_t got;
+    if (read_full(rd, rd_user, hdr, 8, &got) != 0 || got != 8)
+        return -1;
+    uint32_t magic, bs;
+    memcpy(&magic, hdr, 4);
+    memcpy(&bs, hdr + 4, 4);
+    if (magic != 0x53414C5Au || bs == 0) /* programs/salzcli.c:199-207 */
+        return -1;
+    long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
+    /* default: one thread per core, at most 8 (8 x ~2 blocks of buffers bound the memory) */
+    int nt = threads > 0 ? threads : (int)(ncpu > 0 ? (ncpu < 8 ? ncpu : 8) : 1);
+    if (nt > 32)
+        nt = 32;
+    const size_t fcap = (size_t)salz_encoded_len_max(bs);
+    stream_job *jobs = calloc((size_t)nt, sizeof(*jobs));
+    int rc = jobs ? 0 : -1;
+    for (int t = 0; rc == 0 && t < nt; t++) {
+        jobs[t].frame = malloc(fcap);
+        jobs[t].plain = malloc((size_t)bs + 8);
+        jobs[t].plain_cap = bs;
+        if (!jobs[t].frame || !jobs[t].plain)
+            rc = -1;
+    }
+    uint64_t nin = 8, nout = 0;
+    int eof = 0;
+    while (rc == 0 && !eof) {
+        int k = 0;
+        for (; k < nt; k++) { /* up to nt frames: u32 length + stream (programs/salzcli.c:223-264) */
+            uint8_t lb[4];
+            if (read_full(rd, rd_user, lb, 4, &got) != 0) {
+                rc = -1;
+                break;
+            }
+            if (got == 0) {
+                eof = 1;
+                break;
+            }
+            uint32_t L;
+            memcpy(&L, lb, 4);
+            if (got != 4 || L > fcap || read_full(rd, rd_user, jobs[k].frame, L, &got) != 0 || got != L) {
+                rc = -1;
+                break;
+            }
+            jobs[k].frame_len = L;
+            nin += 4 + (uint64_t)L;
+        }
+        if (rc != 0 || k == 0)
+            break;
+        pthread_t th[32];
+        int started[32] = {0};
+        for (int t = 0; t < k; t++)
+            started[t] = pthread_create(&th[t], NULL, stream_decode_worker, &jobs[t]) == 0;
+        for (int t = 0; t < k; t++) {
+            if (started[t])
+                pthread_join(th[t], NULL);
+            else
+                stream_decode_worker(&jobs[t]);
+        }
+        for (int t = 0; t < k && rc == 0; t++) {
+            if (jobs[t].rc != 0 || wr(wr_user, jobs[t].plain, jobs[t].plain_len) != 0)
+                rc = -1;
+            nout += jobs[t].plain_len;
+        }
+    }
+    for (int t = 0; jobs && t < nt; t++) {
+        free(jobs[t].frame);
+        free(jobs[t].plain);
+    }
+    free(jobs);
+    if (rc == 0) {
+        if (in_total)
+            *in_total = nin;
+        if (out_total)
+            *out_total = nout;
+    }
+    return rc;
+}
