@@ -65,6 +65,18 @@ typedef struct {
 int salz_gpu_encode_dump(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, uint8_t *dst,
                          size_t *dst_len, const salz_gpu_dump *dump);
 
+/*
+ * A batch: src_len bytes as consecutive blocks of block_size bytes (the last may be shorter),
+ * all encoded in ONE pass of the pipeline (the suffix array of every block, candidates, parse
+ * and emission run over the whole batch, each block independent and bit-identical to
+ * salz_encode_safe on that block). dst receives the packed frames: per block a u32 LE stream
+ * length then the stream, in block order (the body of the CLI container). *dst_len: [in]
+ * capacity, [out] bytes. Needs block_size % 512 == 0 when there is more than one block, at
+ * most 4096 blocks, and every block longer than 8 bytes. Returns 0 / -1.
+ */
+int salz_gpu_encode_batch(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, size_t block_size,
+                          uint8_t *dst, size_t *dst_len);
+
 typedef struct {
     double ms_upload, ms_sa, ms_lcp, ms_ansv, ms_parse, ms_emit, ms_total;
     int32_t sa_rounds, parse_iters;

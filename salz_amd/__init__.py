@@ -79,6 +79,10 @@ lib.salz_gpu_encode_host.argtypes = [ctypes.c_void_p, _u8p, _sz, _u8p, _szp]
 lib.salz_gpu_encode_host.restype = ctypes.c_int
 lib.salz_gpu_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
 lib.salz_gpu_set_timing.restype = None
+lib.salz_gpu_encode_batch.argtypes = [ctypes.c_void_p, _u8p, _sz, _sz, _u8p, _szp]
+lib.salz_gpu_encode_batch.restype = ctypes.c_int
+lib.salz_debug_init_order.argtypes = [_sz, _sz, ctypes.c_void_p]
+lib.salz_debug_init_order.restype = ctypes.c_int
 lib.salz_encode_blocks.argtypes = [_u8p, _sz, _sz, _u8p, _szp, ctypes.c_int]
 lib.salz_encode_blocks.restype = ctypes.c_int
 lib.salz_blocks_len_max.argtypes = [_sz, _sz]
@@ -94,6 +98,8 @@ class _Dump(ctypes.Structure):
 
 lib.salz_gpu_encode_dump.argtypes = [ctypes.c_void_p, _u8p, _sz, _u8p, _szp, ctypes.POINTER(_Dump)]
 lib.salz_gpu_encode_dump.restype = ctypes.c_int
+lib.salz_debug_encode_batch_dump.argtypes = [ctypes.c_void_p, _u8p, _sz, _sz, _u8p, _szp, ctypes.POINTER(_Dump)]
+lib.salz_debug_encode_batch_dump.restype = ctypes.c_int
 
 
 class Stats(ctypes.Structure):
@@ -255,6 +261,44 @@ class Context:
         if lib.salz_gpu_encode_host(self.handle, _ptr(s), len(s), _ptr(out), ctypes.byref(n)) != 0:
             raise SalzError(f"encode failed: {last_error()}")
         return out[: n.value].tobytes()
+
+    def encode_batch(self, src, block_size: int) -> list[bytes]:
+        """salz_gpu_encode_batch: every block of src in one pipeline pass; the streams."""
+        s = _buf(src)
+        nb = max(1, -(-len(s) // block_size))
+        cap = nb * (encoded_len_max(min(block_size, len(s))) + 8)
+        out = np.empty(max(cap, 1), np.uint8)
+        n = ctypes.c_size_t(cap)
+        if lib.salz_gpu_encode_batch(self.handle, _ptr(s), len(s), block_size, _ptr(out), ctypes.byref(n)) != 0:
+            raise SalzError(f"encode_batch failed: {last_error()}")
+        data, pos, streams = out[: n.value].tobytes(), 0, []
+        while pos < len(data):
+            L = int.from_bytes(data[pos:pos + 4], "little")
+            streams.append(data[pos + 4:pos + 4 + L])
+            pos += 4 + L
+        return streams
+
+    def encode_batch_dump(self, src, block_size: int) -> tuple[list[bytes], dict]:
+        """encode_batch plus the batch's stage arrays (test hook): sa holds global text
+        positions; psv/nsv/lp/ln/dlen/doff/cost are indexed by global position."""
+        s = _buf(src)
+        npos = len(s) - 8
+        arrs = {k: np.zeros(npos + (1 if k == "cost" else 0), np.int32)
+                for k in ("sa", "psv", "nsv", "lp", "ln", "dlen", "doff", "cost")}
+        d = _Dump(**{k: v.ctypes.data for k, v in arrs.items()})
+        nb = max(1, -(-len(s) // block_size))
+        cap = nb * (encoded_len_max(min(block_size, len(s))) + 8)
+        out = np.empty(max(cap, 1), np.uint8)
+        n = ctypes.c_size_t(cap)
+        if lib.salz_debug_encode_batch_dump(self.handle, _ptr(s), len(s), block_size, _ptr(out),
+                                            ctypes.byref(n), ctypes.byref(d)) != 0:
+            raise SalzError(f"encode_batch_dump failed: {last_error()}")
+        data, pos, streams = out[: n.value].tobytes(), 0, []
+        while pos < len(data):
+            L = int.from_bytes(data[pos:pos + 4], "little")
+            streams.append(data[pos + 4:pos + 4 + L])
+            pos += 4 + L
+        return streams, arrs
 
     def encode_device(self, d_src: int, src_len: int, d_dst: int, dst_cap: int,
                       stream: Optional[int] = None) -> int:

@@ -42,25 +42,27 @@ static_assert(kMaxRanges <= kT, "one thread per range");
 
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
+// One half of cand[p]: {p - pos, len}, or {local p + 1, 0} for none (pos == kInf). In a batch
+// the suffix array is the blocks' arrays one after another, so a nearest smaller value found
+// in another block's range means there is none in p's own (every value between lies outside
+// p's range too): it is none as well.
+__device__ __forceinline__ uint2 half(uint32_t p, uint32_t pos, uint32_t len, const Blocks &bl)
+{
+    return pos == kInf || bl.blk(pos) != bl.blk(p) ? make_uint2(p - bl.start(p) + 1u, 0u)
+                                                   : make_uint2(p - pos, len);
+}
+
 // cand is stored in the parse's chunk-interleaved layout (common.hpp, sidx).
 __device__ __forceinline__ void put_psv(uint4 *cand, uint32_t klog, uint32_t p, uint32_t psv_pos,
-                                        uint32_t len)
+                                        uint32_t len, const Blocks &bl)
 {
-    uint2 v = psv_pos == kInf ? make_uint2(p + 1u, 0u) : make_uint2(p - psv_pos, len);
-    reinterpret_cast<uint2 *>(cand)[2 * sidx(p, klog)] = v;
+    reinterpret_cast<uint2 *>(cand)[2 * sidx(p, klog)] = half(p, psv_pos, len, bl);
 }
 
 __device__ __forceinline__ void put_nsv(uint4 *cand, uint32_t klog, uint32_t p, uint32_t nsv_pos,
-                                        uint32_t len)
+                                        uint32_t len, const Blocks &bl)
 {
-    uint2 v = nsv_pos == kInf ? make_uint2(p + 1u, 0u) : make_uint2(p - nsv_pos, len);
-    reinterpret_cast<uint2 *>(cand)[2 * sidx(p, klog) + 1] = v;
-}
-
-// One staged half of cand[p]: {p - pos, len}, or {p + 1, 0} for none (pos == kInf).
-__device__ __forceinline__ uint2 half(uint32_t p, uint32_t pos, uint32_t len)
-{
-    return pos == kInf ? make_uint2(p + 1u, 0u) : make_uint2(p - pos, len);
+    reinterpret_cast<uint2 *>(cand)[2 * sidx(p, klog) + 1] = half(p, nsv_pos, len, bl);
 }
 
 // First queue slot of shard s: the shards' regions hold as many entries as their blocks
@@ -81,7 +83,7 @@ __device__ __forceinline__ uint32_t shard_base(uint32_t s, uint32_t used_blocks,
 __device__ __forceinline__ void block_walk(uint32_t e, uint32_t slot, const uint32_t *vsa,
                                            const uint32_t *vlc, uint32_t b0, uint2 *sh, uint32_t *qp, uint32_t *qp_len,
                                            uint32_t *qn, uint32_t *qn_len, uint32_t *qcount,
-                                           uint32_t qbase)
+                                           uint32_t qbase, const Blocks &bl)
 {
     const uint32_t l = e >> 1, r = b0 + l;
     const uint32_t v = vsa[kB + l];
@@ -111,7 +113,7 @@ __device__ __forceinline__ void block_walk(uint32_t e, uint32_t slot, const uint
             node >>= 1;
         }
         if (hit != kInf)
-            sh[2 * slot] = half(v, vsa[kB + hit], lm);
+            sh[2 * slot] = half(v, vsa[kB + hit], lm, bl);
     } else {
         // NSV: nearest smaller to the right; LCP minimum over (r, r'].
         lm = kInf;
@@ -137,7 +139,7 @@ __device__ __forceinline__ void block_walk(uint32_t e, uint32_t slot, const uint
             node >>= 1;
         }
         if (hit != kInf)
-            sh[2 * slot + 1] = half(v, vsa[kB + hit], lm);
+            sh[2 * slot + 1] = half(v, vsa[kB + hit], lm, bl);
     }
     // global queue: one atomic per wave and side on this block's shard counter
     const bool miss = hit == kInf;
@@ -162,7 +164,7 @@ __device__ __forceinline__ void block_walk(uint32_t e, uint32_t slot, const uint
 }
 
 __global__ __launch_bounds__(kT) void k_ansv_local(
-    const uint32_t *__restrict__ sa, const uint32_t *__restrict__ lcp, uint32_t n, uint32_t np2,
+    const uint32_t *__restrict__ sa, const uint32_t *__restrict__ lcp, uint32_t n, Blocks bl, uint32_t np2,
     uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp, uint4 *__restrict__ stage,
     uint32_t *__restrict__ sp, uint32_t *__restrict__ rfill,
     uint32_t rlog, uint32_t *__restrict__ qp, uint32_t *__restrict__ qp_len,
@@ -280,7 +282,7 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
             wq[slot] = (uint16_t)e;
         else
             block_walk(e, slot_of(e >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len, qcount,
-                       qbase);
+                       qbase, bl);
     };
     if (tid == 0)
         wq_n = 0;
@@ -331,14 +333,15 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
         const uint32_t slot = slot_of(l);
         sp[slot] = v;
         if (hitP != kInf && hitN != kInf) {
-            stage[slot] = make_uint4(v - pvP, lmP, v - pvN, lmN);
+            const uint2 hp = half(v, pvP, lmP, bl), hn = half(v, pvN, lmN, bl);
+            stage[slot] = make_uint4(hp.x, hp.y, hn.x, hn.y);
         } else {
             if (hitP != kInf)
-                sh[2 * slot] = make_uint2(v - pvP, lmP);
+                sh[2 * slot] = half(v, pvP, lmP, bl);
             else
                 enqueue(l << 1);
             if (hitN != kInf)
-                sh[2 * slot + 1] = make_uint2(v - pvN, lmN);
+                sh[2 * slot + 1] = half(v, pvN, lmN, bl);
             else
                 enqueue(l << 1 | 1u);
         }
@@ -353,7 +356,7 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     const uint32_t nw = wq_n < kWQ ? wq_n : kWQ;
     for (uint32_t w = tid; w < nw; w += kT)
         block_walk(wq[w], slot_of(wq[w] >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len,
-                   qcount, qbase);
+                   qcount, qbase, bl);
     if (prof) {
         __syncthreads();
         if (tid == 0) {
@@ -370,9 +373,10 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
 // range, so the workgroups in flight write into one cache-resident window of cand. Halves
 // that went to the global queues are garbage here; k_ansv_global overwrites them afterwards.
 __global__ __launch_bounds__(kT) void k_cand_scatter(const uint32_t *__restrict__ sp,
-                                                     const uint4 *__restrict__ stage, uint32_t n,
+                                                     const uint4 *__restrict__ stage, uint32_t npos,
                                                      uint4 *__restrict__ cand, uint32_t klog,
                                                      uint32_t rlog, uint32_t nranges,
+                                                     const uint32_t *__restrict__ rfill,
                                                      uint32_t *__restrict__ err)
 {
     // XCD-aware: workgroups are dealt round-robin over the 8 XCDs, so workgroup g runs on
@@ -384,12 +388,15 @@ __global__ __launch_bounds__(kT) void k_cand_scatter(const uint32_t *__restrict_
         return;
     // One slot per thread: all three loads are issued under one EXEC mask (DESIGN.md,
     // "Concurrent encodes and the unaligned text load").
-    const size_t i = ((size_t)r << rlog) + (size_t)(k & (tiles - 1u)) * kT + threadIdx.x;
-    if (i >= n)
+    // A range's run holds as many slots as the range has suffixes (all of its positions,
+    // but for a batch's dead ones).
+    const size_t x = (size_t)(k & (tiles - 1u)) * kT + threadIdx.x;
+    if (x >= rfill[r])
         return;
+    const size_t i = ((size_t)r << rlog) + x;
     const uint32_t p = sp[i];
     const uint4 c = stage[i];
-    if (bad_index(p >= n, err, kErrAnsv))
+    if (bad_index(p >= npos, err, kErrAnsv))
         return;
     cand[sidx(p, klog)] = c;
 }
@@ -429,7 +436,7 @@ struct Tree {
 __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
                               const uint32_t *__restrict__ qlen,
                               const uint32_t *__restrict__ qcount, uint32_t used_blocks, int nsv,
-                              uint4 *__restrict__ cand, uint32_t klog)
+                              uint4 *__restrict__ cand, uint32_t klog, Blocks bl)
 {
     const uint32_t x = blockIdx.x * kT + threadIdx.x;
     if (x >= qcount[2u * blockIdx.y + (uint32_t)nsv])
@@ -464,18 +471,25 @@ __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
     }
     uint32_t pos = hit == kInf ? kInf : t.sa[hit];
     if (nsv)
-        put_nsv(cand, klog, v, pos, lm);
+        put_nsv(cand, klog, v, pos, lm, bl);
     else
-        put_psv(cand, klog, v, pos, lm);
+        put_psv(cand, klog, v, pos, lm, bl);
 }
 
-__global__ void k_cand_origin(uint4 *cand) { cand[0] = make_uint4(1u, 1u, 1u, 1u); }  // sidx(0) == 0
+// Every block's first position: no PSV / NSV, lengths 1 (lib/salz.c:547-548).
+__global__ void k_cand_origin(uint4 *cand, Blocks bl, uint32_t klog)
+{
+    const uint32_t b = blockIdx.x * kT + threadIdx.x;
+    if (b < bl.nb)
+        cand[sidx(b * (bl.nb == 1 ? 0u : bl.bs), klog)] = make_uint4(1u, 1u, 1u, 1u);
+}
 
 }  // namespace
 
-int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp)
+int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
 {
     hipStream_t st = ws.stream;
+    const uint32_t n = bl.nsa(), npos = bl.npos;  // suffix array entries, position space
     uint32_t np2 = kB;
     while (np2 < n)
         np2 <<= 1;
@@ -513,7 +527,7 @@ int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp)
         return (uint32_t)(v < 12 ? 12 : v > 30 ? 30 : v);
     }();
     uint32_t rlog = rlog_env;
-    while ((((uint64_t)n - 1) >> rlog) + 1 > kMaxRanges)
+    while ((((uint64_t)npos - 1) >> rlog) + 1 > kMaxRanges)
         rlog++;
     uint32_t *rfill = ws.radix_counts;
     uint32_t *sp = ws.u0;
@@ -524,13 +538,13 @@ int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp)
         return -1;
     }
     SALZ_HIP(hipMemsetAsync(rfill, 0, kMaxRanges * sizeof(uint32_t), st));
-    hipLaunchKernelGGL(k_ansv_local, dim3(used_blocks), dim3(kT), 0, st, ws.sa, lcp, n, np2, tsa,
+    hipLaunchKernelGGL(k_ansv_local, dim3(used_blocks), dim3(kT), 0, st, ws.sa, lcp, n, bl, np2, tsa,
                        tlcp, stage, sp, rfill, rlog, qp, qpl, qn, qnl, cnt, prof);
     SALZ_LAUNCH_CHECK();
-    const uint32_t nranges = (uint32_t)((((uint64_t)n - 1) >> rlog) + 1);
+    const uint32_t nranges = (uint32_t)((((uint64_t)npos - 1) >> rlog) + 1);
     const uint32_t sgrid = 8u * ((nranges + 7u) / 8u) << (rlog - 8);
-    hipLaunchKernelGGL(k_cand_scatter, dim3(sgrid), dim3(kT), 0, st, sp, stage, n, ws.cand,
-                       ws.klog, rlog, nranges, derr);
+    hipLaunchKernelGGL(k_cand_scatter, dim3(sgrid), dim3(kT), 0, st, sp, stage, npos, ws.cand,
+                       ws.klog, rlog, nranges, rfill, derr);
     SALZ_LAUNCH_CHECK();
     if (prof) {
         if (read_scalars(ws, 0, (kQCountWord + 2 * kShards) * sizeof(uint32_t), "ansv.prof") != 0)
@@ -564,15 +578,15 @@ int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp)
     Tree t{tsa, tlcp, ws.sa, lcp, n, np2};
     if (nqp) {
         hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqp, kT), kShards), dim3(kT), 0, st, t,
-                           qp, qpl, cnt, used_blocks, 0, ws.cand, ws.klog);
+                           qp, qpl, cnt, used_blocks, 0, ws.cand, ws.klog, bl);
         SALZ_LAUNCH_CHECK();
     }
     if (nqn) {
         hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqn, kT), kShards), dim3(kT), 0, st, t,
-                           qn, qnl, cnt, used_blocks, 1, ws.cand, ws.klog);
+                           qn, qnl, cnt, used_blocks, 1, ws.cand, ws.klog, bl);
         SALZ_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_cand_origin, dim3(1), dim3(1), 0, st, ws.cand);
+    hipLaunchKernelGGL(k_cand_origin, dim3(grid_for(bl.nb, kT)), dim3(kT), 0, st, ws.cand, bl, ws.klog);
     SALZ_LAUNCH_CHECK();
     return 0;
 }

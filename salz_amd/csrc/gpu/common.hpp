@@ -132,6 +132,52 @@ __host__ __device__ __forceinline__ uint64_t spos(size_t s, uint32_t klog)
     return (((uint64_t)t * 64u + l) << klog) | j;
 }
 
+// ---- batch geometry: several independent blocks encoded by one pipeline pass -------------
+// The batch is the concatenation of nb blocks; block b occupies text positions
+// [b*bs, b*bs + N_b) with N_b = bs for all but the last block. Its suffix text is the first
+// n_b = N_b - 8 bytes (lib/salz.c:197); the 8 bytes after it are "dead" positions: no suffix
+// starts there (they are the block's 8 trailing literals, :743-749), their rank is 0 (end of
+// text) and the parse treats them as cost-0 ends. Suffix order is (block, suffix), so each
+// block's range of the suffix array is that block's own suffix array. npos = end of the last
+// block's suffix text = the position space; nsa = live suffixes = npos - 8 (nb - 1).
+// One block: bs = 0xffffffff, so every position is in block 0 and end() = npos = n.
+struct Blocks {
+    uint32_t bs;    // block stride (bytes)
+    uint32_t nb;    // blocks
+    uint32_t npos;  // (nb - 1) * bs + N_last - 8
+    __host__ __device__ __forceinline__ uint32_t blk(uint32_t p) const { return nb == 1 ? 0u : p / bs; }
+    __host__ __device__ __forceinline__ uint32_t start(uint32_t p) const { return blk(p) * (nb == 1 ? 0u : bs); }
+    // end of p's suffix text (exclusive); p >= end(p) means p is dead
+    __host__ __device__ __forceinline__ uint32_t end(uint32_t p) const
+    {
+        const uint32_t b = blk(p);
+        return b + 1u < nb ? b * bs + bs - 8u : npos;
+    }
+    __host__ __device__ __forceinline__ uint32_t nsa() const { return npos - 8u * (nb - 1u); }
+    __host__ __device__ __forceinline__ uint32_t n_last() const { return npos - (nb - 1u) * (nb == 1 ? 0u : bs); }
+};
+
+// Round 0 of the suffix sorter lists every suffix once, in an order the stable LSD sort turns
+// into "shorter suffix before a longer one it prefixes": first the suffixes with fewer than 8
+// bytes left (length 1 of every block, then length 2, ... 7), then the rest in text order.
+// List entry c -> its suffix. (One block: c < s -> n - 1 - c, else c - s.)
+__host__ __device__ __forceinline__ uint32_t init_suffix(size_t c, const Blocks &g)
+{
+    const uint32_t nl = g.n_last();
+    const uint32_t full = g.nb - 1u;  // blocks with n_b = bs - 8 >= 7
+    uint32_t cc = (uint32_t)c;
+    for (uint32_t len = 1; len <= 7; len++) {
+        const uint32_t cnt = full + (nl >= len ? 1u : 0u);
+        if (cc < cnt)  // block cc's suffix with `len` bytes left
+            return (cc < full ? cc * g.bs + g.bs - 8u : g.npos) - len;
+        cc -= cnt;
+    }
+    const uint32_t per = g.nb == 1 ? 0u : g.bs - 15u;  // long suffixes of a full block
+    if (g.nb > 1 && cc < full * per)
+        return (cc / per) * g.bs + cc % per;
+    return full * (g.nb == 1 ? 0u : g.bs) + (cc - full * per);
+}
+
 // Unaligned little-endian 8-byte load from an 8-byte-aligned, padded byte buffer.
 __device__ __forceinline__ uint64_t load_u64_any(const uint8_t *base, size_t pos)
 {

@@ -13,9 +13,16 @@
 //   3. per chunk, walk again: bytes go straight to their final offsets, bits are assembled
 //      MSB-first into 64-bit words (whole words stored plainly, the <=2 words shared with a
 //      neighbouring chunk merged with atomicOr), and Y_k is recorded for each word start;
-//   4. place every word at 4 + 8k + Y_k; the host writes the 4-byte header. A stream longer
-//      than N + 4 is replaced by the PLAIN form (header + raw copy), as in :755-767.
+//   4. place every word at 4 + 8k + Y_k, then the 4-byte header. A stream longer than N + 4
+//      is replaced by the PLAIN form (header + raw copy), as in :755-767.
+// A batch of blocks (common.hpp, Blocks) emits one stream per block: chunks never straddle two
+// blocks, every block's path starts at its first position, the 8 dead positions after its
+// suffix text are its 8 trailing literals, and (B, Y) restart at each block's first chunk.
+// Block b's words take W[wbase_b ..] (each block word-aligned) and its Y_k are stored offset
+// by the block's first global byte index, so one max-scan serves every block.
 #include "internal.hpp"
+
+#include <vector>
 
 namespace salz {
 namespace {
@@ -58,10 +65,15 @@ __device__ __forceinline__ uint64_t vn_bits(uint32_t v, uint32_t k)
     return r;
 }
 
+// exit of every block's first position (the start of its path)
 __global__ void k_mark_start(const uint32_t *__restrict__ eidx, const uint64_t *__restrict__ pst,
-                             uint32_t klog, uint32_t *__restrict__ emark)
+                             uint32_t klog, uint32_t *__restrict__ emark, Blocks bl)
 {
-    emark[eidx[sidx((uint32_t)pst[0], klog)]] = 1u;  // exit of position 0 (slot sidx(0) == 0)
+    const uint32_t b = blockIdx.x * kT + threadIdx.x;
+    if (b >= bl.nb)
+        return;
+    const uint32_t p0 = b * (bl.nb == 1 ? 0u : bl.bs);
+    emark[eidx[sidx((uint32_t)pst[sidx(p0, klog)], klog)]] = 1u;
 }
 
 __global__ void k_mark_step(const uint32_t *__restrict__ jt, uint32_t *emark, uint32_t ne)
@@ -86,8 +98,11 @@ __global__ void k_entries(const uint32_t *__restrict__ emark, const uint32_t *__
     if (x >= ne || !emark[x])
         return;
     uint32_t q = elist[x];
+    // The smallest marked exit of a chunk is where the path enters it. A batch's path may also
+    // mark the dead position after a block's suffix text inside the block's last chunk (a
+    // factor ending exactly there exits to it): it is the entry only when nothing earlier is.
     if (q < n)
-        entry[q / chunk] = q;
+        atomicMin(&entry[q / chunk], q);
 }
 
 struct Token {
@@ -104,8 +119,25 @@ __device__ __forceinline__ Token token_at(const uint4 *cand, const uint8_t *choi
     return ch == 0 ? Token{1u, 0u} : ch == 1 ? Token{c.y, c.x} : Token{c.w, c.z};
 }
 
+// Path walk range of chunk g: from its entry (a block's first chunk: the block's first
+// position) to its end; a batch's non-last block walks its dead positions as literals, the
+// last block's 8 trailing literals are the virtual chunk nch.
+__device__ __forceinline__ uint32_t walk_start(const uint32_t *entry, uint32_t g, uint32_t chunk,
+                                               const Blocks &bl)
+{
+    const uint32_t a = g * chunk;
+    return a == bl.start(a) ? a : entry[g];
+}
+
+__device__ __forceinline__ uint32_t walk_end(uint32_t g, uint32_t chunk, const Blocks &bl)
+{
+    const uint32_t a = g * chunk;
+    const uint32_t e = bl.blk(a) + 1u < bl.nb ? a + chunk : bl.npos;
+    return (e - a) < chunk ? e : a + chunk;
+}
+
 __global__ void k_emit_count(const uint4 *__restrict__ cand, const uint8_t *__restrict__ choice,
-                             const uint32_t *__restrict__ entry, uint32_t n, uint32_t N,
+                             const uint32_t *__restrict__ entry, Blocks bl, uint32_t N_last,
                              uint32_t chunk, uint32_t nch, uint64_t *__restrict__ cbits,
                              uint64_t *__restrict__ cbytes, uint32_t klog)
 {
@@ -114,14 +146,14 @@ __global__ void k_emit_count(const uint4 *__restrict__ cand, const uint8_t *__re
         return;
     uint64_t bits = 0, bytes = 0;
     if (g == nch) {
-        bits = N - n;
-        bytes = N - n;
+        bits = N_last - bl.n_last();
+        bytes = N_last - bl.n_last();
     } else {
-        uint32_t p = g == 0 ? 0u : entry[g];
+        uint32_t p = walk_start(entry, g, chunk, bl);
         if (p != kNone) {
-            uint32_t b = (n - g * chunk) < chunk ? n : g * chunk + chunk;
+            const uint32_t b = walk_end(g, chunk, bl), e = bl.end(g * chunk);
             while (p < b) {
-                Token t = token_at(cand, choice, p, klog);
+                Token t = p < e ? token_at(cand, choice, p, klog) : Token{1u, 0u};
                 if (t.len == 1) {
                     bits += 1;
                     bytes += 1;
@@ -139,11 +171,12 @@ __global__ void k_emit_count(const uint4 *__restrict__ cand, const uint8_t *__re
 }
 
 struct Sink {
-    uint64_t *W;
-    uint32_t *Yk;
-    uint8_t *out;
-    uint64_t B, B0, B1, Y;
+    uint64_t *W;     // the block's words (W + wbase)
+    uint32_t *Yk;    // the block's Y_k (Yk + wbase), stored + ys
+    uint8_t *out;    // the block's stream
+    uint64_t B, B0, B1, Y;  // block-local
     uint64_t cur, kc;
+    uint32_t ys;     // the block's first global byte index
     bool have;
 
     __device__ __forceinline__ void flush()
@@ -176,7 +209,7 @@ struct Sink {
             uint64_t chunk = (v >> (cnt - take)) & (take == 64 ? ~0ull : ((1ull << take) - 1));
             enter(k);
             if (o == 0)
-                Yk[k] = (uint32_t)Y;
+                Yk[k] = ys + (uint32_t)Y;
             cur |= chunk << (64 - o - take);
             B += take;
             cnt -= take;
@@ -195,18 +228,18 @@ struct Sink {
         const uint64_t take = cnt < (uint64_t)(64 - o) ? cnt : (uint64_t)(64 - o);
         enter(k);
         if (o == 0)
-            Yk[k] = (uint32_t)Y;
+            Yk[k] = ys + (uint32_t)Y;
         B += take;
         cnt -= take;
         if (cnt >= 64) {  // whole words; B is at a word start here
-            Yk[B >> 6] = (uint32_t)Y;  // bytes may have been emitted inside the previous word
+            Yk[B >> 6] = ys + (uint32_t)Y;  // bytes may have been emitted inside the previous word
             B += cnt & ~(uint64_t)63;
             cnt &= 63;
         }
         if (cnt) {
             k = B >> 6;
             enter(k);
-            Yk[k] = (uint32_t)Y;
+            Yk[k] = ys + (uint32_t)Y;
             B += cnt;
         }
     }
@@ -217,38 +250,46 @@ struct Sink {
     }
 };
 
+// Per block: first global bit / byte index, word base in W, stream length.
+struct BlockOut {
+    uint64_t bs, ys, wbase, len;
+};
+
 __global__ void k_emit_write(const uint8_t *__restrict__ T, const uint4 *__restrict__ cand,
                              const uint8_t *__restrict__ choice, const uint32_t *__restrict__ entry,
-                             uint32_t n, uint32_t N, uint32_t chunk, uint32_t nch,
+                             Blocks bl, uint32_t N_last, uint32_t chunk, uint32_t nch,
                              const uint64_t *__restrict__ bst, const uint64_t *__restrict__ yst,
-                             uint64_t btotal, uint64_t *W, uint32_t *Yk, uint8_t *out,
-                             uint32_t klog)
+                             uint64_t btotal, uint64_t *W, uint32_t *Yk, uint8_t *out, size_t stride,
+                             const BlockOut *__restrict__ binfo, uint32_t klog)
 {
     uint32_t g = blockIdx.x * kT + threadIdx.x;
     if (g > nch)
         return;
+    const uint32_t blk = g == nch ? bl.nb - 1u : bl.blk(g * chunk);
+    const BlockOut bo = binfo[blk];
     Sink s;
-    s.W = W;
-    s.Yk = Yk;
-    s.out = out;
-    s.B = s.B0 = bst[g];
-    s.B1 = g == nch ? btotal : bst[g + 1];
-    s.Y = yst[g];
+    s.W = W + bo.wbase;
+    s.Yk = Yk + bo.wbase;
+    s.out = out + (size_t)blk * stride;
+    s.ys = (uint32_t)bo.ys;
+    s.B = s.B0 = bst[g] - bo.bs;
+    s.B1 = (g == nch ? btotal : bst[g + 1]) - bo.bs;
+    s.Y = yst[g] - bo.ys;
     s.cur = 0;
     s.kc = 0;
     s.have = false;
     if (s.B1 == s.B0)
         return;
     if (g == nch) {
-        for (uint32_t i = n; i < N; i++) {
+        for (uint32_t i = bl.npos; i < bl.npos + (N_last - bl.n_last()); i++) {
             s.put(0, 1);
             s.byte(T[i]);
         }
     } else {
-        uint32_t p = g == 0 ? 0u : entry[g];
-        uint32_t b = (n - g * chunk) < chunk ? n : g * chunk + chunk;
+        uint32_t p = walk_start(entry, g, chunk, bl);
+        const uint32_t b = walk_end(g, chunk, bl), e = bl.end(g * chunk);
         while (p < b) {
-            Token t = token_at(cand, choice, p, klog);
+            Token t = p < e ? token_at(cand, choice, p, klog) : Token{1u, 0u};
             if (t.len == 1) {
                 s.put(0, 1);
                 s.byte(T[p]);
@@ -269,35 +310,109 @@ __global__ void k_emit_write(const uint8_t *__restrict__ T, const uint4 *__restr
 }
 
 __global__ void k_place_words(const uint64_t *__restrict__ W, const uint32_t *__restrict__ Yk,
-                              uint64_t nwords, uint8_t *__restrict__ out)
+                              uint64_t nwords, uint8_t *__restrict__ out, size_t stride,
+                              const BlockOut *__restrict__ binfo, uint32_t nb)
 {
     size_t k = (size_t)blockIdx.x * kT + threadIdx.x;
     if (k >= nwords)
         return;
+    uint32_t lo = 0, hi = nb;  // the block owning word k: last with wbase <= k
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (binfo[mid].wbase <= k)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    const BlockOut bo = binfo[lo];
     uint64_t w = W[k];
-    uint8_t *d = out + 4 + 8 * k + Yk[k];
+    uint8_t *d = out + (size_t)lo * stride + 4 + 8 * (k - bo.wbase) + (Yk[k] - (uint32_t)bo.ys);
 #pragma unroll
     for (int i = 0; i < 8; i++)
         d[i] = (uint8_t)(w >> (8 * i));
 }
 
+// Per block: its bit / byte range from the chunk scans, words and stream length
+// 4 + 8 ceil(B / 64) + Y. wcnt gets the word counts for the scan.
+__global__ void k_block_info(Blocks bl, uint32_t chunk, uint32_t nch, const uint64_t *__restrict__ bst,
+                             const uint64_t *__restrict__ yst, const uint64_t *__restrict__ tot,
+                             BlockOut *__restrict__ binfo, uint64_t *__restrict__ wcnt)
+{
+    const uint32_t b = blockIdx.x * kT + threadIdx.x;
+    if (b >= bl.nb)
+        return;
+    const uint32_t c0 = bl.nb == 1 ? 0u : b * (bl.bs / chunk);
+    const bool last = b + 1u == bl.nb;
+    const uint32_t c1 = last ? nch + 1u : (b + 1u) * (bl.bs / chunk);
+    const uint64_t B0 = bst[c0], B1 = last ? tot[0] : bst[c1];
+    const uint64_t Y0 = yst[c0], Y1 = last ? tot[1] : yst[c1];
+    const uint64_t nw = (B1 - B0 + 63) / 64;
+    binfo[b] = BlockOut{B0, Y0, 0, 4 + 8 * nw + (Y1 - Y0)};
+    wcnt[b] = nw;
+}
+
+__global__ void k_block_wbase(BlockOut *__restrict__ binfo, const uint64_t *__restrict__ wpre, uint32_t nb)
+{
+    const uint32_t b = blockIdx.x * kT + threadIdx.x;
+    if (b < nb)
+        binfo[b].wbase = wpre[b];
+}
+
+// Headers (type << 24 | length & 0xffffff, lib/salz.c:760-772) and the PLAIN fallback
+// (lib/salz.c:755-767): one workgroup per block.
+__global__ void k_finalize(const uint8_t *__restrict__ T, Blocks bl, uint32_t N_last,
+                           const BlockOut *__restrict__ binfo, uint8_t *__restrict__ out, size_t stride)
+{
+    const uint32_t b = blockIdx.x;
+    const uint32_t N = b + 1u == bl.nb ? N_last : bl.bs;
+    const uint64_t L = binfo[b].len;
+    uint8_t *o = out + (size_t)b * stride;
+    const bool plain = L > (uint64_t)N + 4;
+    if (plain) {
+        const uint8_t *src = T + (size_t)b * (bl.nb == 1 ? 0u : bl.bs);
+        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x)
+            o[4 + i] = src[i];
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t h = plain ? (N & 0xffffffu) : (1u << 24) | ((uint32_t)(L - 4) & 0xffffffu);
+        o[0] = (uint8_t)h;
+        o[1] = (uint8_t)(h >> 8);
+        o[2] = (uint8_t)(h >> 16);
+        o[3] = (uint8_t)(h >> 24);
+    }
+}
+
 }  // namespace
 
-int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap, size_t *out_len)
+int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, size_t stride,
+               size_t cap, size_t *lens)
 {
     hipStream_t st = ws.stream;
     ParseState &ps = ws.parse;
+    const uint32_t n = bl.npos, nb = bl.nb;
     const uint32_t nch = ps.nchunks, ne = ps.n_exit;
+    if (nb > 1 && bl.bs % ps.chunk != 0) {
+        set_error("emit: batch block size %u is not a multiple of the parse chunk %u", bl.bs, ps.chunk);
+        return -1;
+    }
+    if (nb > kMaxBatchBlocks) {
+        set_error("emit: %u blocks exceed the batch limit %u", nb, kMaxBatchBlocks);
+        return -1;
+    }
     uint32_t *emark = ws.offA, *eidx = ws.offB, *entry = ws.sa;
     uint64_t *cbits = ws.g64, *cbytes = ws.g64 + (nch + 2);
     uint64_t *W = ws.keyA;
     uint32_t *Yk = ws.u2;
-    uint64_t *tot = ws.dscal + 64;  // [0] bits, [1] bytes
+    uint64_t *tot = ws.dscal + 64;  // [0] bits, [1] bytes, [2] words
+    // per-block records after the chunk counts in g64 (free: n + 2 entries, counts use 2 nch + 4)
+    BlockOut *binfo = reinterpret_cast<BlockOut *>(ws.g64 + 2 * ((size_t)nch + 2) + 2);
+    uint64_t *wcnt = reinterpret_cast<uint64_t *>(binfo + nb);
 
     SALZ_HIP(hipMemsetAsync(entry, 0xff, sizeof(uint32_t) * ((size_t)nch + 1), st));
     if (ne) {
         SALZ_HIP(hipMemsetAsync(emark, 0, sizeof(uint32_t) * ne, st));
-        hipLaunchKernelGGL(k_mark_start, dim3(1), dim3(1), 0, st, eidx, ps.pst, ws.klog, emark);
+        hipLaunchKernelGGL(k_mark_start, dim3(grid_for(nb, kT)), dim3(kT), 0, st, eidx, ps.pst, ws.klog,
+                           emark, bl);
         SALZ_LAUNCH_CHECK();
         const uint32_t *lev = ps.jt0;  // parents 2^k steps up (level k)
         uint32_t *pp[2] = {ws.u2, ws.u3};  // recomputed levels when the parse kept only level 0
@@ -320,51 +435,53 @@ int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap, 
         SALZ_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(k_emit_count, dim3(grid_for((size_t)nch + 1, kT)), dim3(kT), 0, st,
-                       ws.cand, ps.choice, entry, n, N, ps.chunk, nch, cbits, cbytes, ws.klog);
+                       ws.cand, ps.choice, entry, bl, N_last, ps.chunk, nch, cbits, cbytes, ws.klog);
     SALZ_LAUNCH_CHECK();
     if (scan_sum_u64(cbits, cbits, (size_t)nch + 1, false, tot + 0, ws, st) != 0)
         return -1;
     if (scan_sum_u64(cbytes, cbytes, (size_t)nch + 1, false, tot + 1, ws, st) != 0)
         return -1;
-    if (read_scalars(ws, 512, 16, "emit.tot") != 0)
+    hipLaunchKernelGGL(k_block_info, dim3(grid_for(nb, kT)), dim3(kT), 0, st, bl, ps.chunk, nch,
+                       cbits, cbytes, tot, binfo, wcnt);
+    SALZ_LAUNCH_CHECK();
+    if (scan_sum_u64(wcnt, wcnt, nb, false, tot + 2, ws, st) != 0)
         return -1;
-    const uint64_t btotal = ws.hscal[64], ytotal = ws.hscal[65];
-    const uint64_t nwords = (btotal + 63) / 64;
-    const uint64_t L = 4 + 8 * nwords + ytotal;
+    hipLaunchKernelGGL(k_block_wbase, dim3(grid_for(nb, kT)), dim3(kT), 0, st, binfo, wcnt, nb);
+    SALZ_LAUNCH_CHECK();
+    // one host round trip: the totals and every block's stream length
+    std::vector<BlockOut> hb(nb);
+    if (read_scalars(ws, 512, 24, "emit.tot") != 0 ||
+        read_device(ws, binfo, sizeof(BlockOut) * nb, hb.data()) != 0)
+        return -1;
+    const uint64_t btotal = ws.hscal[64], ytotal = ws.hscal[65], nwords = ws.hscal[66];
     ws.stats.emit_bits = btotal;
     ws.stats.emit_bytes = ytotal;
-
-    uint32_t *hdr = reinterpret_cast<uint32_t *>(ws.hscal + 100);
-    if (L > cap) {
-        set_error("encoded stream (%llu bytes) exceeds destination capacity (%zu)",
-                  (unsigned long long)L, cap);
-        return -1;  // the reference's writer fails the same way (lib/salz.c:260, :274)
-    }
-    if (L > (uint64_t)N + 4) {  // PLAIN fallback (lib/salz.c:755-767)
-        if ((size_t)N + 4 > cap) {
-            set_error("PLAIN stream exceeds destination capacity");
+    for (uint32_t b = 0; b < nb; b++) {
+        const uint32_t N = b + 1 == nb ? N_last : bl.bs;
+        const uint64_t L = hb[b].len, out = L > (uint64_t)N + 4 ? (uint64_t)N + 4 : L;
+        if (L > cap || out > cap) {  // the reference's writer fails the same way (lib/salz.c:260, :274)
+            set_error("encoded stream (%llu bytes) exceeds destination capacity (%zu)",
+                      (unsigned long long)L, cap);
             return -1;
         }
-        *hdr = (0u << 24) | (N & 0xffffffu);
-        SALZ_HIP(hipMemcpyAsync(dst + 4, ws.text, N, hipMemcpyDeviceToDevice, st));
-        *out_len = (size_t)N + 4;
-    } else {
-        *hdr = (1u << 24) | ((uint32_t)(L - 4) & 0xffffffu);
-        SALZ_HIP(hipMemsetAsync(W, 0, sizeof(uint64_t) * (nwords + 1), st));
-        SALZ_HIP(hipMemsetAsync(Yk, 0, sizeof(uint32_t) * (nwords + 1), st));
-        hipLaunchKernelGGL(k_emit_write, dim3(grid_for((size_t)nch + 1, kT)), dim3(kT), 0, st,
-                           ws.text, ws.cand, ps.choice, entry, n, N, ps.chunk, nch, cbits, cbytes,
-                           btotal, W, Yk, dst, ws.klog);
-        SALZ_LAUNCH_CHECK();
-        // Yk of the words inside zero runs (Sink::zeros): Yk is non-decreasing in k
-        if (scan_max_u32(Yk, Yk, nwords, true, nullptr, ws, st) != 0)
-            return -1;
-        hipLaunchKernelGGL(k_place_words, dim3(grid_for(nwords, kT)), dim3(kT), 0, st, W, Yk,
-                           nwords, dst);
-        SALZ_LAUNCH_CHECK();
-        *out_len = L;
+        lens[b] = (size_t)out;
     }
-    SALZ_HIP(hipMemcpyAsync(dst, hdr, 4, hipMemcpyHostToDevice, st));
+    SALZ_HIP(hipMemsetAsync(W, 0, sizeof(uint64_t) * (nwords + 1), st));
+    SALZ_HIP(hipMemsetAsync(Yk, 0, sizeof(uint32_t) * (nwords + 1), st));
+    hipLaunchKernelGGL(k_emit_write, dim3(grid_for((size_t)nch + 1, kT)), dim3(kT), 0, st,
+                       ws.text, ws.cand, ps.choice, entry, bl, N_last, ps.chunk, nch, cbits, cbytes,
+                       btotal, W, Yk, dst, stride, binfo, ws.klog);
+    SALZ_LAUNCH_CHECK();
+    // Yk of the words inside zero runs (Sink::zeros): Yk is non-decreasing in k
+    if (nwords && scan_max_u32(Yk, Yk, nwords, true, nullptr, ws, st) != 0)
+        return -1;
+    if (nwords) {
+        hipLaunchKernelGGL(k_place_words, dim3(grid_for(nwords, kT)), dim3(kT), 0, st, W, Yk,
+                           nwords, dst, stride, binfo, nb);
+        SALZ_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_finalize, dim3(nb), dim3(kT), 0, st, ws.text, bl, N_last, binfo, dst, stride);
+    SALZ_LAUNCH_CHECK();
     return 0;
 }
 

@@ -70,7 +70,7 @@ struct Workspace {
     void *scan_tmp = nullptr;
     size_t scan_tmp_bytes = 0;
     uint64_t *dscal = nullptr;  // device scalars
-    uint64_t *hscal = nullptr;      // pinned host mirror (mapped)
+    uint64_t *hscal = nullptr;      // pinned host mirror (mapped), kHostScal bytes
     uint64_t *hscal_dev = nullptr;  // its device-side address
     hipStream_t stream = nullptr;
     bool own_stream = false;
@@ -83,10 +83,14 @@ struct Workspace {
     size_t rx_used = 0;
 };
 
+constexpr size_t kHostScal = 64 << 10;  // mapped host buffer: scalars below, read_device above
+
 int workspace_alloc(Workspace &ws, int device, size_t max_block);
 
 // Copy device scalars dscal[off, off + bytes) to hscal (same offset) and wait for them.
 int read_scalars(Workspace &ws, size_t off, size_t bytes, const char *tag);
+// Copy `bytes` of device memory to host memory `dst` through the same mapped buffer.
+int read_device(Workspace &ws, const void *src, size_t bytes, void *dst);
 void workspace_free(Workspace &ws);
 
 // scans (scan.hip)
@@ -104,20 +108,25 @@ int scan_sum_u64(const uint64_t *in, uint64_t *out, size_t n, bool inclusive,
 // radix sort of (u64 key, u32 value) pairs on key bits [bit_lo, bit_hi) (radix.hip).
 // On return *keys / *vals point at whichever buffer holds the sorted result.
 constexpr int kRadixTile = 4096;
-// With `text` set, the first pass builds the round-0 suffix keys from the text itself (m = n
-// suffixes; *keys / *vals are not read).
+// With `text` set, the first pass builds the round-0 suffix keys from the text itself (m =
+// every live suffix of `blocks`; *keys / *vals are not read); a batch of several blocks then
+// gets extra passes on the block of each value, so the result is ordered by (block, key).
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
-                     const uint8_t *text = nullptr);
+                     const uint8_t *text = nullptr, const Blocks *blocks = nullptr);
 
-// stages
-int stage_suffix_array(Workspace &ws, uint32_t n);                 // sa.hip   -> ws.sa
-int stage_lcp(Workspace &ws, uint32_t n, uint32_t *lcp_out);       // lcp.hip  -> lcp[r]
-int stage_candidates(Workspace &ws, uint32_t n, const uint32_t *lcp);  // ansv.hip -> ws.cand
-int stage_parse(Workspace &ws, uint32_t n);                        // parse.hip
-uint32_t parse_chunk_log(size_t N);                                // parse.hip: klog for a block of N bytes
-int stage_emit(Workspace &ws, uint32_t n, uint32_t N, uint8_t *dst, size_t cap,
-               size_t *out_len);                                   // emit.hip -> dst
+// Blocks per batch (one pipeline pass over several blocks, common.hpp Blocks).
+constexpr uint32_t kMaxBatchBlocks = 4096;
+
+// stages; every one takes the batch geometry (one block: Blocks{0xffffffff, 1, n})
+int stage_suffix_array(Workspace &ws, const Blocks &bl);           // sa.hip   -> ws.sa
+int stage_lcp(Workspace &ws, const Blocks &bl, uint32_t *lcp_out); // lcp.hip  -> lcp[r]
+int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp);  // ansv.hip -> ws.cand
+int stage_parse(Workspace &ws, const Blocks &bl);                  // parse.hip
+uint32_t parse_chunk_log(size_t N);                                // parse.hip: klog for N bytes
+// emit.hip: block b's stream at dst + b * stride (at most cap bytes); lens[b] its length
+int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, size_t stride,
+               size_t cap, size_t *lens);
 
 
 }  // namespace salz

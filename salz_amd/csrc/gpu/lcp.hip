@@ -23,36 +23,45 @@ constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kShortBytes = 32;
 constexpr uint32_t kTaskBytes = 512;
 
-__global__ void k_phi(const uint32_t *__restrict__ sa, uint32_t n, uint32_t *__restrict__ phi,
+// A block's first suffix in the suffix array (r = 0, or the previous entry in another block
+// of a batch) has no predecessor: PLCP = 0.
+__global__ void k_phi(const uint32_t *__restrict__ sa, Blocks bl, uint32_t *__restrict__ phi,
                       uint32_t *err)
 {
     size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (r >= n)
+    if (r >= bl.nsa())
         return;
     const uint32_t i = sa[r];
-    if (bad_index(i >= n, err, kErrPhi))
+    if (bad_index(i >= bl.npos, err, kErrPhi))
         return;
-    phi[i] = r ? sa[r - 1] : kNone;
+    const uint32_t j = r ? sa[r - 1] : kNone;
+    phi[i] = j != kNone && bl.blk(j) == bl.blk(i) ? j : kNone;
 }
 
 __global__ void k_plcp_short(const uint8_t *__restrict__ T, const uint32_t *__restrict__ phi,
-                             uint32_t n, uint32_t *__restrict__ plv, uint32_t *__restrict__ queue,
+                             Blocks bl, uint32_t *__restrict__ plv, uint32_t *__restrict__ queue,
                              uint32_t *__restrict__ qcount)
 {
     size_t ii = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (ii >= n)
+    if (ii >= bl.npos)
         return;
-    uint32_t i = (uint32_t)ii, j = phi[i];
-    if (j == kNone) {  // smallest suffix: PLCP = 0
+    uint32_t i = (uint32_t)ii;
+    const uint32_t e = bl.end(i), b0 = bl.start(i);
+    if (i >= e) {  // a batch's dead position: no suffix (the max-scan carries past it)
+        plv[i] = 0;
+        return;
+    }
+    const uint32_t j = phi[i];
+    if (j == kNone) {  // smallest suffix of its block: PLCP = 0
         plv[i] = i;
         return;
     }
-    bool irr = i == 0 || j == 0 || T[i - 1] != T[j - 1];
+    bool irr = i == b0 || j == b0 || T[i - 1] != T[j - 1];  // (j is in i's block)
     if (!irr) {
         plv[i] = 0;
         return;
     }
-    uint32_t limit = n - (i > j ? i : j);
+    uint32_t limit = e - (i > j ? i : j);
     uint32_t L = 0;
     bool done = false;
 #pragma unroll
@@ -82,7 +91,7 @@ __global__ void k_plcp_short(const uint8_t *__restrict__ T, const uint32_t *__re
 
 // One wave per 512-byte task: task t -> item t / nch, bytes [L + (t % nch) * 512, +512).
 __global__ __launch_bounds__(256) void k_plcp_long(const uint8_t *__restrict__ T,
-                                                   const uint32_t *__restrict__ phi, uint32_t n,
+                                                   const uint32_t *__restrict__ phi, Blocks bl,
                                                    const uint32_t *__restrict__ items,
                                                    uint32_t nitems, uint32_t nch, uint32_t L,
                                                    uint32_t *__restrict__ found)
@@ -93,7 +102,7 @@ __global__ __launch_bounds__(256) void k_plcp_long(const uint8_t *__restrict__ T
         return;
     uint32_t item = (uint32_t)(task / nch), ch = (uint32_t)(task % nch);
     uint32_t i = items[item], j = phi[i];
-    uint32_t limit = n - (i > j ? i : j);
+    uint32_t limit = bl.end(i) - (i > j ? i : j);
     uint64_t start = (uint64_t)L + (uint64_t)ch * kTaskBytes + (uint64_t)lane * 8;
     uint32_t mis = kNone;
     if (start < limit) {
@@ -109,7 +118,7 @@ __global__ __launch_bounds__(256) void k_plcp_long(const uint8_t *__restrict__ T
         atomicMin(&found[item], mis);
 }
 
-__global__ void k_plcp_resolve(const uint32_t *__restrict__ phi, uint32_t n,
+__global__ void k_plcp_resolve(const uint32_t *__restrict__ phi, Blocks bl,
                                const uint32_t *__restrict__ items, uint32_t nitems,
                                const uint32_t *__restrict__ found, uint64_t window_end,
                                uint32_t *__restrict__ plv, uint32_t *__restrict__ next_items,
@@ -119,7 +128,7 @@ __global__ void k_plcp_resolve(const uint32_t *__restrict__ phi, uint32_t n,
     if (x >= nitems)
         return;
     uint32_t i = items[x], j = phi[i];
-    uint32_t limit = n - (i > j ? i : j);
+    uint32_t limit = bl.end(i) - (i > j ? i : j);
     uint32_t f = found[x];
     if (f != kNone) {
         plv[i] = f + i;
@@ -132,19 +141,21 @@ __global__ void k_plcp_resolve(const uint32_t *__restrict__ phi, uint32_t n,
 }
 
 __global__ void k_lcp_final(const uint32_t *__restrict__ sa, const uint32_t *__restrict__ mx,
-                            uint32_t n, uint32_t *__restrict__ lcp)
+                            Blocks bl, uint32_t *__restrict__ lcp)
 {
     size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (r >= n)
+    if (r >= bl.nsa())
         return;
-    uint32_t i = sa[r];
-    lcp[r] = r ? mx[i] - i : 0u;
+    const uint32_t i = sa[r], j = r ? sa[r - 1] : i;  // (unconditional loads)
+    // a block's first suffix has no predecessor: LCP 0 (the max-scan may carry a larger value)
+    lcp[r] = r && bl.blk(j) == bl.blk(i) ? mx[i] - i : 0u;
 }
 
 }  // namespace
 
-int stage_lcp(Workspace &ws, uint32_t n, uint32_t *lcp_out)
+int stage_lcp(Workspace &ws, const Blocks &bl, uint32_t *lcp_out)
 {
+    const uint32_t n = bl.npos, nsa = bl.nsa();
     hipStream_t st = ws.stream;
     uint32_t *phi = ws.u0, *plv = ws.u1;
     uint32_t *qa = ws.valA, *qb = ws.valB, *found = ws.offA;
@@ -152,10 +163,10 @@ int stage_lcp(Workspace &ws, uint32_t n, uint32_t *lcp_out)
 
     ws.stats.lcp_long_bytes = 0;
     uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
-    hipLaunchKernelGGL(k_phi, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.sa, n, phi, derr);
+    hipLaunchKernelGGL(k_phi, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.sa, bl, phi, derr);
     SALZ_LAUNCH_CHECK();
     SALZ_HIP(hipMemsetAsync(cnt, 0, 8, st));
-    hipLaunchKernelGGL(k_plcp_short, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, phi, n, plv,
+    hipLaunchKernelGGL(k_plcp_short, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, phi, bl, plv,
                        qa, cnt);
     SALZ_LAUNCH_CHECK();
     if (read_scalars(ws, 0, 256, "lcp.q0") != 0)
@@ -175,10 +186,10 @@ int stage_lcp(Workspace &ws, uint32_t n, uint32_t *lcp_out)
         SALZ_HIP(hipMemsetAsync(cnt + 1, 0, 4, st));
         size_t tasks = (size_t)nitems * nch;
         hipLaunchKernelGGL(k_plcp_long, dim3(grid_for(tasks * 64, 256)), dim3(256), 0, st,
-                           ws.text, phi, n, qa, nitems, nch, (uint32_t)L, found);
+                           ws.text, phi, bl, qa, nitems, nch, (uint32_t)L, found);
         SALZ_LAUNCH_CHECK();
         ws.stats.lcp_long_bytes += tasks * kTaskBytes;
-        hipLaunchKernelGGL(k_plcp_resolve, dim3(grid_for(nitems, kT)), dim3(kT), 0, st, phi, n,
+        hipLaunchKernelGGL(k_plcp_resolve, dim3(grid_for(nitems, kT)), dim3(kT), 0, st, phi, bl,
                            qa, nitems, found, L + W, plv, qb, cnt + 1);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 256, "lcp.q") != 0)
@@ -192,7 +203,7 @@ int stage_lcp(Workspace &ws, uint32_t n, uint32_t *lcp_out)
 
     if (scan_max_u32(plv, plv, n, true, nullptr, ws, st) != 0)
         return -1;
-    hipLaunchKernelGGL(k_lcp_final, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.sa, plv, n,
+    hipLaunchKernelGGL(k_lcp_final, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.sa, plv, bl,
                        lcp_out);
     SALZ_LAUNCH_CHECK();
     return 0;

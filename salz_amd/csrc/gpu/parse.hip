@@ -56,15 +56,17 @@ __device__ __forceinline__ uint32_t factor_bits(uint32_t off, uint32_t len)
 // Storage slots 0..S-1 -> cost seed 3 * (n - p); slots past n unused. Any seed gives the
 // same fixed point (the final pass confirms every decision against exact costs); one near
 // the typical optimum (~3 bits per byte) needs fewer passes on mixed data (tools/parse_sim.c).
-__global__ __launch_bounds__(kT) void k_cost_seed(uint32_t *cost, uint32_t n, uint32_t klog,
+__global__ __launch_bounds__(kT) void k_cost_seed(uint32_t *cost, Blocks bl, uint32_t klog,
                                                   size_t S)
 {
     size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
     if (s >= S)
         return;
     uint64_t p = spos(s, klog);
-    if (p <= n)
-        cost[s] = 3u * (n - (uint32_t)p);
+    if (p <= bl.npos) {  // 3 bits per byte to the block's end; its end / dead positions: 0
+        const uint32_t e = bl.end((uint32_t)p);
+        cost[s] = (uint32_t)p < e ? 3u * (e - (uint32_t)p) : 0u;
+    }
 }
 
 // One lane per chunk, positions b-1 down to a. The states of the last kWin positions
@@ -111,7 +113,7 @@ __device__ __forceinline__ uint64_t far_decode(uint64_t raw, uint32_t q, uint32_
 // their states stay valid through dsum (the uniform cost shift added since their last pass).
 __global__ __launch_bounds__(kT) void k_parse_chunk(
     const uint4 *__restrict__ cand, const uint32_t *__restrict__ cin, uint64_t *__restrict__ pst,
-    const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, uint32_t klog,
+    const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, Blocks bl, uint32_t klog,
     uint32_t *__restrict__ changed, uint32_t *err, uint8_t *__restrict__ eflag,
     const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum)
 {
@@ -123,7 +125,11 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
     if (a64 < n) {
         const uint32_t a = (uint32_t)a64;
         const uint32_t K = 1u << klog;
-        const uint32_t b = (n - a) < K ? n : a + K;
+        // Live positions of the chunk: [a, b). A batch's chunks never straddle two blocks
+        // (blocks are multiples of K); the 8 dead positions after a block's suffix text end
+        // its last chunk and are inert like the steps past n: cost 0, exit n.
+        const uint32_t e = bl.end(a), b0 = bl.start(a);
+        const uint32_t b = (e - a) < K ? e : a + K;
         const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
         auto slot = [&](uint32_t j) { return base + ((size_t)j << 6); };
         if (wdirty && !wdirty[c >> 6]) {  // wave-uniform: a clean wave
@@ -166,9 +172,9 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             const uint4 c0 = cr[0];
             uint32_t best = 9u + (uint32_t)(win[0] >> 32), ex = (uint32_t)win[0];
             uint8_t ch = 0;
-            if (p != 0) {
+            if (p != b0) {  // a block's first position is a literal (lib/salz.c:547-548)
                 if (c0.y >= 3u) {
-                    errw |= live && c0.y > n - p ? kErrParse : 0u;
+                    errw |= live && c0.y > e - p ? kErrParse : 0u;
                     uint64_t t;
                     if (c0.y <= kWin) {
                         t = win[1];
@@ -186,7 +192,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
                     }
                 }
                 if (c0.w >= 3u) {
-                    errw |= live && c0.w > n - p ? kErrParse : 0u;
+                    errw |= live && c0.w > e - p ? kErrParse : 0u;
                     uint64_t t;
                     if (c0.w <= kWin) {
                         t = win[1];
@@ -264,6 +270,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
 __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ cand,
                                                    const uint32_t *__restrict__ cnew,
                                                    const uint32_t *__restrict__ cold, uint32_t n,
+                                                   Blocks bl,
                                                    uint32_t klog, uint8_t *__restrict__ wdirty,
                                                    uint32_t *__restrict__ dsum,
                                                    uint32_t *__restrict__ ndirty)
@@ -276,7 +283,9 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
     uint32_t d0 = 0;
     if (a64 < n) {
         const uint32_t a = (uint32_t)a64, K = 1u << klog;
-        const uint32_t b = (n - a) < K ? n : a + K;
+        // (a block's last chunk ends at its suffix text's end: a cost-0 end, never shifted)
+        const uint32_t e = bl.end(a), b0 = bl.start(a);
+        const uint32_t b = (e - a) < K ? e : a + K;
         const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
         const size_t sb = sidx(b, klog);
         const uint32_t nb = cnew[sb];
@@ -298,7 +307,7 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
 #pragma unroll
             for (uint32_t u = 0; u < 8; u++) {
                 const uint32_t p = a + j0 + u;
-                const bool on = j0 + u < jn && p != 0;
+                const bool on = j0 + u < jn && p != b0;
                 const bool xp = on && cd[u].y >= 3u && p + cd[u].y >= b;
                 const bool xn = on && cd[u].w >= 3u && p + cd[u].w >= b;
                 const size_t sp = sidx(xp ? p + cd[u].y : b, klog), sn = sidx(xn ? p + cd[u].w : b, klog);
@@ -446,8 +455,9 @@ uint32_t parse_chunk_log(size_t N)
     return klog;
 }
 
-int stage_parse(Workspace &ws, uint32_t n)
+int stage_parse(Workspace &ws, const Blocks &bl)
 {
+    const uint32_t n = bl.npos;
     hipStream_t st = ws.stream;
     ParseState &ps = ws.parse;
     const uint32_t klog = ws.klog;
@@ -480,7 +490,7 @@ int stage_parse(Workspace &ws, uint32_t n)
     uint8_t *wdirty = reinterpret_cast<uint8_t *>(dsum + ps.nchunks);
     SALZ_HIP(hipMemsetAsync(dsum, 0, sizeof(uint32_t) * ps.nchunks, st));
 
-    hipLaunchKernelGGL(k_cost_seed, dim3(grid_for(S, kT)), dim3(kT), 0, st, cost[0], n, klog, S);
+    hipLaunchKernelGGL(k_cost_seed, dim3(grid_for(S, kT)), dim3(kT), 0, st, cost[0], bl, klog, S);
     SALZ_LAUNCH_CHECK();
     SALZ_HIP(hipMemsetAsync(choice[0], 0xff, S, st));
 
@@ -507,7 +517,7 @@ int stage_parse(Workspace &ws, uint32_t n)
         if (skipping) {
             SALZ_HIP(hipMemsetAsync(ndirty, 0, 4, st));
             hipLaunchKernelGGL(k_parse_mark, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st,
-                               ws.cand, cin, cout, n, klog, wdirty, dsum, ndirty);
+                               ws.cand, cin, cout, n, bl, klog, wdirty, dsum, ndirty);
             SALZ_LAUNCH_CHECK();
             if (read_scalars(ws, 0, 256, "parse.mark") != 0)
                 return -1;
@@ -526,7 +536,7 @@ int stage_parse(Workspace &ws, uint32_t n)
         if (!skipping)
             SALZ_HIP(hipMemsetAsync(eflag, 0, S, st));
         hipLaunchKernelGGL(k_parse_chunk, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
-                           cin, ws.pst, chold, chnew, n, klog, changed,
+                           cin, ws.pst, chold, chnew, n, bl, klog, changed,
                            reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord, eflag,
                            skipping && skip_on ? wdirty : nullptr, dsum);
         SALZ_LAUNCH_CHECK();

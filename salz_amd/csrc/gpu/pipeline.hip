@@ -107,7 +107,10 @@ void workspace_free(Workspace &ws)
     ws = Workspace{};
 }
 
-static size_t out_bound(size_t N) { return (size_t)salz_encoded_len_max(N) + N / 4 + 4096; }
+// Room for one stream (or a batch's streams at batch_stride apart) with margin: a SALZ stream
+// is at most 12 + 9N/8 bytes before the PLAIN fallback replaces it.
+static size_t batch_stride(size_t bs) { return ((size_t)salz_encoded_len_max(bs) + bs / 4 + 64 + 63) & ~(size_t)63; }
+static size_t out_bound(size_t N) { return (size_t)salz_encoded_len_max(N) + N / 4 + 4096 + 128 * (size_t)kMaxBatchBlocks; }
 
 int workspace_alloc(Workspace &ws, int device, size_t max_block)
 {
@@ -160,7 +163,7 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
     // workspace's stream stores the words there (read_scalars), so no runtime copy path
     // (and none of its staging buffers) is shared between concurrently encoding contexts.
     void *h = nullptr;
-    SALZ_HIP(hipHostMalloc(&h, 4096, hipHostMallocMapped | hipHostMallocCoherent));
+    SALZ_HIP(hipHostMalloc(&h, kHostScal, hipHostMallocMapped | hipHostMallocCoherent));
     ws.hscal = static_cast<uint64_t *>(h);
     void *hd = nullptr;
     SALZ_HIP(hipHostGetDevicePointer(&hd, h, 0));
@@ -176,6 +179,23 @@ __global__ void k_read_scalars(const uint32_t *__restrict__ d, uint32_t *h, uint
 {
     for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
         __hip_atomic_store(&h[i], d[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Arbitrary device memory through the upper half of the mapped buffer, in pieces.
+int read_device(Workspace &ws, const void *src, size_t bytes, void *dst)
+{
+    constexpr size_t kHalf = kHostScal / 2;
+    uint32_t *h = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(ws.hscal_dev) + kHalf);
+    for (size_t o = 0; o < bytes; o += kHalf) {
+        const size_t len = bytes - o < kHalf ? bytes - o : kHalf;
+        hipLaunchKernelGGL(k_read_scalars, dim3(1), dim3(256), 0, ws.stream,
+                           reinterpret_cast<const uint32_t *>(static_cast<const uint8_t *>(src) + o), h,
+                           (uint32_t)((len + 3) / 4));
+        SALZ_LAUNCH_CHECK();
+        SALZ_HIP(hipStreamSynchronize(ws.stream));
+        memcpy(static_cast<uint8_t *>(dst) + o, reinterpret_cast<uint8_t *>(ws.hscal) + kHalf, len);
+    }
+    return 0;
 }
 
 int read_scalars(Workspace &ws, size_t off, size_t bytes, const char *tag)
@@ -335,21 +355,35 @@ static int dump_after_parse(Workspace &ws, uint32_t n, const salz_gpu_dump *d)
     return 0;
 }
 
-// Encode one block. src is host or device memory; the stream goes to device buffer dst.
-static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t N, uint8_t *dst,
-                       size_t cap, size_t *out_len, const salz_gpu_dump *dump)
+// Encode a batch: P bytes of src (host or device memory) as consecutive blocks of bs bytes
+// (bs >= P: one block), every block's stream into device memory at dst + b * stride (at most
+// cap bytes each), lens[b] = its length. A batch of several blocks needs bs to be a multiple
+// of 512 (parse chunks never straddle two blocks) and every block longer than 8 bytes.
+static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P, size_t bs,
+                       uint8_t *dst, size_t stride, size_t cap, size_t *lens, const salz_gpu_dump *dump)
 {
-    if (N <= 8) {
-        set_error("block of %zu bytes: the reference codec needs more than 8 bytes", N);
+    const size_t nbz = bs >= P ? 1 : (P + bs - 1) / bs;
+    const size_t N_last = nbz == 1 ? P : P - (nbz - 1) * bs;
+    if (N_last <= 8) {
+        set_error("block of %zu bytes: the reference codec needs more than 8 bytes", N_last);
         return -1;  // lib/salz.c:197 wraps (N < 8) or crashes (N == 8)
     }
-    if (N > ws.cap_N || N - 8 >= 0x7fffffffu) {
-        set_error("block of %zu bytes exceeds context capacity %zu", N, ws.cap_N);
+    if (P > ws.cap_N || P - 8 >= 0x7fffffffu) {
+        set_error("input of %zu bytes exceeds context capacity %zu", P, ws.cap_N);
         return -1;
     }
+    if (nbz > 1 && bs % 512 != 0) {
+        set_error("batch block size %zu is not a multiple of 512", bs);
+        return -1;
+    }
+    if (nbz > kMaxBatchBlocks) {
+        set_error("%zu blocks exceed the batch limit %u", nbz, kMaxBatchBlocks);
+        return -1;
+    }
+    const Blocks bl{nbz == 1 ? 0xffffffffu : (uint32_t)bs, (uint32_t)nbz, (uint32_t)(P - 8)};
     SALZ_HIP(hipSetDevice(ws.device));
     hipStream_t st = ws.stream;
-    const uint32_t n = (uint32_t)(N - 8);
+    const uint32_t n = bl.npos;
     ws.stats = StageStats{};
     ws.rx_used = 0;
     if (ws.timing && ws.rx_pool.empty()) {
@@ -359,26 +393,32 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t N
     }
 
     if (mark(ws, EV_START)) return -1;
-    SALZ_HIP(hipMemcpyAsync(ws.text, src, N, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+    SALZ_HIP(hipMemcpyAsync(ws.text, src, P, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                             st));
-    SALZ_HIP(hipMemsetAsync(ws.text + N, 0, 128, st));
-    ws.klog = parse_chunk_log(N);
+    SALZ_HIP(hipMemsetAsync(ws.text + P, 0, 128, st));
+    ws.klog = parse_chunk_log(P);
+    if (nbz > 1 && bs % ((size_t)1 << ws.klog) != 0) {
+        set_error("batch block size %zu is not a multiple of the parse chunk", bs);
+        return -1;
+    }
     if (mark(ws, EV_UP)) return -1;
-    if (stage_suffix_array(ws, n) || guard_check(ws, "sa") || check_stage(ws, n, 2)) return -1;
+    if (stage_suffix_array(ws, bl) || guard_check(ws, "sa") || (nbz == 1 && check_stage(ws, n, 2))) return -1;
     if (mark(ws, EV_SA)) return -1;
-    if (dump_after_sa(ws, n, dump)) return -1;
+    if (dump_after_sa(ws, bl.nsa(), dump)) return -1;
     // The suffix sorter usually leaves the LCP array behind (sa.hip, "LCP"); otherwise the
     // Phi / PLCP stage computes it.
     uint32_t *lcp = ws.lcps_ok ? ws.lcps : ws.u3;
-    if ((!ws.lcps_ok && stage_lcp(ws, n, lcp)) || guard_check(ws, "lcp") || check_stage(ws, n, 0, lcp))
+    if ((!ws.lcps_ok && stage_lcp(ws, bl, lcp)) || guard_check(ws, "lcp") ||
+        (nbz == 1 && check_stage(ws, n, 0, lcp)))
         return -1;
     if (mark(ws, EV_LCP)) return -1;
-    if (stage_candidates(ws, n, lcp) || guard_check(ws, "ansv") || check_stage(ws, n, 1)) return -1;
+    if (stage_candidates(ws, bl, lcp) || guard_check(ws, "ansv") || (nbz == 1 && check_stage(ws, n, 1)))
+        return -1;
     if (mark(ws, EV_ANSV)) return -1;
-    if (stage_parse(ws, n) || guard_check(ws, "parse")) return -1;
+    if (stage_parse(ws, bl) || guard_check(ws, "parse")) return -1;
     if (mark(ws, EV_PARSE)) return -1;
     if (dump_after_parse(ws, n, dump)) return -1;
-    if (stage_emit(ws, n, (uint32_t)N, dst, cap, out_len) || guard_check(ws, "emit")) return -1;
+    if (stage_emit(ws, bl, (uint32_t)N_last, dst, stride, cap, lens) || guard_check(ws, "emit")) return -1;
     if (mark(ws, EV_EMIT)) return -1;
     SALZ_HIP(hipStreamSynchronize(st));
     if (ws.timing) {
@@ -400,6 +440,84 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t N
     return 0;
 }
 
+// Frames of a batch, packed: u32 length + stream per block, in block order (the CLI container's
+// body, programs/salzcli.c:163-169). One workgroup per block; foff = exclusive scan of 4 + len.
+__global__ void k_frame_len(const size_t *__restrict__ lens, uint64_t *__restrict__ flen, uint32_t nb)
+{
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    if (b < nb)
+        flen[b] = 4 + (uint64_t)lens[b];
+}
+
+__global__ void k_pack_frames(const uint8_t *__restrict__ regions, size_t stride,
+                              const size_t *__restrict__ lens, const uint64_t *__restrict__ foff,
+                              uint8_t *__restrict__ out)
+{
+    const uint32_t b = blockIdx.x;
+    const uint32_t L = (uint32_t)lens[b];
+    uint8_t *o = out + foff[b];
+    const uint8_t *src = regions + (size_t)b * stride;
+    if (threadIdx.x < 4)
+        o[threadIdx.x] = (uint8_t)(L >> (8 * threadIdx.x));
+    for (uint32_t i = threadIdx.x; i < L; i += blockDim.x)
+        o[4 + i] = src[i];
+}
+
+// A batch from host memory: every block encoded in one pipeline pass, the packed frames copied
+// to host memory dst (capacity *dst_len; set to the bytes written).
+static int encode_batch_locked(Workspace &ws, const uint8_t *src, size_t P, size_t bs, uint8_t *dst,
+                               size_t *dst_len, const salz_gpu_dump *dump = nullptr)
+{
+    const size_t nb = bs >= P ? 1 : (P + bs - 1) / bs;
+    const size_t stride = batch_stride(bs < P ? bs : P);
+    if (P > ws.cap_N || nb * stride > ws.out_cap) {
+        if (workspace_alloc(ws, ws.device, P > ws.cap_N ? P : ws.cap_N) != 0)
+            return -1;
+    }
+    // Every block gets the reference CLI's output capacity, salz_encoded_len_max(block size)
+    // (programs/salzcli.c:130, :156), so a block the reference fails on (an incompressible
+    // block whose SALZ stream runs a few bytes past that bound before the PLAIN fallback)
+    // fails here too.
+    const size_t cap = (size_t)salz_encoded_len_max(bs);
+    std::vector<size_t> lens(nb);
+    if (encode_core(ws, src, false, P, bs, ws.out, stride, cap < stride ? cap : stride, lens.data(), dump) != 0)
+        return -1;
+    size_t total = 0;
+    for (size_t L : lens)
+        total += 4 + L;
+    if (total > *dst_len) {
+        set_error("batch frames (%zu bytes) exceed the destination capacity (%zu)", total, *dst_len);
+        return -1;
+    }
+    // lens to the device through the scalar area (plain host -> device copy)
+    size_t *dlens = reinterpret_cast<size_t *>(ws.lrec);  // free after the suffix sort
+    uint64_t *foff = reinterpret_cast<uint64_t *>(ws.lrec) + nb;
+    if (2 * nb + 2 > ws.cap_n / 1024 + 2) {
+        set_error("batch of %zu blocks: no room for the frame table", nb);
+        return -1;
+    }
+    SALZ_HIP(hipMemcpyAsync(dlens, lens.data(), sizeof(size_t) * nb, hipMemcpyHostToDevice, ws.stream));
+    hipLaunchKernelGGL(k_frame_len, dim3(grid_for(nb, 256)), dim3(256), 0, ws.stream, dlens, foff, (uint32_t)nb);
+    SALZ_LAUNCH_CHECK();
+    if (scan_sum_u64(foff, foff, nb, false, nullptr, ws, ws.stream) != 0)
+        return -1;
+    uint8_t *packed = reinterpret_cast<uint8_t *>(ws.keyB);  // free after emission
+    hipLaunchKernelGGL(k_pack_frames, dim3((unsigned)nb), dim3(256), 0, ws.stream, ws.out, stride, dlens,
+                       foff, packed);
+    SALZ_LAUNCH_CHECK();
+    SALZ_HIP(hipMemcpyAsync(dst, packed, total, hipMemcpyDeviceToHost, ws.stream));
+    SALZ_HIP(hipStreamSynchronize(ws.stream));
+    *dst_len = total;
+    return 0;
+}
+
+// One block (the reference's unit): the stream to device buffer dst (capacity cap).
+static int encode_one(Workspace &ws, const uint8_t *src, bool src_dev, size_t N, uint8_t *dst,
+                      size_t cap, size_t *out_len, const salz_gpu_dump *dump)
+{
+    return encode_core(ws, src, src_dev, N, N, dst, 0, cap, out_len, dump);
+}
+
 }  // namespace salz
 
 using namespace salz;
@@ -414,6 +532,19 @@ extern "C" {
 const char *salz_gpu_last_error(void) { return g_err; }
 
 uint32_t salz_gpu_parse_chunk_log(size_t block_len) { return parse_chunk_log(block_len); }
+
+// Test hook (host only): the round-0 list order of a batch (common.hpp init_suffix), so the
+// CPU tests can check it enumerates every live suffix once, shortest-first per block.
+int salz_debug_init_order(size_t src_len, size_t block_size, uint32_t *out)
+{
+    if (!out || src_len <= 8)
+        return -1;
+    const size_t nb = block_size >= src_len ? 1 : (src_len + block_size - 1) / block_size;
+    const Blocks bl{nb == 1 ? 0xffffffffu : (uint32_t)block_size, (uint32_t)nb, (uint32_t)(src_len - 8)};
+    for (uint32_t c = 0; c < bl.nsa(); c++)
+        out[c] = init_suffix(c, bl);
+    return (int)bl.nsa();
+}
 
 int salz_gpu_device_count(void)
 {
@@ -526,7 +657,7 @@ int salz_gpu_encode_device(salz_gpu_ctx *ctx, const uint8_t *d_src, size_t src_l
     if (stream)
         ws.stream = static_cast<hipStream_t>(stream);
     size_t len = 0;
-    int rc = encode_core(ws, d_src, true, src_len, d_dst, dst_cap, &len, nullptr);
+    int rc = encode_one(ws, d_src, true, src_len, d_dst, dst_cap, &len, nullptr);
     ws.stream = saved;
     if (rc == 0)
         *dst_len = len;
@@ -544,7 +675,7 @@ static int encode_host_locked(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_
     }
     size_t cap = *dst_len < ws.out_cap ? *dst_len : ws.out_cap;
     size_t len = 0;
-    if (encode_core(ws, src, false, src_len, ws.out, cap, &len, dump) != 0)
+    if (encode_one(ws, src, false, src_len, ws.out, cap, &len, dump) != 0)
         return -1;
     if (hipMemcpy(dst, ws.out, len, hipMemcpyDeviceToHost) != hipSuccess) {
         set_error("D2H copy of the encoded stream failed");
@@ -574,6 +705,44 @@ int salz_gpu_encode_dump(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, 
     }
     std::lock_guard<std::mutex> lk(ctx->mu);
     return encode_host_locked(ctx, src, src_len, dst, dst_len, dump);
+}
+
+int salz_gpu_encode_batch(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, size_t block_size,
+                          uint8_t *dst, size_t *dst_len)
+{
+    if (!ctx || !src || !dst || !dst_len || block_size == 0) {
+        set_error("invalid argument");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return encode_batch_locked(ctx->ws, src, src_len, block_size, dst, dst_len);
+}
+
+// Test hook: read workspace scratch left by the last encode (0: ws.sa = emission's chunk
+// entries, 1: ws.g64 = emission's chunk bit / byte starts), `count` u32 / u64 words from `off`.
+int salz_debug_ws_read(salz_gpu_ctx *ctx, int which, size_t off, size_t count, void *out)
+{
+    if (!ctx || !out)
+        return -1;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    Workspace &ws = ctx->ws;
+    if (which == 0)
+        return read_device(ws, ws.sa + off, count * 4, out);
+    return read_device(ws, ws.g64 + off, count * 8, out);
+}
+
+// Test hook: salz_gpu_encode_batch with the stage arrays of the whole batch (suffix array of
+// nsa entries in global text positions; the per-position arrays over the position space).
+int salz_debug_encode_batch_dump(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len,
+                                 size_t block_size, uint8_t *dst, size_t *dst_len,
+                                 const salz_gpu_dump *dump)
+{
+    if (!ctx || !src || !dst || !dst_len || block_size == 0) {
+        set_error("invalid argument");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return encode_batch_locked(ctx->ws, src, src_len, block_size, dst, dst_len, dump);
 }
 
 // ---- default contexts behind salz_encode_safe ----------------------------------------------
@@ -625,6 +794,40 @@ size_t salz_blocks_len_max(size_t src_len, size_t block_size)
     return 8 + blocks * 4 + (size_t)salz_encoded_len_max(block_size) * blocks;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Batching plan of the container encoders: blocks whose size is a multiple of 512 are encoded
+// kBatchBytes at a time (one pipeline pass per batch, salz_gpu_encode_batch), with 2 batches in
+// flight per device; other block sizes go one block per pass with the slot counts below.
+struct BatchPlan {
+    size_t bpb;   // blocks per batch
+    int per_dev;  // encoder contexts (slots) per device
+};
+
+BatchPlan batch_plan(size_t block_size)
+{
+    const char *e = getenv("SALZ_BATCH_BYTES");  // tuning / tests
+    const long long v = e ? atoll(e) : 0;
+    const size_t kBatchBytes = v > 0 ? (size_t)v : (size_t)64 << 20;
+    if (block_size % 512 == 0) {
+        size_t bpb = kBatchBytes / block_size;
+        bpb = bpb < 1 ? 1 : bpb > kMaxBatchBlocks ? kMaxBatchBlocks : bpb;
+        return {bpb, block_size >= (256u << 20) ? 1 : 2};
+    }
+    return {1, block_size >= (256u << 20) ? 2 : block_size >= (1u << 20) ? 4 : kMaxSlots};
+}
+
+size_t frames_cap(size_t bpb, size_t block_size)
+{
+    return bpb * ((size_t)salz_encoded_len_max(block_size) + 4);
+}
+
+}  // namespace
+
+extern "C" {
+
 int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, uint8_t *dst,
                        size_t *dst_len, int n_devices)
 {
@@ -638,24 +841,27 @@ int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, ui
         return -1;
     }
     int ndev = (n_devices <= 0 || n_devices > avail) ? avail : n_devices;
-    // Blocks in flight per device: small blocks are dominated by per-block launch and
-    // host-sync latency, so several streams (one context each) overlap them on one GPU.
     // Block count follows the reference CLI loop (programs/salzcli.c:143-179): it always
     // encodes the trailing fread() chunk, even an empty one when src_len is a multiple.
-    size_t nblocks = src_len / block_size + 1;
-    // (4 slots: +38% on 16 MiB blocks, +21% on 64 MiB blocks, profiles/r01r_*; a 64 MiB
-    // workspace is ~6 GB, so 4 of them fit easily in 288 GB.)
-    int per_dev = block_size >= (256u << 20) ? 2 : block_size >= (1u << 20) ? 4 : kMaxSlots;
-    const size_t per_dev_blocks = (nblocks + ndev - 1) / ndev;
-    if ((size_t)per_dev > per_dev_blocks)
-        per_dev = (int)per_dev_blocks;
-    std::vector<std::vector<uint8_t>> streams(nblocks);
-    std::vector<int> rcs(nblocks, -1);
+    const size_t nblocks = src_len / block_size + 1;
+    if (src_len % block_size == 0) {  // the trailing block is empty: lib/salz.c:197 fails it
+        set_error("block %zu: a block of 0 bytes (the input is a multiple of the block size)", nblocks - 1);
+        return -1;
+    }
+    const BatchPlan plan = batch_plan(block_size);
+    const size_t nbatches = (nblocks + plan.bpb - 1) / plan.bpb;
+    int per_dev = plan.per_dev;
+    const size_t per_dev_batches = (nbatches + ndev - 1) / ndev;
+    if ((size_t)per_dev > per_dev_batches)
+        per_dev = (int)per_dev_batches;
+    std::vector<std::vector<uint8_t>> frames(nbatches);
+    std::vector<int> rcs(nbatches, -1);
     std::atomic<size_t> next{0};
     std::vector<std::string> werr((size_t)ndev * per_dev);
     auto worker = [&](int dev, int slot) {
-        // cached contexts (workspace reused across calls), one per block in flight
-        size_t need = block_size < src_len ? block_size : src_len;
+        // cached contexts (workspace reused across calls), one per batch in flight
+        const size_t span = plan.bpb * block_size;
+        size_t need = span < src_len ? span : src_len;
         salz_gpu_ctx *c = default_ctx(dev, need < 9 ? 9 : need, slot);
         std::string &err = werr[(size_t)dev * per_dev + slot];
         if (!c) {
@@ -663,24 +869,24 @@ int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, ui
             return;
         }
         for (;;) {
-            size_t b = next.fetch_add(1);
-            if (b >= nblocks)
+            size_t t = next.fetch_add(1);
+            if (t >= nbatches)
                 break;
-            size_t off = b * block_size;
-            size_t len = off + block_size <= src_len ? block_size : src_len - off;
-            size_t cap = (size_t)salz_encoded_len_max(block_size);
-            streams[b].resize(cap);
-            size_t out = cap;
+            const size_t b0 = t * plan.bpb, b1 = b0 + plan.bpb < nblocks ? b0 + plan.bpb : nblocks;
+            const size_t off = b0 * block_size;
+            const size_t len = (b1 == nblocks ? src_len : b1 * block_size) - off;
+            size_t out = frames_cap(b1 - b0, block_size);
+            frames[t].resize(out);
             {
                 std::lock_guard<std::mutex> lk(c->mu);
-                rcs[b] = encode_host_locked(c, src + off, len, streams[b].data(), &out, nullptr);
+                rcs[t] = encode_batch_locked(c->ws, src + off, len, block_size, frames[t].data(), &out);
             }
-            if (rcs[b] != 0) {
+            if (rcs[t] != 0) {
                 err = g_err;
-                next.store(nblocks);
+                next.store(nbatches);
                 break;
             }
-            streams[b].resize(out);
+            frames[t].resize(out);
         }
     };
     std::vector<std::thread> th;
@@ -690,16 +896,16 @@ int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, ui
     for (auto &t : th)
         t.join();
     size_t need = 8;
-    for (size_t b = 0; b < nblocks; b++) {
-        if (rcs[b] != 0) {
+    for (size_t t = 0; t < nbatches; t++) {
+        if (rcs[t] != 0) {
             std::string e;
-            for (auto &s : werr)
-                if (!s.empty())
-                    e = s;
-            set_error("block %zu failed: %s", b, e.c_str());
+            for (auto &s_ : werr)
+                if (!s_.empty())
+                    e = s_;
+            set_error("batch %zu (blocks %zu..) failed: %s", t, t * plan.bpb, e.c_str());
             return -1;
         }
-        need += 4 + streams[b].size();
+        need += frames[t].size();
     }
     if (need > *dst_len) {
         set_error("container exceeds destination capacity");
@@ -710,31 +916,28 @@ int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, ui
     memcpy(dst + o, &magic, 4);
     memcpy(dst + o + 4, &bs, 4);
     o += 8;
-    for (size_t b = 0; b < nblocks; b++) {
-        uint32_t L = (uint32_t)streams[b].size();
-        memcpy(dst + o, &L, 4);
-        memcpy(dst + o + 4, streams[b].data(), L);
-        o += 4 + L;
+    for (size_t t = 0; t < nbatches; t++) {
+        memcpy(dst + o, frames[t].data(), frames[t].size());
+        o += frames[t].size();
     }
     *dst_len = o;
     return 0;
 }
 
-
 // ---- streaming container encode (the CLI pipeline, programs/salzcli.c:102-185) ------------
 //
-// One reader (this call's thread pool entry), the encoder slots of salz_encode_blocks, and the
-// caller's thread as the in-order writer. A ring of R pinned block buffers (R = slots + 2)
-// bounds host memory to R x (block + encoded_len_max(block)) whatever the input size; reads,
-// H2D/encode/D2H of several blocks and writes overlap. The block loop is the reference's:
-// blocks are read until a short read, and that last (possibly empty) block is encoded too, so
-// inputs with size mod block in [0, 8] fail exactly as the reference CLI does.
+// One reader thread, the encoder slots, and the caller's thread as the in-order writer. A ring
+// of R pinned buffers (R = slots + 2), each holding one batch of blocks (batch_plan) and its
+// packed frames, bounds host memory whatever the input size; reads, H2D/encode/D2H of several
+// batches and writes overlap. The block loop is the reference's: blocks are read until a short
+// read, and that last (possibly empty) block is encoded too, so inputs with size mod block in
+// [0, 8] fail exactly as the reference CLI does.
 
 namespace {
 struct RingSlot {
     uint8_t *in = nullptr, *out = nullptr;
     size_t in_len = 0, out_len = 0;
-    size_t block = 0;    // block index held
+    size_t batch = 0;    // batch index held
     bool last = false;
     int state = 0;       // 0 free, 1 read (queued for encode), 2 encoded, 3 failed
 };
@@ -753,10 +956,12 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
         return -1;
     }
     const int ndev = (n_devices <= 0 || n_devices > avail) ? avail : n_devices;
-    const int per_dev = block_size >= (256u << 20) ? 2 : block_size >= (1u << 20) ? 4 : kMaxSlots;
+    const BatchPlan plan = batch_plan(block_size);
+    const int per_dev = plan.per_dev;
     const int W = ndev * per_dev;
     const size_t R = (size_t)W + 2;
-    const size_t cap = (size_t)salz_encoded_len_max(block_size);
+    const size_t span = plan.bpb * block_size;   // input bytes per batch
+    const size_t cap = frames_cap(plan.bpb, block_size);
     std::vector<RingSlot> ring(R);
     auto free_ring = [&]() {
         for (RingSlot &r : ring) {
@@ -765,16 +970,16 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
         }
     };
     for (RingSlot &r : ring) {
-        if (hipHostMalloc(reinterpret_cast<void **>(&r.in), block_size ? block_size : 1) != hipSuccess ||
+        if (hipHostMalloc(reinterpret_cast<void **>(&r.in), span) != hipSuccess ||
             hipHostMalloc(reinterpret_cast<void **>(&r.out), cap) != hipSuccess) {
             free_ring();
-            set_error("pinned host buffers for the block ring (%zu x %zu bytes)", R, block_size + cap);
+            set_error("pinned host buffers for the batch ring (%zu x %zu bytes)", R, span + cap);
             return -1;
         }
     }
     std::mutex mu;
     std::condition_variable cv;
-    std::deque<size_t> todo;       // ring indices waiting for an encoder, in block order
+    std::deque<size_t> todo;       // ring indices waiting for an encoder, in batch order
     bool stop = false, reader_done = false;
     std::string err;
     uint64_t nin = 0, nout = 0;
@@ -786,21 +991,21 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
         cv.notify_all();
     };
     auto reader = [&]() {
-        size_t b = 0;
+        size_t t = 0;
         for (;;) {
             size_t k;
             {
                 std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return stop || ring[b % R].state == 0; });
+                cv.wait(lk, [&] { return stop || ring[t % R].state == 0; });
                 if (stop)
                     break;
-                k = b % R;
+                k = t % R;
             }
             RingSlot &r = ring[k];
             size_t got = 0;
             bool eof = false, bad = false;
-            while (got < block_size) {  // fill the block like fread (short only at EOF)
-                const long long n = rd(rd_user, r.in + got, block_size - got);
+            while (got < span) {  // fill the batch like fread (short only at EOF)
+                const long long n = rd(rd_user, r.in + got, span - got);
                 if (n < 0) { bad = true; break; }
                 if (n == 0) { eof = true; break; }
                 got += (size_t)n;
@@ -811,13 +1016,13 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
                 break;
             }
             r.in_len = got;
-            r.block = b;
-            r.last = eof;  // a full block at EOF is followed by the (empty) trailing block
+            r.batch = t;
+            r.last = eof;  // a full batch at EOF is followed by the (empty) trailing block
             r.state = 1;
             nin += got;
             todo.push_back(k);
             cv.notify_all();
-            b++;
+            t++;
             if (r.last)
                 break;
         }
@@ -826,7 +1031,7 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
         cv.notify_all();
     };
     auto worker = [&](int dev, int slot) {
-        salz_gpu_ctx *c = default_ctx(dev, block_size < 9 ? 9 : block_size, slot);
+        salz_gpu_ctx *c = default_ctx(dev, span < 9 ? 9 : span, slot);
         if (!c) {
             std::lock_guard<std::mutex> lk(mu);
             fail(g_err);
@@ -845,14 +1050,18 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
             RingSlot &r = ring[k];
             size_t out = cap;
             int rc;
-            {
+            if (r.last && r.in_len % block_size == 0) {
+                // the trailing fread() chunk is empty: the reference fails it (lib/salz.c:197)
+                set_error("a block of 0 bytes (the input is a multiple of the block size)");
+                rc = -1;
+            } else {
                 std::lock_guard<std::mutex> lk(c->mu);
-                rc = encode_host_locked(c, r.in, r.in_len, r.out, &out, nullptr);
+                rc = encode_batch_locked(c->ws, r.in, r.in_len, block_size, r.out, &out);
             }
             std::lock_guard<std::mutex> lk(mu);
             if (rc != 0) {
                 r.state = 3;
-                fail(std::string("block ") + std::to_string(r.block) + ": " + g_err);
+                fail(std::string("batch ") + std::to_string(r.batch) + ": " + g_err);
                 break;
             }
             r.out_len = out;
@@ -862,8 +1071,7 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
     };
 
     const uint32_t hdr[2] = {0x53414C5Au, (uint32_t)block_size};
-    int rc = wr(wr_user, reinterpret_cast<const uint8_t *>(hdr), 8) == 0 ? 0 : -1;
-    if (rc != 0) {
+    if (wr(wr_user, reinterpret_cast<const uint8_t *>(hdr), 8) != 0) {
         free_ring();
         set_error("write error on the output stream");
         return -1;
@@ -875,23 +1083,22 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
         for (int k = 0; k < per_dev; k++)
             th.emplace_back(worker, d, k);
     // in-order writer
-    for (size_t b = 0;; b++) {
-        RingSlot &r = ring[b % R];
+    for (size_t t = 0;; t++) {
+        RingSlot &r = ring[t % R];
         {
             std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return stop || (r.state == 2 && r.block == b); });
+            cv.wait(lk, [&] { return stop || (r.state == 2 && r.batch == t); });
             if (stop)
                 break;
         }
-        const uint32_t L = (uint32_t)r.out_len;
         const bool last = r.last;
-        if (wr(wr_user, reinterpret_cast<const uint8_t *>(&L), 4) != 0 || wr(wr_user, r.out, r.out_len) != 0) {
+        if (wr(wr_user, r.out, r.out_len) != 0) {
             std::lock_guard<std::mutex> lk(mu);
             fail("write error on the output stream");
             break;
         }
         std::lock_guard<std::mutex> lk(mu);
-        nout += 4 + r.out_len;
+        nout += r.out_len;
         r.state = 0;
         cv.notify_all();
         if (last) {

@@ -20,34 +20,37 @@ namespace {
 constexpr int kThreads = 256;
 
 // Round 0 of the suffix sorter (sa.hip) can start straight from the text: list entry c is
-// suffix i (the < 8 suffixes with fewer than 8 bytes left first, shortest first, then the rest
-// in text order) with the big-endian key of its first 8 bytes (missing bytes zero). The
-// first pass then builds (key, value) itself instead of reading an initial key/value array.
+// suffix init_suffix(c) (common.hpp: the suffixes with fewer than 8 bytes left first,
+// shortest first, then the rest in text order) with the big-endian key of its first 8 bytes
+// (bytes past its block's suffix text zero). The first pass then builds (key, value) itself
+// instead of reading an initial key/value array. A batch of several blocks is then ordered by
+// block with extra passes whose digit is the block of the value (kMode 2).
 struct TextSrc {
     const uint8_t *T;  // padded text
-    uint32_t n;        // suffixes
+    Blocks g;
 };
-
-__device__ __forceinline__ uint32_t init_suffix(size_t c, uint32_t n)
-{
-    const uint32_t s = n < 7 ? n : 7;
-    return c < s ? (n - 1u - (uint32_t)c) : ((uint32_t)c - s);
-}
 
 __device__ __forceinline__ uint64_t init_key(const TextSrc &t, uint32_t i)
 {
     uint64_t w = load_u64_any(t.T, i);
-    const uint32_t left = t.n - i;
+    const uint32_t left = t.g.end(i) - i;
     if (left < 8)
         w &= (1ull << (8u * left)) - 1ull;
     return __builtin_bswap64(w);
+}
+
+// digit source of a pass: 0 = key bits, 1 = key bits of text-built pairs, 2 = block of value
+__device__ __forceinline__ unsigned digit_of(int mode, uint64_t k, uint32_t v, int shift, const Blocks &g)
+{
+    return mode == 2 ? (g.blk(v) >> shift) & 255u : (unsigned)(k >> shift) & 255u;
 }
 constexpr int kItems = 16;
 constexpr int kTile = kThreads * kItems;
 static_assert(kTile == kRadixTile, "tile size mismatch");
 
-template <bool kText>
+template <int kMode>
 __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restrict__ keys,
+                                                         const uint32_t *__restrict__ vals,
                                                          uint32_t m, int shift,
                                                          uint32_t *__restrict__ counts,
                                                          uint32_t ntiles, TextSrc txt)
@@ -66,13 +69,19 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
     const size_t base = (size_t)blockIdx.x * kTile;
     const uint4 *kp = reinterpret_cast<const uint4 *>(keys + base);
     const size_t left = m > base ? m - base : 0;
-    if (kText) {
+    if (kMode == 2) {
+        for (int j = 0; j < kItems; j++) {
+            const size_t i = (size_t)j * kThreads + tid;
+            if (i < left)
+                atomicAdd(&mine[digit_of(2, 0, vals[base + i], shift, txt.g)], 1u);
+        }
+    } else if (kMode == 1) {
         // text loads unconditional (clamped entry), so none is issued under a narrower mask
         uint64_t kk[kItems];
 #pragma unroll
         for (int j = 0; j < kItems; j++) {
             const size_t i = (size_t)j * kThreads + tid;
-            kk[j] = init_key(txt, init_suffix(i < left ? base + i : 0, txt.n));
+            kk[j] = init_key(txt, init_suffix(i < left ? base + i : 0, txt.g));
         }
 #pragma unroll
         for (int j = 0; j < kItems; j++)
@@ -157,7 +166,7 @@ __global__ __launch_bounds__(kRowThreads) void k_radix_rowscan(uint32_t *__restr
         totals[blockIdx.x] = carry;
 }
 
-template <bool kText>
+template <int kMode>
 __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
     uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t m, int shift,
@@ -187,8 +196,8 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     for (int j = 0; j < kItems; j++) {
         size_t i = base + (size_t)j * 64 + lane;
         bool ok = i < m;
-        if (kText) {  // unconditional text loads (clamped entry)
-            const uint32_t sfx = init_suffix(ok ? i : 0, txt.n);
+        if (kMode == 1) {  // unconditional text loads (clamped entry)
+            const uint32_t sfx = init_suffix(ok ? i : 0, txt.g);
             const uint64_t kk = init_key(txt, sfx);
             k[j] = ok ? kk : 0ull;
             v[j] = sfx;
@@ -202,7 +211,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     for (int j = 0; j < kItems; j++) {
         size_t i = base + (size_t)j * 64 + lane;
         bool ok = i < m;
-        unsigned d = (unsigned)(k[j] >> shift) & 255u;
+        unsigned d = digit_of(kMode, k[j], v[j], shift, txt.g);
         uint64_t peers = wave_ballot(ok);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
@@ -270,6 +279,19 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     }
     __syncthreads();
 
+    if (kMode == 2) {  // block passes (a batch's round 0 only): scatter from registers
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            const size_t i = base + (size_t)j * 64 + lane;
+            const unsigned d = digit_of(2, 0, v[j], shift, txt.g);
+            if (i < m) {
+                const uint32_t dst = gbase[d] + cnt[wave][d] + lrank[j];
+                kout[dst] = k[j];
+                vout[dst] = v[j];
+            }
+        }
+        return;
+    }
     uint32_t pos[kItems];  // tile-local sorted position of each item
 #pragma unroll
     for (int j = 0; j < kItems; j++) {
@@ -314,7 +336,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
 
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
-                     const uint8_t *text)
+                     const uint8_t *text, const Blocks *blocks)
 {
     if (m <= 1 || bit_hi <= bit_lo)
         return 0;
@@ -326,15 +348,23 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     }
     uint64_t *kin = *keys, *kout = keys_alt;
     uint32_t *vin = *vals, *vout = vals_alt;
-    for (int shift = bit_lo; shift < bit_hi; shift += 8) {
-        // first pass from the text (round 0 of the suffix sorter): no initial key/value read
-        const bool from_text = text && shift == bit_lo;
-        const TextSrc txt{text, m};
-        if (from_text)
-            hipLaunchKernelGGL(k_radix_hist<true>, dim3(ntiles), dim3(kThreads), 0, st, kin, m,
+    const Blocks g = blocks ? *blocks : Blocks{0xffffffffu, 1u, m};
+    // A batch's round 0: after the key passes, passes on the digits of the value's block
+    // (stable), so the list is ordered by (block, key).
+    const int blk_bits = blocks && g.nb > 1 ? bit_width(g.nb - 1u) : 0;
+    const int passes_key = (bit_hi - bit_lo + 7) / 8, passes = passes_key + (blk_bits + 7) / 8;
+    for (int pass = 0; pass < passes; pass++) {
+        const int mode = pass >= passes_key ? 2 : (text && pass == 0) ? 1 : 0;
+        const int shift = mode == 2 ? 8 * (pass - passes_key) : bit_lo + 8 * pass;
+        const TextSrc txt{text, g};
+        if (mode == 1)
+            hipLaunchKernelGGL(k_radix_hist<1>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
+                               shift, ws.radix_counts, ntiles, txt);
+        else if (mode == 2)
+            hipLaunchKernelGGL(k_radix_hist<2>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
                                shift, ws.radix_counts, ntiles, txt);
         else
-            hipLaunchKernelGGL(k_radix_hist<false>, dim3(ntiles), dim3(kThreads), 0, st, kin, m,
+            hipLaunchKernelGGL(k_radix_hist<0>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
                                shift, ws.radix_counts, ntiles, txt);
         SALZ_LAUNCH_CHECK();
         uint32_t *totals = ws.radix_counts + ncounts;
@@ -342,15 +372,18 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
                            ntiles, totals);
         SALZ_LAUNCH_CHECK();
         // bench.py prices the timed launches at 24 B per element (key + value in and out);
-        // the text-sourced pass reads 1 B of text instead and is left out of that roofline
-        bool timed = ws.timing && !from_text && ws.rx_used + 2 <= ws.rx_pool.size();
+        // the text-sourced and block passes are left out of that roofline
+        bool timed = ws.timing && mode == 0 && ws.rx_used + 2 <= ws.rx_pool.size();
         if (timed)
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used], st));
-        if (from_text)
-            hipLaunchKernelGGL(k_radix_scatter<true>, dim3(ntiles), dim3(kThreads), 0, st, kin,
+        if (mode == 1)
+            hipLaunchKernelGGL(k_radix_scatter<1>, dim3(ntiles), dim3(kThreads), 0, st, kin,
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt);
+        else if (mode == 2)
+            hipLaunchKernelGGL(k_radix_scatter<2>, dim3(ntiles), dim3(kThreads), 0, st, kin,
                                vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt);
         else
-            hipLaunchKernelGGL(k_radix_scatter<false>, dim3(ntiles), dim3(kThreads), 0, st, kin,
+            hipLaunchKernelGGL(k_radix_scatter<0>, dim3(ntiles), dim3(kThreads), 0, st, kin,
                                vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt);
         SALZ_LAUNCH_CHECK();
         if (timed) {

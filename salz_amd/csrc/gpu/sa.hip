@@ -45,16 +45,15 @@ constexpr uint32_t kSegCap = 4096;   // LDS slots: a window's groups span < kSeg
 constexpr int kSegThreads = 256;
 static_assert(kSegCap == 4096, "12-bit slot index in the LDS sort key");
 
-__global__ void k_sa_init(const uint8_t *__restrict__ T, uint32_t n, uint64_t *__restrict__ key,
+__global__ void k_sa_init(const uint8_t *__restrict__ T, Blocks g, uint64_t *__restrict__ key,
                           uint32_t *__restrict__ val)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (c >= n)
+    if (c >= g.nsa())
         return;
-    uint32_t s = n < 7 ? n : 7;
-    uint32_t i = c < s ? (n - 1u - (uint32_t)c) : ((uint32_t)c - s);
+    const uint32_t i = init_suffix(c, g);
     uint64_t w = load_u64_any(T, i);
-    uint32_t left = n - i;
+    uint32_t left = g.end(i) - i;
     if (left < 8)
         w &= (1ull << (8u * left)) - 1ull;
     key[c] = __builtin_bswap64(w);
@@ -79,7 +78,7 @@ __device__ __forceinline__ void put_heads(HeadBits hb, size_t c, uint32_t m, boo
 }
 
 __global__ void k_heads(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
-                        uint32_t m, uint32_t n, int round0, HeadBits hb)
+                        uint32_t m, Blocks bl, int round0, HeadBits hb)
 {
     const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if ((c & ~(size_t)63) >= m)
@@ -90,8 +89,8 @@ __global__ void k_heads(const uint64_t *__restrict__ key, const uint32_t *__rest
     const uint64_t k0 = key[cp], k1 = key[cc];
     const uint32_t v0 = val[cp], v1 = val[cc];
     bool h = cc == 0 || k0 != k1;
-    if (round0 && !h)
-        h = (n - v1) < 8u || (n - v0) < 8u;
+    if (round0 && !h)  // short suffixes are singletons; a batch's blocks never share a group
+        h = (bl.end(v1) - v1) < 8u || (bl.end(v0) - v0) < 8u || bl.blk(v0) != bl.blk(v1);
     put_heads(hb, c, m, in && h);
 }
 
@@ -212,7 +211,7 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
                          const uint32_t *__restrict__ off_old, uint32_t *__restrict__ off_new,
                          uint32_t *__restrict__ nval, uint32_t *__restrict__ ngid,
                          uint32_t *__restrict__ rank, uint32_t *__restrict__ sa, GroupTab tab,
-                         uint32_t m, uint32_t n, int kb_old, int round0, uint32_t *err,
+                         uint32_t m, uint32_t n, uint32_t nsa, int kb_old, int round0, uint32_t *err,
                          uint32_t ihi, uint32_t *__restrict__ later)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
@@ -224,7 +223,7 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     uint32_t size = headpos[g + 1] - hp;
     uint32_t o = round0 ? 0u : off_old[(uint32_t)(key[c] >> kb_old)];
     uint32_t i = val[c];
-    if (bad_index(i >= n || c + o >= n || hp > c || size > m, err, kErrCommit))
+    if (bad_index(i >= n || c + o >= nsa || hp > c || size > m, err, kErrCommit))
         return;
     // The first subgroup of an old group keeps the old group's head, so its members' ranks
     // are unchanged; every other rank (and all of round 0) is written.
@@ -274,7 +273,7 @@ constexpr uint32_t kLcpMaxHk = 4096;
 // k_heads with the LCP of every new head (writes the head ballots like k_heads).
 __global__ __launch_bounds__(kT) void k_heads_lcp(
     const uint64_t *__restrict__ K, const uint32_t *__restrict__ V, HeadBits hb,
-    const uint32_t *__restrict__ off_old, uint32_t m, uint32_t n, int kb_old, uint32_t hk, int round0,
+    const uint32_t *__restrict__ off_old, uint32_t m, Blocks bl, int kb_old, uint32_t hk, int round0,
     const uint8_t *__restrict__ T, uint32_t *__restrict__ lcps, uint32_t *err)
 {
     const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
@@ -284,8 +283,10 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
     const uint64_t k0 = K[cp], k1 = K[cc];
     const uint32_t v0 = V[cp], v1 = V[cc];
     bool head = c == 0 || k0 != k1;
+    const uint32_t e1 = bl.end(v1);  // end of v1's suffix text (its block's)
+    const bool other_block = bl.blk(v0) != bl.blk(v1);
     if (round0 && !head)
-        head = (n - v1) < 8u || (n - v0) < 8u;
+        head = (e1 - v1) < 8u || (bl.end(v0) - v0) < 8u || other_block;
     put_heads(hb, c, m, in && head);
     const uint32_t g1 = round0 ? 0u : (uint32_t)(k1 >> kb_old);
     const uint32_t o = round0 ? 0u : off_old[g1];
@@ -295,17 +296,18 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
     if (in && head) {
         if (round0) {
             uint32_t l = 0;
-            if (c > 0) {
+            if (c > 0 && !other_block) {  // a block's first suffix: LCP 0
                 const uint64_t x = k0 ^ k1;
                 l = x ? (uint32_t)__builtin_clzll(x) >> 3 : 8u;
-                l = umin_(l, n - i);
-                l = umin_(l, n - j);
+                l = umin_(l, e1 - i);
+                l = umin_(l, e1 - j);
             }
             lcps[c] = l;
         } else if (c > 0 && (uint32_t)(k0 >> kb_old) == g1) {
             pos = (uint32_t)c + o;
-            if (!bad_index(i >= n || j >= n || pos >= n || n - mx < hk, err, kErrCommit)) {
-                lim = umin_(hk, n - mx - hk);
+            // (same group, so the same block: e1 bounds both suffixes)
+            if (!bad_index(i >= e1 || j >= e1 || pos >= bl.nsa() || e1 - mx < hk, err, kErrCommit)) {
+                lim = umin_(hk, e1 - mx - hk);
                 if (hk <= kLcpLane) {
                     uint32_t l = lim;
                     for (uint32_t off = 0; off < lim; off += 8) {
@@ -346,6 +348,17 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
         if ((int)lane == src)
             lcps[sp] = hk + mis;
     }
+}
+
+// rank 0 (end of text) at a batch's dead positions: the 8 bytes after every block's suffix
+// text but the last (the last block's end npos gets rank 0 from the host)
+__global__ void k_dead_ranks(Blocks bl, uint32_t *__restrict__ rank)
+{
+    const uint32_t x = blockIdx.x * kT + threadIdx.x;
+    if (x >= 8u * (bl.nb - 1u))
+        return;
+    const uint32_t b = x >> 3;
+    rank[b * bl.bs + bl.bs - 8u + (x & 7u)] = 0u;
 }
 
 // Later passes of a split rank scatter: ranks of suffixes in [ilo, ihi), from k_commit's list.
@@ -524,11 +537,11 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
 }
 
 // SALZ_CHECK_SA=1: every position must appear exactly once in the suffix array.
-__global__ void k_sa_check(const uint32_t *__restrict__ sa, uint32_t n, uint32_t *seen,
+__global__ void k_sa_check(const uint32_t *__restrict__ sa, uint32_t nsa, uint32_t n, uint32_t *seen,
                            uint32_t *err)
 {
     size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (r >= n)
+    if (r >= nsa)
         return;
     const uint32_t i = sa[r];
     if (i >= n || atomicAdd(&seen[i], 1u) != 0)
@@ -547,20 +560,20 @@ __global__ void k_dbg_sorted(const uint64_t *__restrict__ K, uint32_t m, uint32_
 
 __global__ void k_dbg_pairs(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
                             const uint32_t *__restrict__ rank, const uint8_t *__restrict__ T,
-                            uint32_t m, uint32_t n, uint32_t h, int kb, int round0, uint32_t *err)
+                            uint32_t m, Blocks bl, uint32_t h, int kb, int round0, uint32_t *err)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
         return;
     const uint32_t i = V[c];
-    if (i >= n) {
+    if (i >= bl.npos) {
         atomicOr(err, 0x10000u);
         return;
     }
     uint64_t want;
     if (round0) {
         uint64_t w = load_u64_any(T, i);
-        const uint32_t left = n - i;
+        const uint32_t left = bl.end(i) - i;
         if (left < 8)
             w &= (1ull << (8u * left)) - 1ull;
         want = __builtin_bswap64(w);
@@ -675,10 +688,11 @@ __global__ void k_keys(const uint32_t *__restrict__ nval, const uint32_t *__rest
 
 }  // namespace
 
-int stage_suffix_array(Workspace &ws, uint32_t n)
+int stage_suffix_array(Workspace &ws, const Blocks &bl)
 {
     hipStream_t st = ws.stream;
-    if (n == 0)
+    const uint32_t n = bl.npos, nsa = bl.nsa();  // position space, live suffixes
+    if (nsa == 0)
         return 0;
     uint64_t *K = ws.keyA;
     uint32_t *V = ws.valA;
@@ -705,16 +719,20 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     static const bool split_on = !getenv("SALZ_COMMIT_SPLIT") || atoi(getenv("SALZ_COMMIT_SPLIT")) > 1;
     static const uint32_t split_ratio = getenv("SALZ_SPLIT_RATIO") ? (uint32_t)atoi(getenv("SALZ_SPLIT_RATIO")) : 4;
     SALZ_HIP(hipMemsetAsync(ws.rank + n, 0, sizeof(uint32_t), st));  // rank[n] = 0
+    if (bl.nb > 1) {
+        hipLaunchKernelGGL(k_dead_ranks, dim3(grid_for(8u * (bl.nb - 1u), kT)), dim3(kT), 0, st, bl, ws.rank);
+        SALZ_LAUNCH_CHECK();
+    }
     // Round 0's first radix pass reads the text itself (radix.hip, TextSrc); the initial
     // key/value arrays are only materialised for the per-round checks, and for n = 1 (the
     // sort has nothing to do and would leave them unwritten).
-    const bool text_first = !dbg_rounds && n > 1;
+    const bool text_first = !dbg_rounds && nsa > 1;
     if (!text_first) {
-        hipLaunchKernelGGL(k_sa_init, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, n, K, V);
+        hipLaunchKernelGGL(k_sa_init, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.text, bl, K, V);
         SALZ_LAUNCH_CHECK();
     }
-    if (dbg_rounds) {
-        hipLaunchKernelGGL(k_dbg_pairs, dim3(grid_for(n, kT)), dim3(kT), 0, st, K, V, ws.rank, ws.text, n, n,
+    if (dbg_rounds && bl.nb == 1) {
+        hipLaunchKernelGGL(k_dbg_pairs, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, K, V, ws.rank, ws.text, nsa, bl,
                            0u, 0, 1, derr);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 512, "sa.init") != 0)
@@ -727,7 +745,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         }
     }
 
-    uint32_t m = n, h = 8, G_act = 0, GL = 0, mL = 0;
+    uint32_t m = nsa, h = 8, G_act = 0, GL = 0, mL = 0;
     int kb_old = 0, round0 = 1;
     const int kb = bit_width(n);
     ws.stats.sa_rounds = 0;
@@ -743,7 +761,11 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         const char *how = "global";
         bool seg_round = false;
         if (round0) {
-            if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, 64, ws, st, text_first ? ws.text : nullptr) != 0)
+            if (!text_first && bl.nb > 1) {
+                set_error("suffix sort: a batch of blocks needs the text-built first pass");
+                return -1;
+            }
+            if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, 64, ws, st, text_first ? ws.text : nullptr, &bl) != 0)
                 return -1;
         } else {
             // Global sort of every active suffix on (group, rank) vs. LDS sort of the small
@@ -790,20 +812,20 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         Kx = (K == ws.keyA) ? ws.keyB : ws.keyA;
         Vx = (V == ws.valA) ? ws.valB : ws.valA;
 
-        if (dbg_rounds && !seg_round) {
+        if (dbg_rounds && !seg_round && bl.nb == 1) {
             hipLaunchKernelGGL(k_dbg_sorted, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, m, derr, 0x1000u);
             SALZ_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_dbg_pairs, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, ws.rank, ws.text, m,
-                               n, h / 2, kb, round0, derr);
+                               bl, h / 2, kb, round0, derr);
             SALZ_LAUNCH_CHECK();
         }
         if (ws.lcps_ok && !round0 && h / 2 > kLcpMaxHk)
             ws.lcps_ok = false;  // long repeats: the PLCP stage is cheaper than these compares
         if (ws.lcps_ok)
-            hipLaunchKernelGGL(k_heads_lcp, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, offo, m, n,
+            hipLaunchKernelGGL(k_heads_lcp, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, offo, m, bl,
                                kb_old, round0 ? 0u : h / 2, round0, ws.text, ws.lcps, derr);
         else
-            hipLaunchKernelGGL(k_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m, n, round0,
+            hipLaunchKernelGGL(k_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m, bl, round0,
                                hb);
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u32(hb.wcnt, hb.wpre, ((size_t)m + 63) / 64, false, d32 + 0, ws, st) != 0)
@@ -857,7 +879,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
         const uint32_t span = (uint32_t)(((uint64_t)n + parts - 1) / parts);
         uint32_t *later = reinterpret_cast<uint32_t *>(Kx);  // free until k_keys
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, headpos,
-                           gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, kb_old,
+                           gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, nsa, kb_old,
                            round0, derr, parts > 1 ? span : 0xffffffffu, parts > 1 ? later : nullptr);
         SALZ_LAUNCH_CHECK();
         for (uint32_t q = 1; q < parts; q++) {
@@ -906,7 +928,7 @@ int stage_suffix_array(Workspace &ws, uint32_t n)
     static const bool check = getenv("SALZ_CHECK_SA") != nullptr;
     if (check) {
         SALZ_HIP(hipMemsetAsync(ws.u0, 0, sizeof(uint32_t) * n, st));
-        hipLaunchKernelGGL(k_sa_check, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.sa, n, ws.u0, derr);
+        hipLaunchKernelGGL(k_sa_check, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.sa, nsa, n, ws.u0, derr);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 256, "sa.check") != 0)
             return -1;

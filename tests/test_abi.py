@@ -150,3 +150,29 @@ def test_parse_chunk_log_boundaries(monkeypatch):
         assert f(N) == k, (N, f(N), k)
     monkeypatch.setenv("SALZ_PARSE_KLOG", "8")
     assert f(16 * MiB) == 8
+
+
+@pytest.mark.parametrize("size,block", [(100, 1000), (9, 9), (15, 15), (5000, 512), (512 * 7 + 9, 512),
+                                        (512 * 3 + 15, 512), (512 * 4 + 100, 512), (32768 * 5 + 300, 32768)])
+def test_batch_round0_order(size, block):
+    """Round 0 of a batch (common.hpp init_suffix): every live suffix exactly once (dead
+    positions: the 8 bytes after each block's suffix text), the suffixes with fewer than 8
+    bytes left first, shortest first within each block, then the rest in text order."""
+    import salz_amd
+
+    nb = 1 if block >= size else -(-size // block)
+    out = np.zeros(size, np.uint32)
+    m = salz_amd.lib.salz_debug_init_order(size, block, out.ctypes.data)
+    order = out[:m].tolist()
+    starts = [b * block for b in range(nb)]
+    ends = [min(s + block, size) - 8 for s in starts] if nb > 1 else [size - 8]
+    live = sorted(p for s, e in zip(starts, ends) for p in range(s, e))
+    assert sorted(order) == live and m == len(live)
+    blk = (lambda p: 0) if nb == 1 else (lambda p: p // block)
+    left = [ends[blk(p)] - p for p in order]
+    nshort = sum(1 for x in left if x < 8)
+    assert all(x < 8 for x in left[:nshort]) and all(x >= 8 for x in left[nshort:])
+    for b in range(nb):  # shortest first within a block
+        mine = [x for p, x in zip(order[:nshort], left[:nshort]) if blk(p) == b]
+        assert mine == sorted(mine)
+    assert order[nshort:] == sorted(order[nshort:])
