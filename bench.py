@@ -69,6 +69,10 @@ def parse_args():
     ap.add_argument("--slots", type=int, default=0,
                     help="concurrent encoder contexts per GPU for the sharded workloads "
                          "(0 = auto: 4; one block per GPU: 1)")
+    ap.add_argument("--batch-bytes", type=int, default=8 << 20,
+                    help="sharded workloads with blocks of at most 4 MiB: consecutive blocks "
+                         "encoded per pipeline pass (salz_gpu_encode_batch_device; 0 = one block "
+                         "per pass; larger blocks always go one per pass)")
     return ap.parse_args()
 
 
@@ -191,19 +195,29 @@ def main():
         nblocks = world
         spans = [(0, total)]
     block_field = block or total
-    max_block = max([e - s for s, e in spans] + [9])
-    # Several blocks per GPU: independent encoder contexts (own stream + workspace each) on
-    # host threads, so one block's host round trips overlap another block's kernels.
+    # Units of work: the single-block workloads encode their block per pass (the
+    # salz_encode_safe path); the sharded ones encode consecutive blocks of the rank's range
+    # batch_bytes at a time in one pipeline pass each (salz_gpu_encode_batch_device, blocks of at
+    # most 4 MiB, as salz_encode_blocks does), whose
+    # output is already the frames (u32 length + stream per block).
+    use_batch = sharded and block % 512 == 0 and block <= (4 << 20) and args.batch_bytes > 0
+    bpb = max(1, args.batch_bytes // block) if use_batch else 1
+    units = [(spans[i][0], spans[min(i + bpb, len(spans)) - 1][1], min(bpb, len(spans) - i))
+             for i in range(0, len(spans), bpb)]
+    max_unit = max([e - s for s, e, _ in units] + [9])
+    # Several units per GPU: independent encoder contexts (own stream + workspace each) on host
+    # threads, so one unit's host round trips overlap another's kernels.
     nslots = args.slots or (1 if not sharded else 4)
-    nslots = max(1, min(nslots, max(len(spans), 1)))
-    ctxs = [salz_amd.Context(device, max_block) for _ in range(nslots)]
+    nslots = max(1, min(nslots, max(len(units), 1)))
+    ctxs = [salz_amd.Context(device, max_unit) for _ in range(nslots)]
     ctx = ctxs[0]
     streams_t = [torch.cuda.Stream(device=dev) for _ in range(nslots)]
-    cap = salz_amd.encoded_len_max(max_block) + 4096
-    d_src = [torch.from_numpy(src[s:e].copy()).to(dev) for s, e in spans]
-    d_dst = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in spans]
-    d_packed = torch.empty(max(packed_len([cap] * len(spans)), 1), dtype=torch.uint8, device=dev)
-    d_container = torch.empty(8 + nblocks * (cap + 4), dtype=torch.uint8, device=dev) if rank == 0 else None
+    blk_cap = salz_amd.encoded_len_max(block or total) + 4096
+    caps = [k * (blk_cap + 4) + 64 for _, _, k in units]
+    d_src = [torch.from_numpy(src[s:e].copy()).to(dev) for s, e, _ in units]
+    d_dst = [torch.empty(c, dtype=torch.uint8, device=dev) for c in caps]
+    d_packed = torch.empty(max(sum(caps), 1), dtype=torch.uint8, device=dev)
+    d_container = torch.empty(8 + nblocks * (blk_cap + 4), dtype=torch.uint8, device=dev) if rank == 0 else None
     torch.cuda.synchronize()
     pool = None
     if nslots > 1:
@@ -212,24 +226,35 @@ def main():
         pool = ThreadPoolExecutor(nslots)
 
     def enc(k, j):
-        s, e = spans[j]
-        return ctxs[k].encode_device(d_src[j].data_ptr(), e - s, d_dst[j].data_ptr(), cap,
+        s, e, _ = units[j]
+        if use_batch:
+            return ctxs[k].encode_batch_device(d_src[j].data_ptr(), e - s, block, d_dst[j].data_ptr(),
+                                               caps[j], streams_t[k].cuda_stream)
+        return ctxs[k].encode_device(d_src[j].data_ptr(), e - s, d_dst[j].data_ptr(), caps[j],
                                      streams_t[k].cuda_stream)
 
-    def run_slot(k):  # slot k encodes blocks k, k + nslots, ... (ctypes drops the GIL)
-        return [(j, enc(k, j)) for j in range(k, len(spans), nslots)]
+    def run_slot(k):  # slot k encodes units k, k + nslots, ... (ctypes drops the GIL)
+        return [(j, enc(k, j)) for j in range(k, len(units), nslots)]
 
     def step():
-        """One step: encode this rank's blocks into HBM, pack their frames, and the exchange
-        step that assembles the whole container in rank 0's HBM (RCCL for N > 1)."""
+        """One step: encode this rank's blocks into HBM, their frames packed in block order,
+        and the exchange step that assembles the whole container in rank 0's HBM (RCCL for
+        N > 1)."""
         if pool is None:
-            lens = [enc(0, j) for j in range(len(spans))]
+            lens = [enc(0, j) for j in range(len(units))]
         else:
-            lens = [0] * len(spans)
+            lens = [0] * len(units)
             for part in pool.map(run_slot, range(nslots)):
                 for j, v in part:
                     lens[j] = v
-        nb = pack_frames(d_dst, lens, d_packed)
+        if use_batch:  # the units' frames, one after another
+            nb, o = 0, 0
+            for d, n in zip(d_dst, lens):
+                d_packed[o:o + n].copy_(d[:n])
+                o += n
+            nb = o
+        else:
+            nb = pack_frames(d_dst, lens, d_packed)
         cont = gather_container(d_packed, nb, block_field, rank, world, None, d_container)
         torch.cuda.synchronize()
         return lens, cont
@@ -239,8 +264,9 @@ def main():
     for _ in range(args.warmup):
         step()
     ctx.set_timing(True)
-    enc(0, len(spans) - 1)
-    st = ctx.stats()  # stats of the last block of this rank
+    if units:
+        enc(0, len(units) - 1)
+    st = ctx.stats()  # stats of the last unit of this rank (zeros for a rank without blocks)
     ctx.set_timing(bool(args.profile_steps))
     lens, cont = step()
 
@@ -257,8 +283,18 @@ def main():
     if args.profile_steps:
         st = ctx.stats()
 
-    streams = [d.narrow(0, 0, n).cpu().numpy().tobytes() for d, n in zip(d_dst, lens)]
-    in_bytes, out_bytes = allreduce([float(sum(e - s for s, e in spans)), float(sum(lens))], SUM)
+    if use_batch:  # split every unit's frames into its blocks' streams
+        streams = []
+        for d, n in zip(d_dst, lens):
+            data, pos = d.narrow(0, 0, n).cpu().numpy().tobytes(), 0
+            while pos < len(data):
+                L = int.from_bytes(data[pos:pos + 4], "little")
+                streams.append(data[pos + 4:pos + 4 + L])
+                pos += 4 + L
+    else:
+        streams = [d.narrow(0, 0, n).cpu().numpy().tobytes() for d, n in zip(d_dst, lens)]
+    in_bytes, out_bytes = allreduce([float(sum(e - s for s, e in spans)),
+                                     float(sum(len(x) for x in streams))], SUM)
 
     # Round trip of every local block through the product decoder (frame rule > 16 MiB), and on
     # rank 0 the assembled container (every rank's blocks) through the threaded decoder.
@@ -316,14 +352,17 @@ def main():
     # stream), same blocks and slots; never `value`.
     e2e = None
     if not args.no_e2e:
-        host_blocks = [src[s:e] for s, e in spans]
+        host_units = [src[s:e] for s, e, _ in units]
+
+        def enc_host(k, j):
+            return ctxs[k].encode_batch(host_units[j], block) if use_batch else ctxs[k].encode(host_units[j])
 
         def run_slot_host(k):
-            return [ctxs[k].encode(host_blocks[j]) for j in range(k, len(spans), nslots)]
+            return [enc_host(k, j) for j in range(k, len(units), nslots)]
 
         def step_host():
             if pool is None:
-                return [ctx.encode(b) for b in host_blocks]
+                return [enc_host(0, j) for j in range(len(units))]
             return list(pool.map(run_slot_host, range(nslots)))
 
         step_host()
@@ -390,7 +429,8 @@ def main():
                 "block_bytes": block_field,
                 "blocks": nblocks,
                 "input": kind,
-                "parallelism": f"independent blocks over {world} GPU(s), {nslots} encoder slot(s) per GPU; "
+                "parallelism": f"independent blocks over {world} GPU(s), {nslots} encoder slot(s) per GPU"
+                               f"{f', {bpb} blocks per pipeline pass' if use_batch else ''}; "
                                f"step = encode + frame packing + exchange ("
                                f"{'RCCL all-gather of run lengths + xGMI point-to-point payload runs' if world > 1 else 'local'}"
                                f") + container assembly in rank 0's HBM",

@@ -77,6 +77,12 @@ int salz_gpu_encode_dump(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, 
 int salz_gpu_encode_batch(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len, size_t block_size,
                           uint8_t *dst, size_t *dst_len);
 
+/* salz_gpu_encode_batch for a batch already in device memory: the packed frames go to device
+ * buffer d_dst (dst_cap bytes); `stream` as for salz_gpu_encode_device. Returns 0 / -1. */
+int salz_gpu_encode_batch_device(salz_gpu_ctx *ctx, const uint8_t *d_src, size_t src_len,
+                                 size_t block_size, uint8_t *d_dst, size_t dst_cap, size_t *dst_len,
+                                 void *stream);
+
 typedef struct {
     double ms_upload, ms_sa, ms_lcp, ms_ansv, ms_parse, ms_emit, ms_total;
     int32_t sa_rounds, parse_iters;

@@ -81,6 +81,8 @@ lib.salz_gpu_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
 lib.salz_gpu_set_timing.restype = None
 lib.salz_gpu_encode_batch.argtypes = [ctypes.c_void_p, _u8p, _sz, _sz, _u8p, _szp]
 lib.salz_gpu_encode_batch.restype = ctypes.c_int
+lib.salz_gpu_encode_batch_device.argtypes = [ctypes.c_void_p, _u8p, _sz, _sz, _u8p, _sz, _szp, ctypes.c_void_p]
+lib.salz_gpu_encode_batch_device.restype = ctypes.c_int
 lib.salz_debug_init_order.argtypes = [_sz, _sz, ctypes.c_void_p]
 lib.salz_debug_init_order.restype = ctypes.c_int
 lib.salz_encode_blocks.argtypes = [_u8p, _sz, _sz, _u8p, _szp, ctypes.c_int]
@@ -277,6 +279,16 @@ class Context:
             streams.append(data[pos + 4:pos + 4 + L])
             pos += 4 + L
         return streams
+
+    def encode_batch_device(self, d_src: int, src_len: int, block_size: int, d_dst: int, dst_cap: int,
+                            stream: Optional[int] = None) -> int:
+        """salz_gpu_encode_batch_device: packed frames of every block into HBM; their bytes."""
+        n = ctypes.c_size_t(0)
+        rc = lib.salz_gpu_encode_batch_device(self.handle, d_src, src_len, block_size, d_dst, dst_cap,
+                                              ctypes.byref(n), stream)
+        if rc != 0:
+            raise SalzError(f"encode_batch_device failed: {last_error()}")
+        return n.value
 
     def encode_batch_dump(self, src, block_size: int) -> tuple[list[bytes], dict]:
         """encode_batch plus the batch's stage arrays (test hook): sa holds global text

@@ -358,28 +358,45 @@ __global__ void k_block_wbase(BlockOut *__restrict__ binfo, const uint64_t *__re
         binfo[b].wbase = wpre[b];
 }
 
-// Headers (type << 24 | length & 0xffffff, lib/salz.c:760-772) and the PLAIN fallback
-// (lib/salz.c:755-767): one workgroup per block.
-__global__ void k_finalize(const uint8_t *__restrict__ T, Blocks bl, uint32_t N_last,
-                           const BlockOut *__restrict__ binfo, uint8_t *__restrict__ out, size_t stride)
+// Headers (type << 24 | length & 0xffffff, lib/salz.c:760-772), one thread per block.
+__global__ void k_finalize(Blocks bl, uint32_t N_last, const BlockOut *__restrict__ binfo,
+                           uint8_t *__restrict__ out, size_t stride)
 {
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = blockIdx.x * kT + threadIdx.x;
+    if (b >= bl.nb)
+        return;
     const uint32_t N = b + 1u == bl.nb ? N_last : bl.bs;
     const uint64_t L = binfo[b].len;
     uint8_t *o = out + (size_t)b * stride;
     const bool plain = L > (uint64_t)N + 4;
-    if (plain) {
-        const uint8_t *src = T + (size_t)b * (bl.nb == 1 ? 0u : bl.bs);
-        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x)
-            o[4 + i] = src[i];
-    }
-    if (threadIdx.x == 0) {
-        const uint32_t h = plain ? (N & 0xffffffu) : (1u << 24) | ((uint32_t)(L - 4) & 0xffffffu);
-        o[0] = (uint8_t)h;
-        o[1] = (uint8_t)(h >> 8);
-        o[2] = (uint8_t)(h >> 16);
-        o[3] = (uint8_t)(h >> 24);
-    }
+    const uint32_t h = plain ? (N & 0xffffffu) : (1u << 24) | ((uint32_t)(L - 4) & 0xffffffu);
+    o[0] = (uint8_t)h;
+    o[1] = (uint8_t)(h >> 8);
+    o[2] = (uint8_t)(h >> 16);
+    o[3] = (uint8_t)(h >> 24);
+}
+
+// The PLAIN fallback (lib/salz.c:755-767): the raw block after the header, for blocks whose
+// SALZ stream is longer than N + 4. grid (pieces of 4 KiB, blocks); 16 bytes per thread (an
+// aligned 16-byte load of the text, byte stores after the 4-byte header).
+__global__ __launch_bounds__(256) void k_plain_copy(const uint8_t *__restrict__ T, Blocks bl, uint32_t N_last,
+                                                    const BlockOut *__restrict__ binfo,
+                                                    uint8_t *__restrict__ out, size_t stride)
+{
+    const uint32_t b = blockIdx.y;
+    const uint32_t N = b + 1u == bl.nb ? N_last : bl.bs;
+    if (binfo[b].len <= (uint64_t)N + 4)
+        return;
+    const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    if (i >= N)
+        return;
+    const uint8_t *src = T + (size_t)b * (bl.nb == 1 ? 0u : bl.bs);
+    const uint4 v = *reinterpret_cast<const uint4 *>(src + i);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t cnt = N - i < 16 ? (uint32_t)(N - i) : 16u;
+    uint8_t *o = out + (size_t)b * stride + 4 + i;
+    for (uint32_t k = 0; k < cnt; k++)
+        o[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
 }
 
 }  // namespace
@@ -480,8 +497,17 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
                            nwords, dst, stride, binfo, nb);
         SALZ_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_finalize, dim3(nb), dim3(kT), 0, st, ws.text, bl, N_last, binfo, dst, stride);
+    hipLaunchKernelGGL(k_finalize, dim3(grid_for(nb, kT)), dim3(kT), 0, st, bl, N_last, binfo, dst, stride);
     SALZ_LAUNCH_CHECK();
+    bool any_plain = false;
+    for (uint32_t b = 0; b < nb; b++)
+        any_plain |= lens[b] != hb[b].len;
+    if (any_plain) {
+        const uint32_t maxN = nb > 1 ? bl.bs : N_last;
+        hipLaunchKernelGGL(k_plain_copy, dim3(grid_for(maxN, 4096), nb), dim3(256), 0, st, ws.text, bl,
+                           N_last, binfo, dst, stride);
+        SALZ_LAUNCH_CHECK();
+    }
     return 0;
 }
 

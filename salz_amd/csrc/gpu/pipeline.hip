@@ -396,7 +396,9 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P
     SALZ_HIP(hipMemcpyAsync(ws.text, src, P, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                             st));
     SALZ_HIP(hipMemsetAsync(ws.text + P, 0, 128, st));
-    ws.klog = parse_chunk_log(P);
+    // (a batch's chunk length follows its block size: the per-block trade-off of pass count
+    // against pass length, parse.hip)
+    ws.klog = parse_chunk_log(nbz == 1 ? P : bs);
     if (nbz > 1 && bs % ((size_t)1 << ws.klog) != 0) {
         set_error("batch block size %zu is not a multiple of the parse chunk", bs);
         return -1;
@@ -449,24 +451,33 @@ __global__ void k_frame_len(const size_t *__restrict__ lens, uint64_t *__restric
         flen[b] = 4 + (uint64_t)lens[b];
 }
 
-__global__ void k_pack_frames(const uint8_t *__restrict__ regions, size_t stride,
-                              const size_t *__restrict__ lens, const uint64_t *__restrict__ foff,
-                              uint8_t *__restrict__ out)
+// grid (pieces of 4 KiB, blocks): a thread moves 16 bytes, one aligned 16-byte load from the
+// block's region (regions are 64-byte aligned) and 16 byte stores (frames are unaligned).
+__global__ __launch_bounds__(256) void k_pack_frames(const uint8_t *__restrict__ regions, size_t stride,
+                                                     const size_t *__restrict__ lens,
+                                                     const uint64_t *__restrict__ foff,
+                                                     uint8_t *__restrict__ out)
 {
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = blockIdx.y;
     const uint32_t L = (uint32_t)lens[b];
     uint8_t *o = out + foff[b];
-    const uint8_t *src = regions + (size_t)b * stride;
-    if (threadIdx.x < 4)
+    if (blockIdx.x == 0 && threadIdx.x < 4)
         o[threadIdx.x] = (uint8_t)(L >> (8 * threadIdx.x));
-    for (uint32_t i = threadIdx.x; i < L; i += blockDim.x)
-        o[4 + i] = src[i];
+    const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    if (i >= L)
+        return;
+    const uint4 v = *reinterpret_cast<const uint4 *>(regions + (size_t)b * stride + i);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t cnt = L - i < 16 ? (uint32_t)(L - i) : 16u;
+    for (uint32_t k = 0; k < cnt; k++)
+        o[4 + i + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
 }
 
-// A batch from host memory: every block encoded in one pipeline pass, the packed frames copied
-// to host memory dst (capacity *dst_len; set to the bytes written).
-static int encode_batch_locked(Workspace &ws, const uint8_t *src, size_t P, size_t bs, uint8_t *dst,
-                               size_t *dst_len, const salz_gpu_dump *dump = nullptr)
+// A batch: every block encoded in one pipeline pass and its frames packed (u32 length +
+// stream per block) into device memory `packed` (capacity packed_cap); *total = bytes.
+static int encode_batch_packed(Workspace &ws, const uint8_t *src, bool src_dev, size_t P, size_t bs,
+                               uint8_t *packed, size_t packed_cap, size_t *total,
+                               const salz_gpu_dump *dump)
 {
     const size_t nb = bs >= P ? 1 : (P + bs - 1) / bs;
     const size_t stride = batch_stride(bs < P ? bs : P);
@@ -480,16 +491,16 @@ static int encode_batch_locked(Workspace &ws, const uint8_t *src, size_t P, size
     // fails here too.
     const size_t cap = (size_t)salz_encoded_len_max(bs);
     std::vector<size_t> lens(nb);
-    if (encode_core(ws, src, false, P, bs, ws.out, stride, cap < stride ? cap : stride, lens.data(), dump) != 0)
+    if (encode_core(ws, src, src_dev, P, bs, ws.out, stride, cap < stride ? cap : stride, lens.data(), dump) != 0)
         return -1;
-    size_t total = 0;
+    size_t sum = 0;
     for (size_t L : lens)
-        total += 4 + L;
-    if (total > *dst_len) {
-        set_error("batch frames (%zu bytes) exceed the destination capacity (%zu)", total, *dst_len);
+        sum += 4 + L;
+    if (sum > packed_cap) {
+        set_error("batch frames (%zu bytes) exceed the destination capacity (%zu)", sum, packed_cap);
         return -1;
     }
-    // lens to the device through the scalar area (plain host -> device copy)
+    // lens to the device (plain host -> device copy), frame offsets by a device scan
     size_t *dlens = reinterpret_cast<size_t *>(ws.lrec);  // free after the suffix sort
     uint64_t *foff = reinterpret_cast<uint64_t *>(ws.lrec) + nb;
     if (2 * nb + 2 > ws.cap_n / 1024 + 2) {
@@ -501,10 +512,28 @@ static int encode_batch_locked(Workspace &ws, const uint8_t *src, size_t P, size
     SALZ_LAUNCH_CHECK();
     if (scan_sum_u64(foff, foff, nb, false, nullptr, ws, ws.stream) != 0)
         return -1;
-    uint8_t *packed = reinterpret_cast<uint8_t *>(ws.keyB);  // free after emission
-    hipLaunchKernelGGL(k_pack_frames, dim3((unsigned)nb), dim3(256), 0, ws.stream, ws.out, stride, dlens,
-                       foff, packed);
+    size_t maxL = 0;
+    for (size_t L : lens)
+        maxL = L > maxL ? L : maxL;
+    hipLaunchKernelGGL(k_pack_frames, dim3(grid_for(maxL, 4096), (unsigned)nb), dim3(256), 0, ws.stream,
+                       ws.out, stride, dlens, foff, packed);
     SALZ_LAUNCH_CHECK();
+    *total = sum;
+    return 0;
+}
+
+// The same from host memory to host memory dst (capacity *dst_len; set to the bytes written).
+static int encode_batch_locked(Workspace &ws, const uint8_t *src, size_t P, size_t bs, uint8_t *dst,
+                               size_t *dst_len, const salz_gpu_dump *dump = nullptr)
+{
+    uint8_t *packed = reinterpret_cast<uint8_t *>(ws.keyB);  // free after emission (8 bytes per position)
+    size_t total = 0;
+    if (encode_batch_packed(ws, src, false, P, bs, packed, 8 * ws.cap_s, &total, dump) != 0)
+        return -1;
+    if (total > *dst_len) {
+        set_error("batch frames (%zu bytes) exceed the destination capacity (%zu)", total, *dst_len);
+        return -1;
+    }
     SALZ_HIP(hipMemcpyAsync(dst, packed, total, hipMemcpyDeviceToHost, ws.stream));
     SALZ_HIP(hipStreamSynchronize(ws.stream));
     *dst_len = total;
@@ -718,6 +747,31 @@ int salz_gpu_encode_batch(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_len,
     return encode_batch_locked(ctx->ws, src, src_len, block_size, dst, dst_len);
 }
 
+int salz_gpu_encode_batch_device(salz_gpu_ctx *ctx, const uint8_t *d_src, size_t src_len,
+                                 size_t block_size, uint8_t *d_dst, size_t dst_cap, size_t *dst_len,
+                                 void *stream)
+{
+    if (!ctx || !d_src || !d_dst || !dst_len || block_size == 0) {
+        set_error("invalid argument");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    Workspace &ws = ctx->ws;
+    hipStream_t saved = ws.stream;
+    if (stream)
+        ws.stream = static_cast<hipStream_t>(stream);
+    size_t total = 0;
+    int rc = encode_batch_packed(ws, d_src, true, src_len, block_size, d_dst, dst_cap, &total, nullptr);
+    if (rc == 0 && hipStreamSynchronize(ws.stream) != hipSuccess) {
+        set_error("stream synchronize failed");
+        rc = -1;
+    }
+    ws.stream = saved;
+    if (rc == 0)
+        *dst_len = total;
+    return rc;
+}
+
 // Test hook: read workspace scratch left by the last encode (0: ws.sa = emission's chunk
 // entries, 1: ws.g64 = emission's chunk bit / byte starts), `count` u32 / u64 words from `off`.
 int salz_debug_ws_read(salz_gpu_ctx *ctx, int which, size_t off, size_t count, void *out)
@@ -808,15 +862,21 @@ struct BatchPlan {
 
 BatchPlan batch_plan(size_t block_size)
 {
+    // Blocks of up to 4 MiB share passes: 8 MiB batches, 4 in flight per device (1 MiB blocks
+    // 864 -> 2292 MB/s, 32 KiB blocks 122 -> 1746; profiles/r02h_*, r02i_*). From 8 MiB a
+    // block fills the GPU on its own and four concurrent single-block passes beat batches
+    // (16 MiB mixed blocks: 2045 vs 1625 with 64 MiB batches).
     const char *e = getenv("SALZ_BATCH_BYTES");  // tuning / tests
     const long long v = e ? atoll(e) : 0;
-    const size_t kBatchBytes = v > 0 ? (size_t)v : (size_t)64 << 20;
-    if (block_size % 512 == 0) {
+    const size_t kBatchBytes = v > 0 ? (size_t)v : (size_t)8 << 20;
+    const char *se = getenv("SALZ_SLOTS");  // tuning: encoder contexts per device
+    const int slots = se ? atoi(se) : 0;
+    if (block_size % 512 == 0 && (block_size <= (4u << 20) || v > 0)) {
         size_t bpb = kBatchBytes / block_size;
         bpb = bpb < 1 ? 1 : bpb > kMaxBatchBlocks ? kMaxBatchBlocks : bpb;
-        return {bpb, block_size >= (256u << 20) ? 1 : 2};
+        return {bpb, slots > 0 ? slots : 4};
     }
-    return {1, block_size >= (256u << 20) ? 2 : block_size >= (1u << 20) ? 4 : kMaxSlots};
+    return {1, slots > 0 ? slots : block_size >= (256u << 20) ? 2 : block_size >= (1u << 20) ? 4 : kMaxSlots};
 }
 
 size_t frames_cap(size_t bpb, size_t block_size)
