@@ -475,15 +475,24 @@ __global__ __launch_bounds__(256) void k_pack_frames(const uint8_t *__restrict__
 
 // A batch: every block encoded in one pipeline pass and its frames packed (u32 length +
 // stream per block) into device memory `packed` (capacity packed_cap); *total = bytes.
+// Grow the workspace (reallocating every buffer) until a batch of P bytes in blocks of bs fits.
+static int ensure_batch_room(Workspace &ws, size_t P, size_t bs)
+{
+    const size_t nb = bs >= P ? 1 : (P + bs - 1) / bs;
+    if (P > ws.cap_N || nb * batch_stride(bs < P ? bs : P) > ws.out_cap)
+        return workspace_alloc(ws, ws.device, P > ws.cap_N ? P : ws.cap_N);
+    return 0;
+}
+
 static int encode_batch_packed(Workspace &ws, const uint8_t *src, bool src_dev, size_t P, size_t bs,
                                uint8_t *packed, size_t packed_cap, size_t *total,
                                const salz_gpu_dump *dump)
 {
     const size_t nb = bs >= P ? 1 : (P + bs - 1) / bs;
     const size_t stride = batch_stride(bs < P ? bs : P);
-    if (P > ws.cap_N || nb * stride > ws.out_cap) {
-        if (workspace_alloc(ws, ws.device, P > ws.cap_N ? P : ws.cap_N) != 0)
-            return -1;
+    if (P > ws.cap_N || nb * stride > ws.out_cap) {  // callers grow the workspace beforehand
+        set_error("batch of %zu bytes exceeds the context's workspace", P);
+        return -1;
     }
     // Every block gets the reference CLI's output capacity, salz_encoded_len_max(block size)
     // (programs/salzcli.c:130, :156), so a block the reference fails on (an incompressible
@@ -526,6 +535,8 @@ static int encode_batch_packed(Workspace &ws, const uint8_t *src, bool src_dev, 
 static int encode_batch_locked(Workspace &ws, const uint8_t *src, size_t P, size_t bs, uint8_t *dst,
                                size_t *dst_len, const salz_gpu_dump *dump = nullptr)
 {
+    if (ensure_batch_room(ws, P, bs) != 0)
+        return -1;
     uint8_t *packed = reinterpret_cast<uint8_t *>(ws.keyB);  // free after emission (8 bytes per position)
     size_t total = 0;
     if (encode_batch_packed(ws, src, false, P, bs, packed, 8 * ws.cap_s, &total, dump) != 0)
@@ -757,6 +768,8 @@ int salz_gpu_encode_batch_device(salz_gpu_ctx *ctx, const uint8_t *d_src, size_t
     }
     std::lock_guard<std::mutex> lk(ctx->mu);
     Workspace &ws = ctx->ws;
+    if (ensure_batch_room(ws, src_len, block_size) != 0)  // (before the stream swap: it recreates ws)
+        return -1;
     hipStream_t saved = ws.stream;
     if (stream)
         ws.stream = static_cast<hipStream_t>(stream);
