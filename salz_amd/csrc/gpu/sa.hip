@@ -25,8 +25,9 @@
 //   scan        of the per-wave head counts; k_headpos -> group ids and head index per group
 //   k_grpsum /  groups of size >= 2 survive; exclusive scans (per-wave sums, then per group)
 //   k_grpscan   pack (compact start, new gid) and (start in the extracted array, large-group id)
-//   k_commit    rank update for every active suffix (in large rounds the upper text half
-//               through k_rank_upper), SA write for singletons, compaction
+//   k_commit    rank update for every active suffix (in large rounds staged by text range
+//               and applied window by window: k_rank_stage / k_rank_apply), SA write for
+//               singletons, compaction
 //   k_keys      next round's keys: gid << kb | rank[i + h]
 #include "internal.hpp"
 
@@ -229,9 +230,9 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     // are unchanged; every other rank (and all of round 0) is written.
     const bool same = !round0 && (hp == 0 || (key[hp - 1] >> kb_old) != (key[hp] >> kb_old));
     // rank[i] is a random 4-byte scatter (a read-modify-write of a whole HBM burst). Large
-    // rounds split it by text range: this kernel writes the ranks of i < ihi and leaves the
-    // others, in list order, to k_rank_upper, so the rank lines each pass writes fit in the
-    // 256 MB Infinity Cache and are merged there.
+    // rounds write only the ranks of i < ihi here and leave every update in list order in
+    // `later` for the split passes (k_rank_upper) or the staged scatter (k_rank_stage /
+    // k_rank_apply); small ones write rank directly (ihi = ~0, no `later`).
     const uint32_t rv = same ? 0xffffffffu : hp + o + 1u;
     if (!same && i < ihi)
         rank[i] = rv;
@@ -359,6 +360,69 @@ __global__ void k_dead_ranks(Blocks bl, uint32_t *__restrict__ rank)
         return;
     const uint32_t b = x >> 3;
     rank[b * bl.bs + bl.bs - 8u + (x & 7u)] = 0u;
+}
+
+// Staged rank scatter. k_commit leaves the new ranks in list order (later[c], 0xffffffff when
+// unchanged); the list's suffixes are in random text order, so writing rank[i] directly is a
+// 4-byte scatter over the whole rank array (n * 4 bytes, beyond the 256 MB Infinity Cache on
+// large blocks). Instead k_rank_stage bins the updates by text range (2^rlog positions = 4 MB
+// of rank per range) into per-range runs (LDS counts, one global atomic per range and tile),
+// and k_rank_apply writes them range by range, XCD-aware, so the writes in flight on one XCD
+// fall in one L2-sized window of the rank array (the ANSV staging of ansv.hip, for ranks).
+constexpr uint32_t kStageTile = 4096;
+constexpr uint32_t kStageRanges = 1024;
+
+__global__ __launch_bounds__(kT) void k_rank_stage(const uint32_t *__restrict__ val,
+                                                   const uint32_t *__restrict__ later, uint32_t m,
+                                                   uint32_t rlog, uint32_t *__restrict__ rfill,
+                                                   uint2 *__restrict__ stage)
+{
+    __shared__ uint32_t cnt[kStageRanges];
+    constexpr uint32_t kItems = kStageTile / kT;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t r = tid; r < kStageRanges; r += kT)
+        cnt[r] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * kStageTile;
+    uint32_t iv[kItems], rv[kItems], loc[kItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; j++) {  // unconditional loads (clamped entry)
+        const size_t c = base + (size_t)j * kT + tid;
+        const size_t cc = c < m ? c : 0;
+        iv[j] = val[cc];
+        rv[j] = later[cc];
+        if (c >= m)
+            rv[j] = 0xffffffffu;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; j++)
+        loc[j] = rv[j] != 0xffffffffu ? atomicAdd(&cnt[iv[j] >> rlog], 1u) : 0u;
+    __syncthreads();
+    for (uint32_t r = tid; r < kStageRanges; r += kT)
+        if (cnt[r])
+            cnt[r] = (r << rlog) + atomicAdd(&rfill[r], cnt[r]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kItems; j++)
+        if (rv[j] != 0xffffffffu)
+            stage[cnt[iv[j] >> rlog] + loc[j]] = make_uint2(iv[j], rv[j]);
+}
+
+// Workgroup g runs on XCD g mod 8 (round-robin dispatch, a speed assumption only): XCD x takes
+// text ranges x, x + 8, ... in turn, 256 staged updates per workgroup.
+__global__ __launch_bounds__(kT) void k_rank_apply(const uint2 *__restrict__ stage,
+                                                   const uint32_t *__restrict__ rfill, uint32_t rlog,
+                                                   uint32_t nranges, uint32_t *__restrict__ rank)
+{
+    const uint32_t g = blockIdx.x, tiles = 1u << (rlog - 8);
+    const uint32_t k = g >> 3, r = (g & 7u) + 8u * (k >> (rlog - 8));
+    if (r >= nranges)
+        return;
+    const uint32_t x = (k & (tiles - 1u)) * kT + threadIdx.x;
+    if (x >= rfill[r])
+        return;
+    const uint2 e = stage[((size_t)r << rlog) + x];
+    rank[e.x] = e.y;
 }
 
 // Later passes of a split rank scatter: ranks of suffixes in [ilo, ihi), from k_commit's list.
@@ -716,8 +780,6 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
     static const bool dbg_rounds = getenv("SALZ_CHECK_ROUNDS") != nullptr;
     const char *lcp_env = getenv("SALZ_LCP_SA");  // tests: "0" forces the Phi/PLCP stage
     ws.lcps_ok = !lcp_env || atoi(lcp_env) != 0;
-    static const bool split_on = !getenv("SALZ_COMMIT_SPLIT") || atoi(getenv("SALZ_COMMIT_SPLIT")) > 1;
-    static const uint32_t split_ratio = getenv("SALZ_SPLIT_RATIO") ? (uint32_t)atoi(getenv("SALZ_SPLIT_RATIO")) : 4;
     SALZ_HIP(hipMemsetAsync(ws.rank + n, 0, sizeof(uint32_t), st));  // rank[n] = 0
     if (bl.nb > 1) {
         hipLaunchKernelGGL(k_dead_ranks, dim3(grid_for(8u * (bl.nb - 1u), kT)), dim3(kT), 0, st, bl, ws.rank);
@@ -832,9 +894,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
             return -1;
         hipLaunchKernelGGL(k_headpos, dim3(grid_for(m, kT)), dim3(kT), 0, st, hb, m, headpos);
         SALZ_LAUNCH_CHECK();
-        // The host needs G only to choose the split rank scatter (large rounds) and for the
-        // debug checks; other rounds do not wait for it.
-        const bool need_G = dbg_rounds || verbose || (m >= (32u << 20) && split_on);
+        // The host needs G only for the debug checks; no round waits for it.
+        const bool need_G = dbg_rounds || verbose;
         uint32_t G = 0;
         if (need_G) {
             if (read_scalars(ws, 0, 64, "sa.G") != 0)
@@ -867,24 +928,48 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
             hipLaunchKernelGGL(k_dbg_gsc, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, gsc, G, ws.hscal[8], derr);
             SALZ_LAUNCH_CHECK();
         }
-        // Large rounds: the rank scatter in text-range passes of at most ~200 MB of rank array
-        // each (the Infinity Cache holds 256 MB; k_commit comment). Worth it where many ranks
-        // change: round 0, a round that multiplied the groups, or any round once the rank
-        // array is past 400 MB (a scatter over 1 GB costs ~3x one over 200 MB,
-        // profiles/r01t_scatter_bench.txt; Fibonacci 256 MiB: SA 691 -> 657 ms).
+        // Rank updates (SALZ_RANK_MODE=direct|split|stage for experiments):
+        //   direct  k_commit writes rank[i] (small rounds);
+        //   split   k_commit writes the lower text part, k_rank_upper passes the rest, parts of
+        //           at most ~200 MB of rank array each (Infinity-Cache-sized windows);
+        //   stage   every update binned by text range (k_rank_stage) and applied window by
+        //           window (k_rank_apply, XCD-aware), for rank arrays far past the cache.
+        // Default: up to 512 MB of ranks split from 32M updates, above it stage from 4M, 1 MB
+        // windows (Fibonacci 256 MiB: SA 554 -> 505 ms; text 100 MB: SA 24.8 ms split, 25.3
+        // staged; profiles/r02l_*).
+        static const char *rank_mode = getenv("SALZ_RANK_MODE");
+        static const uint32_t rlog_min = getenv("SALZ_RANK_RLOG") ? (uint32_t)atoi(getenv("SALZ_RANK_RLOG")) : 18;
+        int mode = (uint64_t)n * 4 <= (512ull << 20) ? (m >= (32u << 20) ? 1 : 0) : (m >= (4u << 20) ? 2 : 0);
+        if (rank_mode)
+            mode = !strcmp(rank_mode, "direct") ? 0 : !strcmp(rank_mode, "split") ? 1 : 2;
         const uint32_t parts_all = (uint32_t)(((uint64_t)n * 4 + (200u << 20) - 1) / (200u << 20));
-        const uint32_t ratio = parts_all >= 3 ? 1u : split_ratio;
-        const bool many = round0 || (uint64_t)G >= (uint64_t)ratio * G_act;
-        const uint32_t parts = (m >= (32u << 20) && split_on && many) ? (parts_all > 1 ? parts_all : 2) : 1;
+        const uint32_t parts = mode == 1 ? (parts_all > 1 ? parts_all : 2) : 1;
         const uint32_t span = (uint32_t)(((uint64_t)n + parts - 1) / parts);
         uint32_t *later = reinterpret_cast<uint32_t *>(Kx);  // free until k_keys
+        const uint32_t ihi = mode == 0 ? 0xffffffffu : mode == 1 ? span : 0u;
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, headpos,
                            gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, nsa, kb_old,
-                           round0, derr, parts > 1 ? span : 0xffffffffu, parts > 1 ? later : nullptr);
+                           round0, derr, ihi, mode ? later : nullptr);
         SALZ_LAUNCH_CHECK();
         for (uint32_t q = 1; q < parts; q++) {
             hipLaunchKernelGGL(k_rank_upper, dim3(grid_for(m, kT)), dim3(kT), 0, st, V, later, m,
                                q * span, q + 1 == parts ? 0xffffffffu : (q + 1) * span, ws.rank);
+            SALZ_LAUNCH_CHECK();
+        }
+        if (mode == 2) {
+            uint32_t rlog = rlog_min < 9 ? 9 : rlog_min;
+            while ((((uint64_t)n - 1) >> rlog) + 1 > kStageRanges)
+                rlog++;
+            const uint32_t nranges = (uint32_t)((((uint64_t)n - 1) >> rlog) + 1);
+            uint32_t *rfill = ws.radix_counts;  // free outside the radix sorts
+            uint2 *stage = reinterpret_cast<uint2 *>(ws.pst);  // free after this round's sort
+            SALZ_HIP(hipMemsetAsync(rfill, 0, kStageRanges * sizeof(uint32_t), st));
+            hipLaunchKernelGGL(k_rank_stage, dim3(grid_for(m, kStageTile)), dim3(kT), 0, st, V, later, m,
+                               rlog, rfill, stage);
+            SALZ_LAUNCH_CHECK();
+            const uint32_t agrid = 8u * ((nranges + 7u) / 8u) << (rlog - 8);
+            hipLaunchKernelGGL(k_rank_apply, dim3(agrid), dim3(kT), 0, st, stage, rfill, rlog, nranges,
+                               ws.rank);
             SALZ_LAUNCH_CHECK();
         }
         if (read_scalars(ws, 0, 256, "sa.m") != 0)
