@@ -178,6 +178,18 @@ __host__ __device__ __forceinline__ uint32_t init_suffix(size_t c, const Blocks 
     return full * (g.nb == 1 ? 0u : g.bs) + (cc - full * per);
 }
 
+// Round-0 keys of the suffix sorter. Raw (bits == 0): the first 8 bytes, big-endian, bytes past
+// the suffix's end zero (short suffixes are ordered by the initial list order). Alphabet
+// (bits > 0, a text with at most 127 distinct bytes): every byte mapped to its rank 1..sigma
+// in the block's alphabet (order-preserving; 0 = past the end, below every symbol), k symbols
+// of `bits` bits packed big-endian into the low k * bits bits: 7-bit text gives 8 symbols in
+// 56 bits (7 radix passes instead of 8), a binary text 32 symbols (round 0 reaches depth 32).
+struct Alpha {
+    uint32_t bits;  // 0: raw bytes
+    uint32_t k;     // symbols per key (the depth round 0 sorts to)
+    uint8_t code[256];
+};
+
 // Unaligned little-endian 8-byte load from an 8-byte-aligned, padded byte buffer.
 __device__ __forceinline__ uint64_t load_u64_any(const uint8_t *base, size_t pos)
 {
@@ -187,6 +199,91 @@ __device__ __forceinline__ uint64_t load_u64_any(const uint8_t *base, size_t pos
     const unsigned sh = (unsigned)(pos & 7) * 8u;
     const uint64_t a = w[0], b = w[1];
     return (a >> sh) | ((b << 1) << (63u - sh));
+}
+
+}  // namespace salz
+
+namespace salz {
+
+// Round-0 key of suffix i whose suffix text ends at e (see Alpha); `code` is the symbol table
+// (a.code, or a copy in LDS: kernel-argument memory indexed per lane is slow).
+__device__ __forceinline__ uint64_t round0_key(const uint8_t *T, uint32_t i, uint32_t e, const Alpha &a,
+                                               const uint8_t *code)
+{
+    const uint32_t left = e - i;
+    if (a.bits == 0) {
+        uint64_t w = load_u64_any(T, i);
+        if (left < 8)
+            w &= (1ull << (8u * left)) - 1ull;
+        return __builtin_bswap64(w);
+    }
+    uint64_t key = 0;
+    if (a.k == 8) {  // the usual text case: one load, 8 table lookups, unrolled
+        const uint64_t w = load_u64_any(T, i);
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t c = j < left ? code[(w >> (8 * j)) & 255u] : 0u;
+            key = (key << a.bits) | c;
+        }
+        return key;
+    }
+    for (uint32_t j0 = 0; j0 < a.k; j0 += 8) {
+        const uint64_t w = load_u64_any(T, (size_t)i + j0);
+        const uint32_t cnt = a.k - j0 < 8 ? a.k - j0 : 8u;
+        for (uint32_t j = 0; j < cnt; j++) {
+            const uint32_t c = j0 + j < left ? code[(w >> (8 * j)) & 255u] : 0u;
+            key = (key << a.bits) | c;
+        }
+    }
+    return key;
+}
+
+__device__ __forceinline__ uint64_t round0_key(const uint8_t *T, uint32_t i, uint32_t e, const Alpha &a)
+{
+    return round0_key(T, i, e, a, a.code);
+}
+
+// The same from the text already mapped to symbols (Tm[i] = a.code[T[i]], zero padded): no
+// table lookups, just the packing (the radix passes that build round 0's keys use this).
+__device__ __forceinline__ uint64_t round0_key_mapped(const uint8_t *Tm, uint32_t i, uint32_t e, const Alpha &a)
+{
+    const uint32_t left = e - i;
+    uint64_t key = 0;
+    if (a.k == 8) {  // the usual text case: straight-line, so the loads of a thread's items batch
+        uint64_t w = load_u64_any(Tm, i);
+        if (left < 8)
+            w &= (1ull << (8u * left)) - 1ull;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+            key = (key << a.bits) | ((w >> (8 * j)) & 255u);
+        return key;
+    }
+    for (uint32_t j0 = 0; j0 < a.k; j0 += 8) {
+        uint64_t w = load_u64_any(Tm, (size_t)i + j0);
+        if (left < j0 + 8)
+            w = left <= j0 ? 0ull : w & ((1ull << (8u * (left - j0))) - 1ull);
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++)
+            if (j0 + j < a.k)
+                key = (key << a.bits) | ((w >> (8 * j)) & 255u);
+    }
+    return key;
+}
+
+// Copy of the symbol table in LDS (every thread of the workgroup calls it, then a barrier).
+__device__ __forceinline__ void load_codes(uint8_t *lds, const Alpha &a)
+{
+    for (uint32_t c = threadIdx.x; c < 256; c += blockDim.x)
+        lds[c] = a.code[c];
+}
+
+// Leading equal symbols of two round-0 keys (x = key_a ^ key_b, not both equal).
+__device__ __forceinline__ uint32_t round0_lcp(uint64_t x, const Alpha &a)
+{
+    if (a.bits == 0)
+        return x ? (uint32_t)__builtin_clzll(x) >> 3 : 8u;
+    const uint32_t kb = a.k * a.bits;
+    return x ? ((uint32_t)__builtin_clzll(x) - (64u - kb)) / a.bits : a.k;
 }
 
 }  // namespace salz

@@ -113,7 +113,8 @@ constexpr int kRadixTile = 4096;
 // gets extra passes on the block of each value, so the result is ordered by (block, key).
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
-                     const uint8_t *text = nullptr, const Blocks *blocks = nullptr);
+                     const uint8_t *text = nullptr, const Blocks *blocks = nullptr,
+                     const Alpha *alpha = nullptr);
 
 // Blocks per batch (one pipeline pass over several blocks, common.hpp Blocks).
 constexpr uint32_t kMaxBatchBlocks = 4096;

@@ -28,15 +28,14 @@ constexpr int kThreads = 256;
 struct TextSrc {
     const uint8_t *T;  // padded text
     Blocks g;
+    Alpha a;
 };
 
-__device__ __forceinline__ uint64_t init_key(const TextSrc &t, uint32_t i)
+// (alphabet keys: t.T is the text mapped to symbols, round0_key_mapped)
+__device__ __forceinline__ uint64_t init_key(const TextSrc &t, uint32_t i, const uint8_t *code)
 {
-    uint64_t w = load_u64_any(t.T, i);
-    const uint32_t left = t.g.end(i) - i;
-    if (left < 8)
-        w &= (1ull << (8u * left)) - 1ull;
-    return __builtin_bswap64(w);
+    (void)code;
+    return t.a.bits ? round0_key_mapped(t.T, i, t.g.end(i), t.a) : round0_key(t.T, i, t.g.end(i), t.a);
 }
 
 // digit source of a pass: 0 = key bits, 1 = key bits of text-built pairs, 2 = block of value
@@ -81,7 +80,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
 #pragma unroll
         for (int j = 0; j < kItems; j++) {
             const size_t i = (size_t)j * kThreads + tid;
-            kk[j] = init_key(txt, init_suffix(i < left ? base + i : 0, txt.g));
+            kk[j] = init_key(txt, init_suffix(i < left ? base + i : 0, txt.g), nullptr);
         }
 #pragma unroll
         for (int j = 0; j < kItems; j++)
@@ -198,7 +197,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
         bool ok = i < m;
         if (kMode == 1) {  // unconditional text loads (clamped entry)
             const uint32_t sfx = init_suffix(ok ? i : 0, txt.g);
-            const uint64_t kk = init_key(txt, sfx);
+            const uint64_t kk = init_key(txt, sfx, nullptr);
             k[j] = ok ? kk : 0ull;
             v[j] = sfx;
         } else {
@@ -336,7 +335,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
 
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
-                     const uint8_t *text, const Blocks *blocks)
+                     const uint8_t *text, const Blocks *blocks, const Alpha *alpha)
 {
     if (m <= 1 || bit_hi <= bit_lo)
         return 0;
@@ -356,7 +355,9 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     for (int pass = 0; pass < passes; pass++) {
         const int mode = pass >= passes_key ? 2 : (text && pass == 0) ? 1 : 0;
         const int shift = mode == 2 ? 8 * (pass - passes_key) : bit_lo + 8 * pass;
-        const TextSrc txt{text, g};
+        TextSrc txt{text, g, Alpha{}};
+        if (alpha)
+            txt.a = *alpha;
         if (mode == 1)
             hipLaunchKernelGGL(k_radix_hist<1>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
                                shift, ws.radix_counts, ntiles, txt);

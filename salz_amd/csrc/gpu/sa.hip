@@ -46,19 +46,45 @@ constexpr uint32_t kSegCap = 4096;   // LDS slots: a window's groups span < kSeg
 constexpr int kSegThreads = 256;
 static_assert(kSegCap == 4096, "12-bit slot index in the LDS sort key");
 
-__global__ void k_sa_init(const uint8_t *__restrict__ T, Blocks g, uint64_t *__restrict__ key,
+__global__ void k_sa_init(const uint8_t *__restrict__ T, Blocks g, Alpha a, uint64_t *__restrict__ key,
                           uint32_t *__restrict__ val)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= g.nsa())
         return;
     const uint32_t i = init_suffix(c, g);
-    uint64_t w = load_u64_any(T, i);
-    uint32_t left = g.end(i) - i;
-    if (left < 8)
-        w &= (1ull << (8u * left)) - 1ull;
-    key[c] = __builtin_bswap64(w);
+    key[c] = round0_key(T, i, g.end(i), a);
     val[c] = i;
+}
+
+// Tm[i] = symbol of T[i] (and 64 zero bytes of padding past P), for round0_key_mapped.
+__global__ void k_map_text(const uint8_t *__restrict__ T, size_t P, Alpha a, uint8_t *__restrict__ Tm)
+{
+    __shared__ uint8_t code[256];
+    load_codes(code, a);
+    __syncthreads();
+    for (size_t i = ((size_t)blockIdx.x * kT + threadIdx.x) * 16; i < P + 64; i += (size_t)gridDim.x * kT * 16) {
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            Tm[i + j] = i + j < P ? code[T[i + j]] : 0u;
+    }
+}
+
+// Byte presence of the text (the alphabet for round 0's keys): 8 words of 32 bits.
+__global__ void k_alpha_presence(const uint8_t *__restrict__ T, size_t P, uint32_t *__restrict__ words)
+{
+    __shared__ uint32_t w[8];
+    if (threadIdx.x < 8)
+        w[threadIdx.x] = 0;
+    __syncthreads();
+    for (size_t i = (size_t)blockIdx.x * kT + threadIdx.x; i < P; i += (size_t)gridDim.x * kT) {
+        const uint32_t c = T[i];
+        if (!(w[c >> 5] & (1u << (c & 31))))
+            atomicOr(&w[c >> 5], 1u << (c & 31));
+    }
+    __syncthreads();
+    if (threadIdx.x < 8 && w[threadIdx.x])
+        atomicOr(&words[threadIdx.x], w[threadIdx.x]);
 }
 
 // Group-head flags travel as one 64-bit ballot per wave of the sorted list (hmask) plus its
@@ -79,7 +105,7 @@ __device__ __forceinline__ void put_heads(HeadBits hb, size_t c, uint32_t m, boo
 }
 
 __global__ void k_heads(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
-                        uint32_t m, Blocks bl, int round0, HeadBits hb)
+                        uint32_t m, Blocks bl, uint32_t h0, int round0, HeadBits hb)
 {
     const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if ((c & ~(size_t)63) >= m)
@@ -91,7 +117,7 @@ __global__ void k_heads(const uint64_t *__restrict__ key, const uint32_t *__rest
     const uint32_t v0 = val[cp], v1 = val[cc];
     bool h = cc == 0 || k0 != k1;
     if (round0 && !h)  // short suffixes are singletons; a batch's blocks never share a group
-        h = (bl.end(v1) - v1) < 8u || (bl.end(v0) - v0) < 8u || bl.blk(v0) != bl.blk(v1);
+        h = (bl.end(v1) - v1) < h0 || (bl.end(v0) - v0) < h0 || bl.blk(v0) != bl.blk(v1);
     put_heads(hb, c, m, in && h);
 }
 
@@ -274,7 +300,7 @@ constexpr uint32_t kLcpMaxHk = 4096;
 // k_heads with the LCP of every new head (writes the head ballots like k_heads).
 __global__ __launch_bounds__(kT) void k_heads_lcp(
     const uint64_t *__restrict__ K, const uint32_t *__restrict__ V, HeadBits hb,
-    const uint32_t *__restrict__ off_old, uint32_t m, Blocks bl, int kb_old, uint32_t hk, int round0,
+    const uint32_t *__restrict__ off_old, uint32_t m, Blocks bl, Alpha a, int kb_old, uint32_t hk, int round0,
     const uint8_t *__restrict__ T, uint32_t *__restrict__ lcps, uint32_t *err)
 {
     const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
@@ -286,8 +312,9 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
     bool head = c == 0 || k0 != k1;
     const uint32_t e1 = bl.end(v1);  // end of v1's suffix text (its block's)
     const bool other_block = bl.blk(v0) != bl.blk(v1);
+    const uint32_t h0 = a.bits ? a.k : 8u;  // round 0's depth
     if (round0 && !head)
-        head = (e1 - v1) < 8u || (bl.end(v0) - v0) < 8u || other_block;
+        head = (e1 - v1) < h0 || (bl.end(v0) - v0) < h0 || other_block;
     put_heads(hb, c, m, in && head);
     const uint32_t g1 = round0 ? 0u : (uint32_t)(k1 >> kb_old);
     const uint32_t o = round0 ? 0u : off_old[g1];
@@ -298,8 +325,7 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
         if (round0) {
             uint32_t l = 0;
             if (c > 0 && !other_block) {  // a block's first suffix: LCP 0
-                const uint64_t x = k0 ^ k1;
-                l = x ? (uint32_t)__builtin_clzll(x) >> 3 : 8u;
+                l = round0_lcp(k0 ^ k1, a);
                 l = umin_(l, e1 - i);
                 l = umin_(l, e1 - j);
             }
@@ -624,7 +650,7 @@ __global__ void k_dbg_sorted(const uint64_t *__restrict__ K, uint32_t m, uint32_
 
 __global__ void k_dbg_pairs(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
                             const uint32_t *__restrict__ rank, const uint8_t *__restrict__ T,
-                            uint32_t m, Blocks bl, uint32_t h, int kb, int round0, uint32_t *err)
+                            uint32_t m, Blocks bl, Alpha a, uint32_t h, int kb, int round0, uint32_t *err)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
@@ -636,11 +662,7 @@ __global__ void k_dbg_pairs(const uint64_t *__restrict__ K, const uint32_t *__re
     }
     uint64_t want;
     if (round0) {
-        uint64_t w = load_u64_any(T, i);
-        const uint32_t left = bl.end(i) - i;
-        if (left < 8)
-            w &= (1ull << (8u * left)) - 1ull;
-        want = __builtin_bswap64(w);
+        want = round0_key(T, i, bl.end(i), a);
         const uint64_t got = K[c];
         if (got != want) {
             atomicOr(err, 0x20000u);
@@ -780,6 +802,41 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
     static const bool dbg_rounds = getenv("SALZ_CHECK_ROUNDS") != nullptr;
     const char *lcp_env = getenv("SALZ_LCP_SA");  // tests: "0" forces the Phi/PLCP stage
     ws.lcps_ok = !lcp_env || atoi(lcp_env) != 0;
+    // Round 0's alphabet: texts of at most 127 distinct bytes get compacted keys (Alpha,
+    // common.hpp); SALZ_ALPHA=0 keeps raw 8-byte keys (tests run both).
+    Alpha alpha{};
+    const bool alpha_on = !getenv("SALZ_ALPHA") || atoi(getenv("SALZ_ALPHA")) != 0;
+    if (alpha_on && n >= 64) {
+        uint32_t *words = reinterpret_cast<uint32_t *>(ws.dscal) + 240;
+        SALZ_HIP(hipMemsetAsync(words, 0, 8 * sizeof(uint32_t), st));
+        const size_t P = (size_t)n + 8;
+        hipLaunchKernelGGL(k_alpha_presence, dim3(grid_for(P, kT * 16) < 2048 ? grid_for(P, kT * 16) : 2048),
+                           dim3(kT), 0, st, ws.text, P, words);
+        SALZ_LAUNCH_CHECK();
+        if (read_scalars(ws, 960, 32, "sa.alpha") != 0)
+            return -1;
+        const uint32_t *pw = reinterpret_cast<const uint32_t *>(ws.hscal) + 240;
+        uint32_t sigma = 0;
+        for (int c = 0; c < 256; c++)
+            if (pw[c >> 5] & (1u << (c & 31)))
+                alpha.code[c] = (uint8_t)++sigma;
+        const uint32_t bits = (uint32_t)bit_width(sigma);  // codes 1..sigma, 0 = past the end
+        if (bits <= 7) {
+            alpha.bits = bits;
+            alpha.k = bits >= 5 ? 8u : 64u / bits;  // 8 symbols in fewer passes, or more depth
+        }
+    }
+    const uint32_t h0 = alpha.bits ? alpha.k : 8u;
+    // The text mapped to symbols for the text-sourced radix pass (u1 is free until round 0's
+    // group sums): one byte per position, zero padded.
+    uint8_t *tmapped = nullptr;
+    if (alpha.bits) {
+        tmapped = reinterpret_cast<uint8_t *>(ws.u1);
+        const size_t P = (size_t)n + 8;
+        hipLaunchKernelGGL(k_map_text, dim3(grid_for(P + 64, kT * 16)), dim3(kT), 0, st, ws.text, P, alpha,
+                           tmapped);
+        SALZ_LAUNCH_CHECK();
+    }
     SALZ_HIP(hipMemsetAsync(ws.rank + n, 0, sizeof(uint32_t), st));  // rank[n] = 0
     if (bl.nb > 1) {
         hipLaunchKernelGGL(k_dead_ranks, dim3(grid_for(8u * (bl.nb - 1u), kT)), dim3(kT), 0, st, bl, ws.rank);
@@ -790,12 +847,12 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
     // sort has nothing to do and would leave them unwritten).
     const bool text_first = !dbg_rounds && nsa > 1;
     if (!text_first) {
-        hipLaunchKernelGGL(k_sa_init, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.text, bl, K, V);
+        hipLaunchKernelGGL(k_sa_init, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.text, bl, alpha, K, V);
         SALZ_LAUNCH_CHECK();
     }
     if (dbg_rounds && bl.nb == 1) {
         hipLaunchKernelGGL(k_dbg_pairs, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, K, V, ws.rank, ws.text, nsa, bl,
-                           0u, 0, 1, derr);
+                           alpha, 0u, 0, 1, derr);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 512, "sa.init") != 0)
             return -1;
@@ -807,7 +864,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
         }
     }
 
-    uint32_t m = nsa, h = 8, G_act = 0, GL = 0, mL = 0;
+    uint32_t m = nsa, h = h0, G_act = 0, GL = 0, mL = 0;
     int kb_old = 0, round0 = 1;
     const int kb = bit_width(n);
     ws.stats.sa_rounds = 0;
@@ -827,7 +884,9 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
                 set_error("suffix sort: a batch of blocks needs the text-built first pass");
                 return -1;
             }
-            if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, 64, ws, st, text_first ? ws.text : nullptr, &bl) != 0)
+            const int key_bits = alpha.bits ? (int)(alpha.k * alpha.bits) : 64;
+            const uint8_t *src_text = !text_first ? nullptr : tmapped ? tmapped : ws.text;
+            if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, key_bits, ws, st, src_text, &bl, &alpha) != 0)
                 return -1;
         } else {
             // Global sort of every active suffix on (group, rank) vs. LDS sort of the small
@@ -878,16 +937,16 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
             hipLaunchKernelGGL(k_dbg_sorted, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, m, derr, 0x1000u);
             SALZ_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_dbg_pairs, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, ws.rank, ws.text, m,
-                               bl, h / 2, kb, round0, derr);
+                               bl, alpha, h / 2, kb, round0, derr);
             SALZ_LAUNCH_CHECK();
         }
         if (ws.lcps_ok && !round0 && h / 2 > kLcpMaxHk)
             ws.lcps_ok = false;  // long repeats: the PLCP stage is cheaper than these compares
         if (ws.lcps_ok)
             hipLaunchKernelGGL(k_heads_lcp, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, offo, m, bl,
-                               kb_old, round0 ? 0u : h / 2, round0, ws.text, ws.lcps, derr);
+                               alpha, kb_old, round0 ? 0u : h / 2, round0, ws.text, ws.lcps, derr);
         else
-            hipLaunchKernelGGL(k_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m, bl, round0,
+            hipLaunchKernelGGL(k_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m, bl, h0, round0,
                                hb);
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u32(hb.wcnt, hb.wpre, ((size_t)m + 63) / 64, false, d32 + 0, ws, st) != 0)

@@ -233,14 +233,19 @@ def test_encode_blocks_container(salz, block, size):
     assert salz.decode_blocks(got, size) == src.tobytes()
 
 
+@pytest.mark.parametrize("keys", ["1", "0"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
                                                ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
-                                               ("runs", 120000, 0, 0), ("zeros", 70000, 0, 0)])
-def test_suffix_sort_modes(ctx, monkeypatch, mode, kind, n, seed, alpha):
+                                               ("smx", 150000, 3, 20), ("runs", 120000, 0, 0),
+                                               ("zeros", 70000, 0, 0)])
+def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
     """Both doubling-round sorts (global radix on (group, rank); LDS sort of small groups +
-    extracted large groups) give the unique suffix array."""
+    extracted large groups), with round-0 keys from the compacted alphabet (SALZ_ALPHA=1, the
+    default for texts of <= 127 distinct bytes: 2 to 32 symbols per key) or raw bytes, give the
+    unique suffix array."""
     monkeypatch.setenv("SALZ_SA_MODE", mode)
+    monkeypatch.setenv("SALZ_ALPHA", keys)
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
     o = oracle_stages(src)
