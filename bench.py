@@ -449,6 +449,7 @@ def main():
             "stages_ms_last_block": {k: round(st[k], 3) for k in
                                      ("ms_sa", "ms_lcp", "ms_ansv", "ms_parse", "ms_emit", "ms_total")},
             "sa_rounds": st["sa_rounds"],
+            "sa_dc3_levels": st["sa_dc3_levels"],
             "parse_iters": st["parse_iters"],
         }
         print(json.dumps(line), flush=True)

@@ -91,6 +91,7 @@ typedef struct {
     uint32_t radix_scatter_launches;
     double ms_radix_scatter;
     uint64_t radix_scatter_elems;
+    int32_t sa_dc3_levels; /* > 0: the suffix array came from the DC3 sorter (repetitive block) */
 } salz_gpu_stats;
 
 /* Per-stage HIP-event timing of subsequent calls (small overhead when on). */

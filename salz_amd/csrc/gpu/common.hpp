@@ -100,7 +100,7 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 constexpr size_t kErrWord = 60;  // u32 index into Workspace::dscal
 enum : uint32_t {
     kErrCommit = 1u, kErrKeys = 2u, kErrSeg = 4u, kErrExtract = 8u, kErrPutback = 16u,
-    kErrPhi = 32u, kErrAnsv = 64u, kErrParse = 128u
+    kErrPhi = 32u, kErrAnsv = 64u, kErrParse = 128u, kErrDc3 = 0x100000u
 };
 
 __device__ __forceinline__ bool bad_index(bool bad, uint32_t *err, uint32_t code)

@@ -1,0 +1,423 @@
+// dc3.hip - suffix array by the difference cover modulo 3 (Kärkkäinen-Sanders skew) for
+// highly repetitive blocks.
+//
+// Replaces libsais() at /root/reference/lib/salz.c:463-469 for inputs where prefix doubling
+// (sa.hip) keeps almost every suffix unfinished for ~log2(max LCP) rounds: a Fibonacci word
+// has only h + 1 distinct substrings of length h, so all 2^28 suffixes of the 256 MiB config
+// stay in play for 26 full-width rounds. Here each level sorts the sample suffixes
+// (i mod 3 != 0) by their first three symbols, names the triples, recurses on the 2/3-length
+// string of names when names repeat, and merges the sorted sample with the mod-0 suffixes:
+// the levels shrink by 2/3, so the whole sort costs about three times its first level.
+//
+// Per level (string t[0, n) of symbols >= 1, zero past the end; tools/dc3_sim.py models every
+// step on the CPU):
+//   k_dc3_sample_keys  sample j -> position p(j) (j < n1: 3j + 1, else 3(j - n1) + 2) and its
+//                      triple key; n = 1 mod 3 adds a dummy sample at p = n (triple 000, the
+//                      unique smallest name), so the names of the mod-1 part end in a unique
+//                      symbol and comparisons of the name string never run into the mod-2 part
+//   radix sort         (radix.hip) on the triple (or on two symbols, then stably on the first,
+//                      when three do not fit 64 bits)
+//   k_dc3_heads + scan names 1..D; D == n_sample means the sample is sorted already
+//   k_dc3_names        the child's string R[j] = name (R = mod-1 names, then mod-2 names)
+//   k_dc3_rank         rank[p] = 1 + sorted position of sample p (0 past the end)
+//   k_dc3_mod0         mod-0 suffixes i = p - 1 for the mod-1 samples p in sorted order: the
+//                      list is ordered by rank[i + 1], so a stable sort by t[i] sorts it
+//   k_dc3_partition /  merge path over the two sorted lists: sample p against mod-0 i compares
+//   k_dc3_merge        (t[i], rank[i + 1]) when p = 1 mod 3, (t[i], t[i + 1], rank[i + 2]) when
+//                      p = 2 mod 3; 2048 outputs per workgroup, merged in LDS
+// Symbols and ranks of a level are interleaved (TR[q] = {t[q], rank[q]}), so the merge's
+// comparison operands of one suffix are one 24-byte run.
+#include "internal.hpp"
+
+#include <cstdlib>
+#include <cstring>
+
+namespace salz {
+namespace {
+
+constexpr int kT = 256;
+
+__device__ __forceinline__ uint32_t dc3_pos(uint32_t j, uint32_t n1)
+{
+    return j < n1 ? 3u * j + 1u : 3u * (j - n1) + 2u;
+}
+
+// Level 0: the block's bytes as symbols 1..sigma (order-preserving codes) or byte + 1.
+__global__ void k_dc3_text(const uint8_t *__restrict__ T, uint32_t n, Alpha a, int raw, uint2 *__restrict__ tr)
+{
+    __shared__ uint8_t code[256];
+    load_codes(code, a);
+    __syncthreads();
+    for (size_t q = (size_t)blockIdx.x * kT + threadIdx.x; q < (size_t)n + 8; q += (size_t)gridDim.x * kT) {
+        const uint32_t c = q < n ? T[q] : 0u;
+        tr[q] = make_uint2(q < n ? (raw ? c + 1u : (uint32_t)code[c]) : 0u, 0u);
+    }
+}
+
+// Sample keys: full (t[p] << 2b | t[p+1] << b | t[p+2]) or, when 3b > 64, the last two symbols.
+__global__ void k_dc3_sample_keys(const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1, int b, int full,
+                                  uint64_t *__restrict__ key, uint32_t *__restrict__ val)
+{
+    const size_t j = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (j >= ns)
+        return;
+    const uint32_t p = dc3_pos((uint32_t)j, n1);
+    const uint64_t t0 = tr[p].x, t1 = tr[p + 1].x, t2 = tr[p + 2].x;
+    key[j] = full ? (t0 << (2 * b)) | (t1 << b) | t2 : (t1 << b) | t2;
+    val[j] = (uint32_t)j;
+}
+
+// Second phase of a split triple sort: key = first symbol of the (already sorted) sample.
+__global__ void k_dc3_first_keys(const uint2 *__restrict__ tr, const uint32_t *__restrict__ val, uint32_t ns,
+                                 uint32_t n1, uint64_t *__restrict__ key)
+{
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (c >= ns)
+        return;
+    key[c] = tr[dc3_pos(val[c], n1)].x;
+}
+
+// Name boundaries of the sorted sample: a new triple starts a new name.
+__global__ void k_dc3_heads(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
+                            const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1, int full,
+                            uint32_t *__restrict__ flag)
+{
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (c >= ns)
+        return;
+    const size_t cp = c ? c - 1 : 0;  // unconditional loads (clamped)
+    bool head;
+    if (full) {
+        head = c == 0 || key[c] != key[cp];
+    } else {
+        const uint32_t p = dc3_pos(val[c], n1), q = dc3_pos(val[cp], n1);
+        head = c == 0 || tr[p].x != tr[q].x || tr[p + 1].x != tr[q + 1].x || tr[p + 2].x != tr[q + 2].x;
+    }
+    flag[c] = head ? 1u : 0u;
+}
+
+// The child's string: R[j] = name of sample j (rank part zero).
+__global__ void k_dc3_names(const uint32_t *__restrict__ val, const uint32_t *__restrict__ name, uint32_t ns,
+                            uint2 *__restrict__ child)
+{
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (c >= ns)
+        return;
+    child[val[c]] = make_uint2(name[c], 0u);
+}
+
+// rank[p] = 1 + sorted position of sample p; the dummy (p = n) keeps rank 0.
+__global__ void k_dc3_rank(const uint32_t *__restrict__ sar, uint32_t ns, uint32_t n1, uint32_t n,
+                           uint2 *__restrict__ tr, uint32_t *err)
+{
+    const size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (r >= ns)
+        return;
+    const uint32_t j = sar[r];
+    if (bad_index(j >= ns, err, kErrDc3))
+        return;
+    const uint32_t p = dc3_pos(j, n1);
+    if (p < n)
+        tr[p].y = (uint32_t)r + 1u;
+}
+
+__global__ void k_dc3_mod0_flags(const uint32_t *__restrict__ sar, uint32_t ns, uint32_t n1,
+                                 uint32_t *__restrict__ flag)
+{
+    const size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (r < ns)
+        flag[r] = sar[r] < n1 ? 1u : 0u;
+}
+
+// Mod-0 suffixes in rank[i + 1] order (the dummy stands for i = n - 1), keyed by t[i].
+__global__ void k_dc3_mod0(const uint32_t *__restrict__ sar, const uint32_t *__restrict__ idx, uint32_t ns,
+                           uint32_t n1, uint32_t n0, const uint2 *__restrict__ tr, uint64_t *__restrict__ key,
+                           uint32_t *__restrict__ val, uint32_t *err)
+{
+    const size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (r >= ns)
+        return;
+    const uint32_t j = sar[r];
+    if (j >= n1)
+        return;
+    const uint32_t c = idx[r], i = 3u * j;
+    if (bad_index(c >= n0, err, kErrDc3))
+        return;
+    key[c] = tr[i].x;
+    val[c] = i;
+}
+
+// ---- merge of the sorted sample (A) and the sorted mod-0 suffixes (B) ----------------------
+struct Quad {
+    uint32_t t0, t1, r1, r2;  // t[p], t[p + 1], rank[p + 1], rank[p + 2]
+};
+
+__device__ __forceinline__ Quad quad_of(const uint2 *__restrict__ tr, uint32_t p)
+{
+    const uint2 a = tr[p], b = tr[p + 1], c = tr[p + 2];
+    return Quad{a.x, b.x, b.y, c.y};
+}
+
+// Mod-0 suffix b before sample suffix a (a at a position = am mod 3)? Never equal.
+__device__ __forceinline__ bool b_before_a(const Quad &b, const Quad &a, uint32_t am)
+{
+    if (b.t0 != a.t0)
+        return b.t0 < a.t0;
+    if (am == 1)
+        return b.r1 < a.r1;
+    if (b.t1 != a.t1)
+        return b.t1 < a.t1;
+    return b.r2 < a.r2;
+}
+
+constexpr int kMergeItems = 8;
+constexpr uint32_t kMergeTile = kT * kMergeItems;
+
+struct MergeIn {
+    const uint32_t *sar;  // sorted sample as child indices (A = sar[dummy ..])
+    uint32_t na, dummy, n1;
+    const uint32_t *posb;  // sorted mod-0 positions (B)
+    uint32_t nb;
+    const uint2 *tr;
+};
+
+__device__ __forceinline__ uint32_t a_pos(const MergeIn &m, uint32_t r)
+{
+    return dc3_pos(m.sar[r + m.dummy], m.n1);
+}
+
+// A elements among the first `diag` outputs of every tile boundary (merge path, A first on ties
+// -- there are none).
+__global__ void k_dc3_partition(MergeIn m, uint32_t ntiles, uint32_t *__restrict__ split)
+{
+    const size_t t = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (t > ntiles)
+        return;
+    const uint64_t tot = (uint64_t)m.na + m.nb;
+    const uint32_t diag = (uint32_t)((uint64_t)t * kMergeTile < tot ? (uint64_t)t * kMergeTile : tot);
+    uint32_t lo = diag > m.nb ? diag - m.nb : 0u, hi = diag < m.na ? diag : m.na;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint32_t pa = a_pos(m, mid), pb = m.posb[diag - 1u - mid];
+        if (b_before_a(quad_of(m.tr, pb), quad_of(m.tr, pa), pa % 3u))
+            hi = mid;
+        else
+            lo = mid + 1u;
+    }
+    split[t] = lo;
+}
+
+__global__ __launch_bounds__(kT) void k_dc3_merge(MergeIn m, const uint32_t *__restrict__ split,
+                                                  uint32_t *__restrict__ out)
+{
+    __shared__ Quad sq[kMergeTile];
+    __shared__ uint32_t sp[kMergeTile];
+    const uint32_t tid = threadIdx.x, t = blockIdx.x;
+    const uint64_t tot = (uint64_t)m.na + m.nb;
+    const uint32_t d0 = t * kMergeTile;
+    const uint32_t d1 = (uint32_t)((uint64_t)d0 + kMergeTile < tot ? (uint64_t)d0 + kMergeTile : tot);
+    const uint32_t a0 = split[t], a1 = split[t + 1];
+    const uint32_t b0 = d0 - a0, b1 = d1 - a1;
+    const uint32_t na = a1 - a0, cnt = d1 - d0;
+    // A run then B run, each element's position and comparison operands
+    for (uint32_t s = tid; s < cnt; s += kT) {
+        const uint32_t p = s < na ? a_pos(m, a0 + s) : m.posb[b0 + (s - na)];
+        sp[s] = p;
+        sq[s] = quad_of(m.tr, p);
+    }
+    __syncthreads();
+    const uint32_t nb = b1 - b0;
+    const uint32_t diag = tid * kMergeItems < cnt ? tid * kMergeItems : cnt;
+    uint32_t lo = diag > nb ? diag - nb : 0u, hi = diag < na ? diag : na;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (b_before_a(sq[na + diag - 1u - mid], sq[mid], sp[mid] % 3u))
+            hi = mid;
+        else
+            lo = mid + 1u;
+    }
+    uint32_t ia = lo, ib = diag - lo;
+    uint32_t res[kMergeItems];
+#pragma unroll
+    for (int k = 0; k < kMergeItems; k++) {
+        bool take_a;
+        if (ia >= na)
+            take_a = false;
+        else if (ib >= nb)
+            take_a = true;
+        else
+            take_a = !b_before_a(sq[na + ib], sq[ia], sp[ia] % 3u);
+        const uint32_t s = take_a ? ia : na + ib;
+        res[k] = sp[s < cnt ? s : 0];
+        ia += take_a ? 1u : 0u;
+        ib += take_a ? 0u : 1u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kMergeItems; k++)
+        if (diag + k < cnt)
+            sp[diag + k] = res[k];
+    __syncthreads();
+    for (uint32_t s = tid; s < cnt; s += kT)
+        out[d0 + s] = sp[s];
+}
+
+struct Dc3 {
+    Workspace &ws;
+    hipStream_t st;
+    uint8_t *top;  // arena bump pointer
+    uint8_t *end;
+    uint32_t *derr;
+    int levels = 0;
+};
+
+template <typename T> static T *arena_take(Dc3 &d, size_t count)
+{
+    uint8_t *p = d.top;
+    const size_t bytes = (count * sizeof(T) + 255) & ~(size_t)255;
+    if (p + bytes > d.end)
+        return nullptr;
+    d.top += bytes;
+    return reinterpret_cast<T *>(p);
+}
+
+// Suffix array of the level string tr[0, n) (symbols < 2^b, tail zero) into sa_out.
+int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
+{
+    Workspace &ws = d.ws;
+    hipStream_t st = d.st;
+    d.levels++;
+    if (n == 1) {
+        SALZ_HIP(hipMemsetAsync(sa_out, 0, sizeof(uint32_t), st));
+        return 0;
+    }
+    const uint32_t dummy = n % 3u == 1u ? 1u : 0u;
+    const uint32_t n1 = (n + 1u) / 3u + dummy, n2 = n / 3u, ns = n1 + n2, n0 = (n + 2u) / 3u;
+    uint32_t *d32 = reinterpret_cast<uint32_t *>(ws.dscal) + 300;
+    uint64_t *K = ws.keyA;
+    uint32_t *V = ws.valA;
+    const bool full = 3 * b <= 64;
+    hipLaunchKernelGGL(k_dc3_sample_keys, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, ns, n1, b, full ? 1 : 0, K,
+                       V);
+    SALZ_LAUNCH_CHECK();
+    if (radix_sort_pairs(&K, &V, K == ws.keyA ? ws.keyB : ws.keyA, V == ws.valA ? ws.valB : ws.valA, ns, 0,
+                         full ? 3 * b : 2 * b, ws, st) != 0)
+        return -1;
+    if (!full) {
+        hipLaunchKernelGGL(k_dc3_first_keys, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, V, ns, n1, K);
+        SALZ_LAUNCH_CHECK();
+        if (radix_sort_pairs(&K, &V, K == ws.keyA ? ws.keyB : ws.keyA, V == ws.valA ? ws.valB : ws.valA, ns, 0, b,
+                             ws, st) != 0)
+            return -1;
+    }
+    uint32_t *flag = ws.u0, *name = ws.u1;
+    hipLaunchKernelGGL(k_dc3_heads, dim3(grid_for(ns, kT)), dim3(kT), 0, st, K, V, tr, ns, n1, full ? 1 : 0, flag);
+    SALZ_LAUNCH_CHECK();
+    if (scan_sum_u32(flag, name, ns, true, d32, ws, st) != 0)
+        return -1;
+    if (read_scalars(ws, 1200, 8, "dc3.D") != 0)
+        return -1;
+    const uint32_t D = reinterpret_cast<const uint32_t *>(ws.hscal)[300];
+    uint8_t *mark = d.top;
+    uint32_t *sar;
+    if (D < ns) {
+        uint2 *child = arena_take<uint2>(d, (size_t)ns + 8);
+        sar = arena_take<uint32_t>(d, ns);
+        if (!child || !sar) {
+            set_error("dc3: arena exhausted at level %d (n=%u)", d.levels, n);
+            return -1;
+        }
+        SALZ_HIP(hipMemsetAsync(child + ns, 0, 8 * sizeof(uint2), st));
+        hipLaunchKernelGGL(k_dc3_names, dim3(grid_for(ns, kT)), dim3(kT), 0, st, V, name, ns, child);
+        SALZ_LAUNCH_CHECK();
+        if (dc3_level(d, child, ns, bit_width(D), sar) != 0)
+            return -1;
+    } else {
+        sar = ws.u2;  // the sorted sample is the order (survives the mod-0 sort below)
+        SALZ_HIP(hipMemcpyAsync(sar, V, (size_t)ns * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    }
+    hipLaunchKernelGGL(k_dc3_rank, dim3(grid_for(ns, kT)), dim3(kT), 0, st, sar, ns, n1, n, tr, d.derr);
+    SALZ_LAUNCH_CHECK();
+    // mod-0 list, then its stable sort by t[i]
+    hipLaunchKernelGGL(k_dc3_mod0_flags, dim3(grid_for(ns, kT)), dim3(kT), 0, st, sar, ns, n1, flag);
+    SALZ_LAUNCH_CHECK();
+    if (scan_sum_u32(flag, name, ns, false, d32 + 1, ws, st) != 0)
+        return -1;
+    K = ws.keyA;
+    V = ws.valA;
+    hipLaunchKernelGGL(k_dc3_mod0, dim3(grid_for(ns, kT)), dim3(kT), 0, st, sar, name, ns, n1, n0, tr, K, V,
+                       d.derr);
+    SALZ_LAUNCH_CHECK();
+    if (radix_sort_pairs(&K, &V, ws.keyB, ws.valB, n0, 0, b, ws, st) != 0)
+        return -1;
+    // merge
+    MergeIn mi{sar, ns - dummy, dummy, n1, V, n0, tr};
+    const uint32_t ntiles = grid_for(n, kMergeTile);
+    uint32_t *split = ws.offA;
+    hipLaunchKernelGGL(k_dc3_partition, dim3(grid_for((size_t)ntiles + 1, kT)), dim3(kT), 0, st, mi, ntiles, split);
+    SALZ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_dc3_merge, dim3(ntiles), dim3(kT), 0, st, mi, split, sa_out);
+    SALZ_LAUNCH_CHECK();
+    d.top = mark;  // the child's string and suffix array are consumed
+    return 0;
+}
+
+}  // namespace
+
+// Arena bytes for a block of n suffixes: level 0's TR plus, for every deeper level, its TR and
+// suffix array (the string lengths shrink to ceil(2n / 3) + 1 per level).
+static size_t dc3_arena_bytes(uint32_t n)
+{
+    size_t bytes = (((size_t)n + 8) * 8 + 255) & ~(size_t)255;
+    uint64_t m = n;
+    while (m > 1) {
+        const uint64_t dm = m % 3 == 1 ? 1 : 0;
+        m = (m + 1) / 3 + dm + m / 3;
+        bytes += (((m + 8) * 8 + 255) & ~(size_t)255) + ((m * 4 + 255) & ~(size_t)255);
+    }
+    return bytes + 4096;
+}
+
+int stage_suffix_array_dc3(Workspace &ws, const Blocks &bl, const Alpha &codes, int raw)
+{
+    hipStream_t st = ws.stream;
+    const uint32_t n = bl.npos;
+    if (bl.nb != 1) {
+        set_error("dc3: one block per pass only");
+        return -1;
+    }
+    const size_t need = dc3_arena_bytes(n);
+    if (ws.dc3_bytes < need) {
+        if (ws.dc3)
+            SALZ_HIP(hipFree(ws.dc3));
+        ws.dc3 = nullptr;
+        ws.dc3_bytes = 0;
+        void *p = nullptr;
+        SALZ_HIP(hipMalloc(&p, need));
+        ws.dc3 = static_cast<uint8_t *>(p);
+        ws.dc3_bytes = need;
+    }
+    uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
+    Dc3 d{ws, st, ws.dc3, ws.dc3 + ws.dc3_bytes, derr};
+    uint2 *tr = arena_take<uint2>(d, (size_t)n + 8);
+    const unsigned g = grid_for((size_t)n + 8, kT) < 8192u ? grid_for((size_t)n + 8, kT) : 8192u;
+    hipLaunchKernelGGL(k_dc3_text, dim3(g), dim3(kT), 0, st, ws.text, n, codes, raw, tr);
+    SALZ_LAUNCH_CHECK();
+    uint32_t sigma = 0;
+    for (int c = 0; c < 256; c++)
+        sigma = codes.code[c] > sigma ? codes.code[c] : sigma;
+    const int b = raw ? 9 : bit_width(sigma);
+    if (dc3_level(d, tr, n, b, ws.sa) != 0)
+        return -1;
+    if (read_scalars(ws, 0, 256, "dc3.err") != 0)
+        return -1;
+    if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
+        set_error("dc3 suffix sort: device index check failed (code 0x%x)", e);
+        return -1;
+    }
+    ws.stats.sa_dc3_levels = d.levels;
+    ws.lcps_ok = false;  // the LCP array comes from the Phi/PLCP stage (lcp.hip)
+    return 0;
+}
+
+}  // namespace salz

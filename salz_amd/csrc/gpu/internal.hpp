@@ -17,6 +17,7 @@ struct StageStats {
     int sa_rounds;
     int parse_iters;
     uint64_t sa_sorted_elems;  // sum over rounds of active suffixes sorted
+    int sa_dc3_levels;         // DC3 levels (0: prefix doubling built the suffix array)
     uint32_t exit_nodes;
     uint64_t lcp_long_bytes;
     float ms_radix_scatter;   // summed over every radix scatter launch (HIP events)
@@ -63,6 +64,8 @@ struct Workspace {
     uint64_t *lsc = nullptr;   // 2 n1: suffix sorter's large-group scan; ANSV staging (uint4)
     uint64_t *lrec = nullptr;  // per large group: (start in extracted array << 32) | start
     uint32_t *lg2g = nullptr;  // per large group: its group id
+    uint8_t *dc3 = nullptr;    // DC3 suffix sorter's level arena (dc3.hip), allocated on first use
+    size_t dc3_bytes = 0;
     uint8_t *out = nullptr;                                              // encoded_len_max
     size_t out_cap = 0;
     uint32_t *radix_counts = nullptr;
@@ -121,6 +124,9 @@ constexpr uint32_t kMaxBatchBlocks = 4096;
 
 // stages; every one takes the batch geometry (one block: Blocks{0xffffffff, 1, n})
 int stage_suffix_array(Workspace &ws, const Blocks &bl);           // sa.hip   -> ws.sa
+// dc3.hip -> ws.sa for one block (repetitive inputs); symbols = codes.code[byte] (1..sigma) or
+// byte + 1 when raw
+int stage_suffix_array_dc3(Workspace &ws, const Blocks &bl, const Alpha &codes, int raw);
 int stage_lcp(Workspace &ws, const Blocks &bl, uint32_t *lcp_out); // lcp.hip  -> lcp[r]
 int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp);  // ansv.hip -> ws.cand
 int stage_parse(Workspace &ws, const Blocks &bl);                  // parse.hip

@@ -91,7 +91,7 @@ void workspace_free(Workspace &ws)
         (void)hipSetDevice(ws.device);
     void *ptrs[] = {ws.text, ws.rank,     ws.sa,   ws.keyA, ws.keyB, ws.valA, ws.valB,
                     ws.u0,   ws.u1,       ws.u2,   ws.u3,   ws.g64,  ws.offA, ws.offB, ws.lcps,
-                    ws.cand, ws.pst, ws.lsc, ws.lrec, ws.lg2g, ws.out, ws.radix_counts,  ws.scan_tmp,      ws.dscal};
+                    ws.cand, ws.pst, ws.lsc, ws.lrec, ws.lg2g, ws.dc3, ws.out, ws.radix_counts,  ws.scan_tmp,      ws.dscal};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -681,6 +681,7 @@ int salz_gpu_get_stats(const salz_gpu_ctx *ctx, salz_gpu_stats *o)
     o->radix_scatter_launches = s.radix_scatter_launches;
     o->ms_radix_scatter = s.ms_radix_scatter;
     o->radix_scatter_elems = s.radix_scatter_elems;
+    o->sa_dc3_levels = s.sa_dc3_levels;
     return 0;
 }
 

@@ -791,6 +791,9 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
     uint64_t *d64 = ws.dscal + 8;
     uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
     SALZ_HIP(hipMemsetAsync(derr, 0, sizeof(uint32_t) * 12, st));
+    ws.stats.sa_rounds = 0;
+    ws.stats.sa_sorted_elems = 0;
+    ws.stats.sa_dc3_levels = 0;
     // Scratch borrowed from later stages (free while the suffix array is built): the
     // extracted large groups live in pst (keys) and cand (values), the group table in cand.
     uint8_t *cb = reinterpret_cast<uint8_t *>(ws.cand);
@@ -806,6 +809,15 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
     // common.hpp); SALZ_ALPHA=0 keeps raw 8-byte keys (tests run both).
     Alpha alpha{};
     const bool alpha_on = !getenv("SALZ_ALPHA") || atoi(getenv("SALZ_ALPHA")) != 0;
+    // DC3 (dc3.hip) instead of doubling for repetitive single blocks: SALZ_SA_ALGO=dc3 forces it,
+    // =doubling never; by default a block of >= 1 MiB switches once the sort has reached depth 32
+    // with more than 3/4 of its suffixes still unfinished (long repeats: the following rounds stay
+    // that wide; text keeps ~17% at depth 32, Fibonacci and periodic blocks all of them).
+    const char *algo_env = getenv("SALZ_SA_ALGO");
+    const bool dc3_force = algo_env && !strcmp(algo_env, "dc3") && bl.nb == 1 && n >= 2;
+    const bool dc3_auto = !(algo_env && !strcmp(algo_env, "doubling")) && bl.nb == 1 && n >= (1u << 20);
+    Alpha codes{};  // the block's byte codes 1..sigma for DC3 (raw bytes + 1 when not known)
+    int codes_raw = 1;
     if (alpha_on && n >= 64) {
         uint32_t *words = reinterpret_cast<uint32_t *>(ws.dscal) + 240;
         SALZ_HIP(hipMemsetAsync(words, 0, 8 * sizeof(uint32_t), st));
@@ -821,11 +833,17 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
             if (pw[c >> 5] & (1u << (c & 31)))
                 alpha.code[c] = (uint8_t)++sigma;
         const uint32_t bits = (uint32_t)bit_width(sigma);  // codes 1..sigma, 0 = past the end
+        if (sigma <= 255) {
+            codes = alpha;
+            codes_raw = 0;
+        }
         if (bits <= 7) {
             alpha.bits = bits;
             alpha.k = bits >= 5 ? 8u : 64u / bits;  // 8 symbols in fewer passes, or more depth
         }
     }
+    if (dc3_force)
+        return stage_suffix_array_dc3(ws, bl, codes, codes_raw);
     const uint32_t h0 = alpha.bits ? alpha.k : 8u;
     // The text mapped to symbols for the text-sourced radix pass (u1 is free until round 0's
     // group sums): one byte per position, zero padded.
@@ -867,8 +885,6 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
     uint32_t m = nsa, h = h0, G_act = 0, GL = 0, mL = 0;
     int kb_old = 0, round0 = 1;
     const int kb = bit_width(n);
-    ws.stats.sa_rounds = 0;
-    ws.stats.sa_sorted_elems = 0;
     static const bool verbose = getenv("SALZ_DEBUG_SA") != nullptr;
     const char *mode_env = getenv("SALZ_SA_MODE");  // tests: "global" or "segmented"
     auto t_round = std::chrono::steady_clock::now();
@@ -1049,6 +1065,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
         }
         if (mnew == 0)
             break;
+        if (dc3_auto && h >= 32 && (uint64_t)mnew * 4 > (uint64_t)n * 3)
+            return stage_suffix_array_dc3(ws, bl, codes, codes_raw);
         if (h >= n || Gnew == 0) {
             set_error("suffix sort did not converge (h=%u n=%u m=%u)", h, n, mnew);
             return -1;

@@ -255,6 +255,63 @@ def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
+DC3_CASES = STAGE_CASES + [("text", 300001, 4, 0), ("smx", 40000, 7, 200), ("mixed", 200003, 8, 0),
+                           ("fib", 65537, 0, 0), ("zeros", 3000, 0, 0)]
+
+
+@pytest.mark.parametrize("keys", ["1", "0"])
+@pytest.mark.parametrize("kind,n,seed,alpha", DC3_CASES)
+def test_dc3_matches_oracle(ctx, monkeypatch, keys, kind, n, seed, alpha):
+    """The DC3 suffix sorter (dc3.hip, forced with SALZ_SA_ALGO=dc3) gives the unique suffix
+    array on every input kind, from the block's byte codes (SALZ_ALPHA=1) or raw bytes + 1."""
+    monkeypatch.setenv("SALZ_SA_ALGO", "dc3")
+    monkeypatch.setenv("SALZ_ALPHA", keys)
+    src = _make(kind, n, seed, alpha)
+    out, d = ctx.encode_dump(src)
+    assert ctx.stats()["sa_dc3_levels"] > 0
+    o = oracle_stages(src)
+    i = _first_diff(d["sa"], o["sa"])
+    assert i < 0, f"sa differs at rank {i}: gpu {d['sa'][i]} oracle {o['sa'][i]}"
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and out == ref
+
+
+def test_dc3_edge_sizes(ctx, monkeypatch):
+    """DC3 at every suffix count 1..200 (each n mod 3, the dummy sample, one-level and
+    recursing strings) and around powers of two."""
+    monkeypatch.setenv("SALZ_SA_ALGO", "dc3")
+    rng = np.random.default_rng(13)
+    sizes = list(range(9, 209)) + [4096 + 8 + d for d in (-1, 0, 1, 2)] + [65536 + 8 + d for d in (0, 1, 2)]
+    for N in sizes:
+        for kind in ("rand2", "zeros", "rand256"):
+            if kind == "rand2":
+                src = rng.integers(97, 99, N, dtype=np.uint8)
+            elif kind == "zeros":
+                src = np.zeros(N, np.uint8)
+            else:
+                src = rng.integers(0, 256, N, dtype=np.uint8)
+            rc, ref = oracle_encode(src)
+            out = ctx.encode(src)
+            assert rc == 0 and out == ref, (N, kind)
+
+
+@pytest.mark.parametrize("algo", ["", "doubling"])
+def test_dc3_auto_switch(ctx, monkeypatch, algo):
+    """A repetitive block of >= 1 MiB switches to DC3 after round 0 by default; text does not;
+    SALZ_SA_ALGO=doubling keeps prefix doubling. Both give the reference stream."""
+    if algo:
+        monkeypatch.setenv("SALZ_SA_ALGO", algo)
+    else:
+        monkeypatch.delenv("SALZ_SA_ALGO", raising=False)
+    for kind, n in (("fib", 3 << 20), ("period3", 2 << 20), ("text", 2 << 20)):
+        src = _make(kind, n, 1, 0)
+        out = ctx.encode(src)
+        rep = kind != "text" and not algo
+        assert (ctx.stats()["sa_dc3_levels"] > 0) == rep, kind
+        rc, ref = oracle_encode(src)
+        assert rc == 0 and out == ref, kind
+
+
 @pytest.mark.parametrize("lcp_sa", ["1", "0"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 400000, 1, 0), ("mixed", 500000, 3, 0),
                                                ("fib", 200000, 0, 0), ("smx", 300000, 2, 4),
