@@ -87,6 +87,53 @@ __global__ void k_alpha_presence(const uint8_t *__restrict__ T, size_t P, uint32
         atomicOr(&words[threadIdx.x], w[threadIdx.x]);
 }
 
+// Repetition probe (one workgroup): fingerprints of the 32 bytes at 4096 evenly spaced
+// positions, sorted in LDS; out = how many samples share their fingerprint with another. A
+// Fibonacci or periodic block repeats every 32-gram (all samples collide), text almost never.
+constexpr uint32_t kProbe = 4096;
+constexpr uint32_t kProbeThreads = 1024;
+__global__ __launch_bounds__(kProbeThreads) void k_repeat_probe(const uint8_t *__restrict__ T, uint32_t n,
+                                                                uint32_t *__restrict__ out)
+{
+    __shared__ uint64_t k[kProbe];
+    __shared__ uint32_t dups;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0)
+        dups = 0;
+    for (uint32_t s = tid; s < kProbe; s += kProbeThreads) {
+        const size_t p = (size_t)s * (n - 32u) / kProbe;
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            h ^= load_u64_any(T, p + 8u * w);
+            h *= 0xBF58476D1CE4E5B9ull;
+            h ^= h >> 31;
+        }
+        k[s] = h;
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= kProbe; size <<= 1)  // bitonic sort
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (uint32_t t = tid; t < kProbe / 2; t += kProbeThreads) {
+                const uint32_t i = 2 * t - (t & (stride - 1)), j = i + stride;
+                const bool up = (i & size) == 0;
+                const uint64_t a = k[i], b = k[j];
+                if ((a > b) == up) {
+                    k[i] = b;
+                    k[j] = a;
+                }
+            }
+            __syncthreads();
+        }
+    uint32_t d = 0;
+    for (uint32_t s = tid; s < kProbe; s += kProbeThreads)
+        d += (s > 0 && k[s - 1] == k[s]) || (s + 1 < kProbe && k[s + 1] == k[s]);
+    atomicAdd(&dups, d);
+    __syncthreads();
+    if (tid == 0)
+        *out = dups;
+}
+
 // Group-head flags travel as one 64-bit ballot per wave of the sorted list (hmask) plus its
 // popcount (wcnt): the group ids are then a scan over m / 64 wave counts, not over m flags.
 struct HeadBits {
@@ -810,12 +857,16 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
     Alpha alpha{};
     const bool alpha_on = !getenv("SALZ_ALPHA") || atoi(getenv("SALZ_ALPHA")) != 0;
     // DC3 (dc3.hip) instead of doubling for repetitive single blocks: SALZ_SA_ALGO=dc3 forces it,
-    // =doubling never; by default a block of >= 1 MiB switches once the sort has reached depth 32
+    // =doubling never. By default a block of >= 1 MiB starts with DC3 when the repetition probe
+    // finds half of its sampled 32-grams repeated, and otherwise switches once the sort has reached depth 32
     // with more than 3/4 of its suffixes still unfinished (long repeats: the following rounds stay
     // that wide; text keeps ~17% at depth 32, Fibonacci and periodic blocks all of them).
     const char *algo_env = getenv("SALZ_SA_ALGO");
     const bool dc3_force = algo_env && !strcmp(algo_env, "dc3") && bl.nb == 1 && n >= 2;
     const bool dc3_auto = !(algo_env && !strcmp(algo_env, "doubling")) && bl.nb == 1 && n >= (1u << 20);
+    // SALZ_SA_PROBE=0: no repetition probe (only the depth-32 switch)
+    const bool dc3_probe_off = getenv("SALZ_SA_PROBE") && atoi(getenv("SALZ_SA_PROBE")) == 0;
+    bool dc3_now = false;
     Alpha codes{};  // the block's byte codes 1..sigma for DC3 (raw bytes + 1 when not known)
     int codes_raw = 1;
     if (alpha_on && n >= 64) {
@@ -825,8 +876,14 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
         hipLaunchKernelGGL(k_alpha_presence, dim3(grid_for(P, kT * 16) < 2048 ? grid_for(P, kT * 16) : 2048),
                            dim3(kT), 0, st, ws.text, P, words);
         SALZ_LAUNCH_CHECK();
-        if (read_scalars(ws, 960, 32, "sa.alpha") != 0)
+        if (dc3_auto && !dc3_probe_off) {
+            hipLaunchKernelGGL(k_repeat_probe, dim3(1), dim3(kProbeThreads), 0, st, ws.text, n, words + 8);
+            SALZ_LAUNCH_CHECK();
+        }
+        if (read_scalars(ws, 960, 48, "sa.alpha") != 0)
             return -1;
+        // half the samples repeated: long repeats everywhere, DC3 from the start
+        dc3_now = dc3_auto && !dc3_probe_off && reinterpret_cast<const uint32_t *>(ws.hscal)[248] * 2 >= kProbe;
         const uint32_t *pw = reinterpret_cast<const uint32_t *>(ws.hscal) + 240;
         uint32_t sigma = 0;
         for (int c = 0; c < 256; c++)
@@ -842,7 +899,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
             alpha.k = bits >= 5 ? 8u : 64u / bits;  // 8 symbols in fewer passes, or more depth
         }
     }
-    if (dc3_force)
+    if (dc3_force || dc3_now)
         return stage_suffix_array_dc3(ws, bl, codes, codes_raw);
     const uint32_t h0 = alpha.bits ? alpha.k : 8u;
     // The text mapped to symbols for the text-sourced radix pass (u1 is free until round 0's

@@ -295,19 +295,23 @@ def test_dc3_edge_sizes(ctx, monkeypatch):
             assert rc == 0 and out == ref, (N, kind)
 
 
-@pytest.mark.parametrize("algo", ["", "doubling"])
+@pytest.mark.parametrize("algo", ["", "noprobe", "doubling"])
 def test_dc3_auto_switch(ctx, monkeypatch, algo):
-    """A repetitive block of >= 1 MiB switches to DC3 after round 0 by default; text does not;
-    SALZ_SA_ALGO=doubling keeps prefix doubling. Both give the reference stream."""
-    if algo:
+    """A repetitive block of >= 1 MiB goes to DC3 by default: before round 0 when the repetition
+    probe finds its sampled 32-grams repeated, else (SALZ_SA_PROBE=0) at depth 32; text does
+    not; SALZ_SA_ALGO=doubling keeps prefix doubling. All give the reference stream."""
+    monkeypatch.delenv("SALZ_SA_ALGO", raising=False)
+    monkeypatch.setenv("SALZ_SA_PROBE", "0" if algo == "noprobe" else "1")
+    if algo == "doubling":
         monkeypatch.setenv("SALZ_SA_ALGO", algo)
-    else:
-        monkeypatch.delenv("SALZ_SA_ALGO", raising=False)
     for kind, n in (("fib", 3 << 20), ("period3", 2 << 20), ("text", 2 << 20)):
         src = _make(kind, n, 1, 0)
         out = ctx.encode(src)
-        rep = kind != "text" and not algo
-        assert (ctx.stats()["sa_dc3_levels"] > 0) == rep, kind
+        rep = kind != "text" and algo != "doubling"
+        st = ctx.stats()
+        assert (st["sa_dc3_levels"] > 0) == rep, kind
+        if rep:  # the probe skips round 0 of doubling
+            assert st["sa_rounds"] == (1 if algo == "noprobe" else 0), kind
         rc, ref = oracle_encode(src)
         assert rc == 0 and out == ref, kind
 
