@@ -87,12 +87,17 @@ constexpr uint32_t kCDepth = 7;
 // state in pst; past it, the aligned pair of cin words holding cin[sidx(q)] (far_decode picks
 // the half). A factor that is not long (or runs past the end) loads its own chunk's first
 // state, pst[base]: the 64 lanes then read 512 contiguous bytes instead of 64 lines.
+// Consecutive positions of one match share its end (p + len stays put while len shrinks by
+// one), so a target equal to the one loaded for position p + 1 (lq) is not loaded again: the
+// lane reads its chunk's first state instead and `same` tells the step to reuse p + 1's value.
 __device__ __forceinline__ uint64_t far_load(const uint64_t *pst, const uint32_t *cin, size_t base,
                                              uint32_t a, uint32_t b, uint32_t klog, uint32_t p,
-                                             uint32_t len, uint32_t n)
+                                             uint32_t len, uint32_t n, uint32_t &lq, uint32_t &same)
 {
     const bool far = len > kWin && len <= n - p;
-    const uint32_t q = far ? p + len : a;
+    same = far && p + len == lq ? 1u : 0u;
+    lq = far ? p + len : 0xffffffffu;
+    const uint32_t q = far && !same ? p + len : a;
     const uint64_t *addr = q < b ? pst + base + ((size_t)(q - a) << 6)
                                  : reinterpret_cast<const uint64_t *>(cin) + (sidx(q, klog) >> 1);
     return *addr;
@@ -149,14 +154,20 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         uint64_t fP[kDepth], fN[kDepth];
         uint64_t win[kWin];  // win[k] = state of p + 1 + k
         const uint32_t pK = a + K - 1;
+        // ring bit k: the far target of position p - k equals p - k + 1's (value reused)
+        uint32_t sameP = 0, sameN = 0, lqP = 0xffffffffu, lqN = 0xffffffffu;
+        uint64_t prevP = 0, prevN = 0;  // decoded far targets of the previous step (p + 1)
 #pragma unroll
         for (uint32_t k = 0; k <= kCDepth; k++)
             cr[k] = cand[slot(K - 1 - k)];
 #pragma unroll
         for (uint32_t k = 0; k < kDepth; k++) {
             orr[k] = chold[slot(K - 1 - k)];
-            fP[k] = far_load(pst, cin, base, a, b, klog, pK - k, cr[k].y, n);
-            fN[k] = far_load(pst, cin, base, a, b, klog, pK - k, cr[k].w, n);
+            uint32_t sp, sn;
+            fP[k] = far_load(pst, cin, base, a, b, klog, pK - k, cr[k].y, n, lqP, sp);
+            fN[k] = far_load(pst, cin, base, a, b, klog, pK - k, cr[k].w, n, lqN, sn);
+            sameP |= sp << k;
+            sameN |= sn << k;
         }
 #pragma unroll
         for (uint32_t k = 0; k < kWin; k++) {  // states a + K .. a + K + kWin - 1 (past n: unused)
@@ -182,7 +193,8 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
                         for (uint32_t k = 2; k < kWin; k++)
                             t = c0.y == k + 1 ? win[k] : t;
                     } else {
-                        t = far_decode(fP[0], p + c0.y, b, klog);
+                        t = (sameP & 1u) ? prevP : far_decode(fP[0], p + c0.y, b, klog);
+                        prevP = t;
                     }
                     const uint32_t alt = factor_bits(c0.x, c0.y) + (uint32_t)(t >> 32);
                     if ((int32_t)alt < (int32_t)best) {
@@ -200,7 +212,8 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
                         for (uint32_t k = 2; k < kWin; k++)
                             t = c0.w == k + 1 ? win[k] : t;
                     } else {
-                        t = far_decode(fN[0], p + c0.w, b, klog);
+                        t = (sameN & 1u) ? prevN : far_decode(fN[0], p + c0.w, b, klog);
+                        prevN = t;
                     }
                     const uint32_t alt = factor_bits(c0.z, c0.w) + (uint32_t)(t >> 32);
                     if ((int32_t)alt < (int32_t)best) {
@@ -245,8 +258,11 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             const uint32_t jd = j >= kDepth ? j - kDepth : 0u;
             const uint4 cd = cr[kDepth - 1];
             orr[kDepth - 1] = chold[slot(jd)];
-            fP[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, cd.y, n);
-            fN[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, cd.w, n);
+            uint32_t sp, sn;
+            fP[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, cd.y, n, lqP, sp);
+            fN[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, cd.w, n, lqN, sn);
+            sameP = (sameP >> 1) | (sp << (kDepth - 1));
+            sameN = (sameN >> 1) | (sn << (kDepth - 1));
             cr[kCDepth] = cand[slot(j >= kCDepth + 1 ? j - kCDepth - 1 : 0u)];
         }
     }
@@ -259,6 +275,52 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         atomicAdd(changed, diff);
 }
 
+// Farthest target of each chunk's candidates (at least its end b): the candidates do not change
+// between passes, so this is computed once per parse. One lane per chunk, row by row.
+__global__ __launch_bounds__(kT) void k_chunk_reach(const uint4 *__restrict__ cand, uint32_t n, Blocks bl,
+                                                    uint32_t klog, uint32_t *__restrict__ reach)
+{
+    const uint32_t c = blockIdx.x * kT + threadIdx.x;
+    const uint64_t a64 = (uint64_t)c << klog;
+    if (a64 >= n)
+        return;
+    const uint32_t a = (uint32_t)a64, K = 1u << klog;
+    const uint32_t e = bl.end(a);
+    const uint32_t b = (e - a) < K ? e : a + K;
+    const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
+    uint32_t r = b;
+    for (uint32_t j = 0; j < b - a; j++) {
+        const uint4 cd = cand[base + ((size_t)j << 6)];
+        const uint32_t p = a + j;
+        if (cd.y >= 3u && p + cd.y > r)
+            r = p + cd.y;
+        if (cd.w >= 3u && p + cd.w > r)
+            r = p + cd.w;
+    }
+    reach[c] = r;
+}
+
+// Breaks of the cost shift d[q] = cnew[q] - cold[q] (q >= 1 with d[q] != d[q - 1], or a cost at
+// or above 2^30), counted per chunk k over q in (kK, (k + 1)K]: one lane per chunk, row by row.
+__global__ __launch_bounds__(kT) void k_shift_breaks(const uint32_t *__restrict__ cnew,
+                                                     const uint32_t *__restrict__ cold, uint32_t n,
+                                                     uint32_t klog, uint32_t nchunks, uint32_t *__restrict__ cnt)
+{
+    const uint32_t c = blockIdx.x * kT + threadIdx.x;
+    if (c >= nchunks)
+        return;
+    const uint32_t K = 1u << klog, a = c << klog;
+    const uint32_t last = a + K <= n ? a + K : n;  // q in (a, last]
+    uint32_t prev = cnew[sidx(a, klog)] - cold[sidx(a, klog)], k = 0;
+    for (uint32_t q = a + 1; q <= last; q++) {
+        const size_t sq = sidx(q, klog);
+        const uint32_t v = cnew[sq], d = v - cold[sq];
+        k += (d != prev) | (v >= (1u << 30));
+        prev = d;
+    }
+    cnt[c] = k;
+}
+
 // Uniform-shift test, one chunk per lane, before every pass from the third on: every target
 // at or past the chunk end b (the literal's b, and each candidate's p + len beyond it) must
 // have moved by the same delta from cold (the costs the chunk's decisions are consistent
@@ -267,13 +329,17 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
 // argmins repeat. A wave of 64 chunks that all pass is clean (wdirty = 0) and skips the pass;
 // its chunks' states then lag cin by the delta, which dsum accumulates. ndirty counts the
 // dirty waves; none left means the fixed point.
+// A chunk whose targets [b, reach] hold no break of the shift (prefix counts pbrk over chunks)
+// passes without looking at its candidates; only the others run the per-candidate test.
 __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ cand,
                                                    const uint32_t *__restrict__ cnew,
                                                    const uint32_t *__restrict__ cold, uint32_t n,
                                                    Blocks bl,
                                                    uint32_t klog, uint8_t *__restrict__ wdirty,
                                                    uint32_t *__restrict__ dsum,
-                                                   uint32_t *__restrict__ ndirty)
+                                                   uint32_t *__restrict__ ndirty,
+                                                   const uint32_t *__restrict__ reach,
+                                                   const uint32_t *__restrict__ pbrk)
 {
     const uint32_t c = blockIdx.x * kT + threadIdx.x;
     const uint64_t a64 = (uint64_t)c << klog;
@@ -291,7 +357,15 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
         const uint32_t nb = cnew[sb];
         d0 = nb - cold[sb];
         bad = nb >= (1u << 30);
-        const uint32_t jn = b - a;
+        bool range_ok = false;
+        if (reach) {  // breaks in (b, r] lie in chunks c + 1 .. (r - 1) >> klog
+            const uint32_t r = reach[c];  // loads unconditional (an empty range compares c + 1 twice)
+            const uint32_t hi = r > b ? ((r - 1) >> klog) + 1 : c + 1;
+            range_ok = pbrk[hi] == pbrk[c + 1];
+        }
+        const uint32_t jn = range_ok ? 0u : b - a;
+        // rows tested: K when some chunk of the wave needs the full test, else none (uniform)
+        const uint32_t rows = wave_ballot(jn != 0) != 0 ? K : 0u;
         // K rows for every lane (rows past jn test b itself, which always passes), in batches
         // of 8: a batch's candidates are loaded while the previous batch's costs are checked
         // (two register sets, so no in-flight register is moved), and the loop count is
@@ -299,7 +373,7 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
         auto load = [&](uint4(&cd)[8], uint32_t j0) {
 #pragma unroll
             for (uint32_t u = 0; u < 8; u++) {
-                const uint32_t j = j0 + u < jn ? j0 + u : jn - 1;
+                const uint32_t j = j0 + u < jn ? j0 + u : (jn ? jn - 1u : 0u);
                 cd[u] = cand[base + ((size_t)j << 6)];
             }
         };
@@ -318,7 +392,7 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
         };
         uint4 A[8], B[8];
         load(A, 0);
-        for (uint32_t j0 = 0; j0 < K; j0 += 16) {
+        for (uint32_t j0 = 0; j0 < rows; j0 += 16) {
             load(B, j0 + 8);
             check(A, j0);
             load(A, j0 + 16);
@@ -489,6 +563,15 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     uint32_t *dsum = reinterpret_cast<uint32_t *>(ws.lsc);
     uint8_t *wdirty = reinterpret_cast<uint8_t *>(dsum + ps.nchunks);
     SALZ_HIP(hipMemsetAsync(dsum, 0, sizeof(uint32_t) * ps.nchunks, st));
+    // Range test of k_parse_mark (SALZ_PARSE_RANGE=0: per-candidate test only): each chunk's
+    // farthest target, and per test the shift breaks per chunk and their prefix counts.
+    const bool range_on = !getenv("SALZ_PARSE_RANGE") || atoi(getenv("SALZ_PARSE_RANGE")) != 0;
+    uint32_t *reach = dsum + 2 * ((size_t)ps.nchunks + 64);
+    uint32_t *brk = reach + ps.nchunks + 64, *pbrk = brk + ps.nchunks + 64;
+    bool reach_done = false;
+    // Large blocks test for skipping only late in the iteration (SALZ_PARSE_EARLY=1: from the
+    // third pass like smaller blocks; mixed 100 MB: 22.3 -> 23.7 ms, text 4.5 -> 5.0 ms)
+    const bool early = getenv("SALZ_PARSE_EARLY") && atoi(getenv("SALZ_PARSE_EARLY")) != 0;
 
     hipLaunchKernelGGL(k_cost_seed, dim3(grid_for(S, kT)), dim3(kT), 0, st, cost[0], bl, klog, S);
     SALZ_LAUNCH_CHECK();
@@ -513,11 +596,26 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         // save throughput, run it before every pass from the third.
         const bool late = (uint64_t)prev_changed * 64 < n &&
                           (it == 2 || (uint64_t)prev_changed * 4096 < n);
-        const bool skipping = it >= 2 && (n < (1u << 25) || late);
+        const bool skipping = it >= 2 && (n < (1u << 25) || late || early);
         if (skipping) {
             SALZ_HIP(hipMemsetAsync(ndirty, 0, 4, st));
+            if (range_on) {
+                if (!reach_done) {
+                    hipLaunchKernelGGL(k_chunk_reach, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand, n,
+                                       bl, klog, reach);
+                    SALZ_LAUNCH_CHECK();
+                    reach_done = true;
+                }
+                hipLaunchKernelGGL(k_shift_breaks, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, cin, cout, n,
+                                   klog, ps.nchunks, brk);
+                SALZ_LAUNCH_CHECK();
+                SALZ_HIP(hipMemsetAsync(brk + ps.nchunks, 0, sizeof(uint32_t), st));
+                if (scan_sum_u32(brk, pbrk, (size_t)ps.nchunks + 1, false, nullptr, ws, st) != 0)
+                    return -1;
+            }
             hipLaunchKernelGGL(k_parse_mark, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st,
-                               ws.cand, cin, cout, n, bl, klog, wdirty, dsum, ndirty);
+                               ws.cand, cin, cout, n, bl, klog, wdirty, dsum, ndirty,
+                               range_on ? reach : nullptr, pbrk);
             SALZ_LAUNCH_CHECK();
             if (read_scalars(ws, 0, 256, "parse.mark") != 0)
                 return -1;

@@ -72,7 +72,18 @@ def test_scanner_flags_the_known_hazard(tmp_path):
 	global_load_dwordx2 v[6:7], v[8:9], off
 	s_waitcnt vmcnt(1)
 """
+    # a loop latch laid out after an unconditional jump: its EXEC join is not a region change
+    # for the loads linearly above it
+    jump = """0000000000000200 <k_jump>:
+	s_and_saveexec_b64 s[30:31], vcc
+	global_load_dword v1, v[2:3], off
+	global_load_dword v4, v[2:3], off offset:4
+	s_branch 12
+	s_or_b64 exec, exec, s[2:3]
+	global_load_dword v5, v[6:7], off
+	s_waitcnt vmcnt(1)
+"""
     p = tmp_path / "snip.s"
-    p.write_text(bad + good)
+    p.write_text(bad + good + jump)
     hits = scan(str(p))
     assert [k for k, _ in hits] == ["k_bad"], hits

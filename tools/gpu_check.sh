@@ -21,3 +21,6 @@ timeout -k 10 200 python bench.py --no-cpu-baseline --kind mixed --steps 2 --war
 timeout -k 10 200 python bench.py --workload silesia --steps 2 --warmup 1 > $out/silesia.json 2> $out/silesia.err &&
 timeout -k 10 300 python bench.py --workload enwik9 --steps 1 --warmup 1 > $out/enwik9.json 2> $out/enwik9.err
 timeout -k 10 300 python tools/bench_levels.py --size 50000003 > $out/levels.jsonl 2> $out/levels.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof_fib -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-e2e --workload fib256 --steps 2 --warmup 1 > $out/fib_prof.json 2> $out/fib_prof.err
+SALZ_SA_ALGO=dc3 timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e --steps 2 --warmup 1 > $out/text_dc3.json 2> $out/text_dc3.err
+SALZ_SA_ALGO=dc3 timeout -k 10 200 python bench.py --no-cpu-baseline --no-e2e --kind mixed --steps 2 --warmup 1 > $out/mixed_dc3.json 2> $out/mixed_dc3.err

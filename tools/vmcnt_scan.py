@@ -20,20 +20,29 @@ def scan(path):
     """EXEC masks are modelled as a stack of regions: `s_and_saveexec` opens a region, `s_xor`,
     `s_or_saveexec` / `s_andn2_saveexec` on EXEC switch to the sibling (else) region, `s_or_b64 exec, exec, s`
     and `s_mov_b64 exec, s` join back to the enclosing one, and other EXEC writes (loop masks,
-    atomic optimisations) start a new region in place. Each VMEM op records its region."""
+    atomic optimisations) start a new region in place. Each VMEM op records its region. The block
+    after an unconditional `s_branch` starts with no outstanding ops (it is entered by jumps)."""
     hits = []
     kern = None
     stack, nxt, pend = [0], 1, []
+    after_jump = False
     for line in open(path):
         m = re.match(r"^[0-9a-f]+ <(.*)>:$", line)
         if m:
             kern, stack, nxt, pend = m.group(1), [0], 1, []
+            after_jump = False
             continue
         code = line.split("//")[0].strip()
         if not code:
             continue
         op = code.split()[0]
         args = code[len(op):].replace(" ", "")
+        if after_jump:
+            # the block after an unconditional jump is entered only by branches, whose
+            # outstanding ops this linear scan does not know: start it with none
+            pend, after_jump = [], False
+        if op == "s_branch":
+            after_jump = True
         if VMEM.match(code):
             pend.append(stack[-1])
         elif op.startswith("s_") and not op.startswith("s_cbranch") and (
