@@ -83,6 +83,45 @@ int salz_gpu_encode_batch_device(salz_gpu_ctx *ctx, const uint8_t *d_src, size_t
                                  size_t block_size, uint8_t *d_dst, size_t dst_cap, size_t *dst_len,
                                  void *stream);
 
+/* ---- one block's suffix array split over several GPUs -------------------
+ * Every rank holds the whole block in its HBM. The suffixes are bucketed by their first two
+ * bytes (contiguous ranges of the 65536 classes, about N / nranks suffixes each, the same plan on
+ * every rank), and each rank prefix-doubles its own bucket with the single-GPU kernels. The only
+ * exchange is rank[i + h] for suffixes i + h of other buckets, once per doubling round: requests
+ * and answers go through the caller's all-to-all over fixed device buffers (RCCL over xGMI, or
+ * gloo with host staging in the tests); an allreduce tells when every bucket is sorted. The
+ * pieces are SA[offsets[r] .. offsets[r + 1]) of the block's suffix array, with their LCPs. */
+typedef struct salz_dist_ops {
+    void *user;
+    /* All-to-all of u32 words from xsend to xrecv (the buffers given below): send_counts[d]
+     * words for rank d, packed in rank order; fill recv_counts[s] (packed in rank order in
+     * xrecv). The library has finished writing xsend when it calls; the data must be in xrecv
+     * when this returns. Return 0 on success. */
+    int (*alltoall)(void *user, const uint64_t *send_counts, uint64_t *recv_counts);
+    /* Sum of *value over the ranks, into *value. Return 0 on success. */
+    int (*allreduce_sum)(void *user, uint64_t *value);
+} salz_dist_ops;
+
+/* This rank's piece of the suffix array of the block d_text[0, N) (device memory, N - 8
+ * suffixes as salz_encode_safe sorts them). xsend / xrecv: device buffers of xcap u32 words
+ * (N words always suffice). d_sa_piece / d_lcp_piece: device buffers of N words; they receive
+ * this rank's SA range and the LCP of each entry with its predecessor (entry 0 of a piece is
+ * left for the caller to fix, see salz_gpu_encode_from_sa). offsets: nranks + 1 values.
+ * *lcp_ok = 0 when the LCPs were not kept (very long repeats: the PLCP stage recomputes them).
+ * Collective: every rank calls it with the same block. Returns 0 / -1. */
+int salz_gpu_dist_suffix_array(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t N, int nranks, int rank,
+                               const salz_dist_ops *ops, uint32_t *d_xsend, uint32_t *d_xrecv,
+                               size_t xcap, uint32_t *d_sa_piece, uint32_t *d_lcp_piece,
+                               uint64_t *offsets, int *lcp_ok);
+
+/* Encode one block from its suffix array (device memory, N - 8 entries, e.g. gathered from the
+ * pieces above) and, when d_lcp is not NULL, its LCP array: the LCPs at the nfix positions in
+ * lcp_fix (a piece's first entry) are recomputed from the text. The stream goes to device buffer
+ * d_dst (capacity dst_cap); *dst_len its length. Returns 0 / -1. */
+int salz_gpu_encode_from_sa(salz_gpu_ctx *ctx, const uint8_t *d_src, size_t N, const uint32_t *d_sa,
+                            const uint32_t *d_lcp, const uint64_t *lcp_fix, size_t nfix, uint8_t *d_dst,
+                            size_t dst_cap, size_t *dst_len);
+
 typedef struct {
     double ms_upload, ms_sa, ms_lcp, ms_ansv, ms_parse, ms_emit, ms_total;
     int32_t sa_rounds, parse_iters;

@@ -93,6 +93,26 @@ lib.salz_decode_blocks.argtypes = [_u8p, _sz, _u8p, _szp, ctypes.c_int]
 lib.salz_decode_blocks.restype = ctypes.c_int
 
 
+# split suffix sort (include/salz_gpu.h salz_dist_ops): collectives supplied by the caller
+DIST_ALLTOALL = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                 ctypes.POINTER(ctypes.c_uint64))
+DIST_ALLREDUCE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
+
+
+class DistOps(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("alltoall", DIST_ALLTOALL), ("allreduce_sum", DIST_ALLREDUCE)]
+
+
+lib.salz_gpu_dist_suffix_array.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _sz, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(DistOps), ctypes.c_void_p, ctypes.c_void_p, _sz,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.POINTER(ctypes.c_int)]
+lib.salz_gpu_dist_suffix_array.restype = ctypes.c_int
+lib.salz_gpu_encode_from_sa.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _sz, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.POINTER(ctypes.c_uint64), _sz, ctypes.c_void_p, _sz, _szp]
+lib.salz_gpu_encode_from_sa.restype = ctypes.c_int
+
+
 class _Dump(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name in
                 ("sa", "psv", "nsv", "lp", "ln", "dlen", "doff", "cost")]

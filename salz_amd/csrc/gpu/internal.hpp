@@ -6,6 +6,7 @@
 #pragma once
 
 #include "common.hpp"
+#include "../../../include/salz_gpu.h"
 
 #include <vector>
 
@@ -65,6 +66,7 @@ struct Workspace {
     uint64_t *lrec = nullptr;  // per large group: (start in extracted array << 32) | start
     uint32_t *lg2g = nullptr;  // per large group: its group id
     uint8_t *dc3 = nullptr;    // DC3 suffix sorter's level arena (dc3.hip), allocated on first use
+    uint8_t *dist_owner = nullptr;  // split suffix sort: owning rank per two-byte class (dsa.hip)
     size_t dc3_bytes = 0;
     uint8_t *out = nullptr;                                              // encoded_len_max
     size_t out_cap = 0;
@@ -123,7 +125,25 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
 constexpr uint32_t kMaxBatchBlocks = 4096;
 
 // stages; every one takes the batch geometry (one block: Blocks{0xffffffff, 1, n})
-int stage_suffix_array(Workspace &ws, const Blocks &bl);           // sa.hip   -> ws.sa
+// One block's suffix array split over ranks (dsa.hip): this rank sorts the suffixes whose first
+// two bytes fall in its bucket (list, m0 of them, global SA positions gbase ..); rank[i + h] of
+// other buckets comes through the caller's all-to-all (ops).
+struct DistSa {
+    const struct ::salz_dist_ops *ops;
+    int rank, nranks;
+    const uint8_t *owner;  // device: owning rank per two-byte class (65536)
+    const uint32_t *list;  // device: own suffixes in round-0 order
+    uint32_t m0, gbase;
+    uint32_t n;               // the block's suffixes
+    uint32_t *xsend, *xrecv;  // device exchange buffers (u32 words), xcap each
+    size_t xcap;
+};
+int dist_suffix_array(Workspace &ws, uint32_t n, int nranks, int rank, const salz_dist_ops *ops, uint32_t *xsend,
+                      uint32_t *xrecv, size_t xcap, uint64_t *offsets, uint32_t *m0_out);
+int dist_keys(Workspace &ws, const DistSa &d, const uint32_t *nval, const uint32_t *ngid, uint32_t m, uint32_t h,
+              int kb, uint64_t *key);
+int dist_idle_rounds(Workspace &ws, const DistSa &d);
+int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist = nullptr);  // sa.hip -> ws.sa
 // dc3.hip -> ws.sa for one block (repetitive inputs); symbols = codes.code[byte] (1..sigma) or
 // byte + 1 when raw
 int stage_suffix_array_dc3(Workspace &ws, const Blocks &bl, const Alpha &codes, int raw);

@@ -377,14 +377,20 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
                 cd[u] = cand[base + ((size_t)j << 6)];
             }
         };
+        // a target equal to the previous row's (one match's end) was checked already: such a row
+        // reads b's costs instead (which pass by definition)
+        uint32_t lqp = 0xffffffffu, lqn = 0xffffffffu;
         auto check = [&](const uint4(&cd)[8], uint32_t j0) {
 #pragma unroll
             for (uint32_t u = 0; u < 8; u++) {
                 const uint32_t p = a + j0 + u;
                 const bool on = j0 + u < jn && p != b0;
-                const bool xp = on && cd[u].y >= 3u && p + cd[u].y >= b;
-                const bool xn = on && cd[u].w >= 3u && p + cd[u].w >= b;
-                const size_t sp = sidx(xp ? p + cd[u].y : b, klog), sn = sidx(xn ? p + cd[u].w : b, klog);
+                const uint32_t qp = p + cd[u].y, qn = p + cd[u].w;
+                const bool xp = on && cd[u].y >= 3u && qp >= b && qp != lqp;
+                const bool xn = on && cd[u].w >= 3u && qn >= b && qn != lqn;
+                lqp = on && cd[u].y >= 3u ? qp : 0xffffffffu;
+                lqn = on && cd[u].w >= 3u ? qn : 0xffffffffu;
+                const size_t sp = sidx(xp ? qp : b, klog), sn = sidx(xn ? qn : b, klog);
                 const uint32_t vp = cnew[sp], vn = cnew[sn];
                 bad |= vp - cold[sp] != d0 || vp >= (1u << 30);
                 bad |= vn - cold[sn] != d0 || vn >= (1u << 30);

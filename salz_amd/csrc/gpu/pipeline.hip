@@ -91,7 +91,7 @@ void workspace_free(Workspace &ws)
         (void)hipSetDevice(ws.device);
     void *ptrs[] = {ws.text, ws.rank,     ws.sa,   ws.keyA, ws.keyB, ws.valA, ws.valB,
                     ws.u0,   ws.u1,       ws.u2,   ws.u3,   ws.g64,  ws.offA, ws.offB, ws.lcps,
-                    ws.cand, ws.pst, ws.lsc, ws.lrec, ws.lg2g, ws.dc3, ws.out, ws.radix_counts,  ws.scan_tmp,      ws.dscal};
+                    ws.cand, ws.pst, ws.lsc, ws.lrec, ws.lg2g, ws.dc3, ws.dist_owner, ws.out, ws.radix_counts,  ws.scan_tmp,      ws.dscal};
     for (void *p : ptrs)
         if (p)
             (void)hipFree(p);
@@ -355,12 +355,56 @@ static int dump_after_parse(Workspace &ws, uint32_t n, const salz_gpu_dump *d)
     return 0;
 }
 
+// LCP of SA[r - 1] and SA[r] for the listed ranks r (a split suffix array's piece starts):
+// one wave per entry, 8 bytes per lane and step.
+__global__ void k_lcp_fix(const uint32_t *__restrict__ sa, const uint8_t *__restrict__ T, uint32_t n,
+                          const uint64_t *__restrict__ fix, uint32_t nfix, uint32_t *__restrict__ lcp)
+{
+    const uint32_t e = blockIdx.x;
+    if (e >= nfix)
+        return;
+    const uint64_t r = fix[e];
+    if (r >= n)
+        return;
+    if (r == 0) {
+        if (threadIdx.x == 0)
+            lcp[0] = 0;
+        return;
+    }
+    const uint32_t a = sa[r - 1], b = sa[r];
+    const uint32_t lim = n - (a > b ? a : b);
+    uint32_t res = lim;
+    for (uint32_t base = 0; base < lim; base += 64 * 8) {
+        const uint32_t off = base + threadIdx.x * 8;
+        const uint64_t x = load_u64_any(T, (size_t)a + off) ^ load_u64_any(T, (size_t)b + off);
+        uint32_t mm = 0xffffffffu;
+        if (off < lim && x)
+            mm = off + ((uint32_t)__builtin_ctzll(x) >> 3);
+        mm = wave_min_u32(mm);
+        if (mm != 0xffffffffu) {
+            res = mm < lim ? mm : lim;
+            break;
+        }
+    }
+    if (threadIdx.x == 0)
+        lcp[r] = res;
+}
+
+// A suffix array (and LCP array) computed elsewhere, e.g. gathered from the pieces of a split
+// suffix sort (dsa.hip): encode_core then starts at the candidates.
+struct ExtSa {
+    const uint32_t *sa, *lcp;
+    const uint64_t *fix;  // host: LCP entries to recompute
+    size_t nfix;
+};
+
 // Encode a batch: P bytes of src (host or device memory) as consecutive blocks of bs bytes
 // (bs >= P: one block), every block's stream into device memory at dst + b * stride (at most
 // cap bytes each), lens[b] = its length. A batch of several blocks needs bs to be a multiple
 // of 512 (parse chunks never straddle two blocks) and every block longer than 8 bytes.
 static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P, size_t bs,
-                       uint8_t *dst, size_t stride, size_t cap, size_t *lens, const salz_gpu_dump *dump)
+                       uint8_t *dst, size_t stride, size_t cap, size_t *lens, const salz_gpu_dump *dump,
+                       const ExtSa *ext = nullptr)
 {
     const size_t nbz = bs >= P ? 1 : (P + bs - 1) / bs;
     const size_t N_last = nbz == 1 ? P : P - (nbz - 1) * bs;
@@ -404,7 +448,23 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P
         return -1;
     }
     if (mark(ws, EV_UP)) return -1;
-    if (stage_suffix_array(ws, bl) || guard_check(ws, "sa") || (nbz == 1 && check_stage(ws, n, 2))) return -1;
+    if (ext) {
+        SALZ_HIP(hipMemcpyAsync(ws.sa, ext->sa, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+        ws.lcps_ok = ext->lcp != nullptr;
+        if (ws.lcps_ok) {
+            SALZ_HIP(hipMemcpyAsync(ws.lcps, ext->lcp, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+            if (ext->nfix) {
+                uint64_t *dfix = reinterpret_cast<uint64_t *>(ws.lsc);  // free before the candidates
+                SALZ_HIP(hipMemcpyAsync(dfix, ext->fix, ext->nfix * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+                hipLaunchKernelGGL(k_lcp_fix, dim3((unsigned)ext->nfix), dim3(64), 0, st, ws.sa, ws.text, n, dfix,
+                                   (uint32_t)ext->nfix, ws.lcps);
+                SALZ_LAUNCH_CHECK();
+            }
+        }
+    } else if (stage_suffix_array(ws, bl)) {
+        return -1;
+    }
+    if (guard_check(ws, "sa") || (nbz == 1 && check_stage(ws, n, 2))) return -1;
     if (mark(ws, EV_SA)) return -1;
     if (dump_after_sa(ws, bl.nsa(), dump)) return -1;
     // The suffix sorter usually leaves the LCP array behind (sa.hip, "LCP"); otherwise the
@@ -723,6 +783,64 @@ static int encode_host_locked(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_
         return -1;
     }
     *dst_len = len;  // set only on success (lib/salz.c:818)
+    return 0;
+}
+
+int salz_gpu_dist_suffix_array(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t N, int nranks, int rank,
+                               const salz_dist_ops *ops, uint32_t *d_xsend, uint32_t *d_xrecv,
+                               size_t xcap, uint32_t *d_sa_piece, uint32_t *d_lcp_piece,
+                               uint64_t *offsets, int *lcp_ok)
+{
+    if (!ctx || !d_text || !ops || !ops->alltoall || !ops->allreduce_sum || !d_xsend || !d_xrecv ||
+        !d_sa_piece || !d_lcp_piece || !offsets || !lcp_ok) {
+        set_error("NULL argument");
+        return -1;
+    }
+    if (N <= 8 || N - 8 >= 0x7fffffffu) {
+        set_error("block of %zu bytes: the reference codec needs more than 8 bytes", N);
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    Workspace &ws = ctx->ws;
+    if (N > ws.cap_N && workspace_alloc(ws, ws.device, N) != 0)
+        return -1;
+    SALZ_HIP(hipSetDevice(ws.device));
+    hipStream_t st = ws.stream;
+    ws.stats = StageStats{};
+    SALZ_HIP(hipMemcpyAsync(ws.text, d_text, N, hipMemcpyDeviceToDevice, st));
+    SALZ_HIP(hipMemsetAsync(ws.text + N, 0, 128, st));
+    const uint32_t n = (uint32_t)(N - 8);
+    uint32_t m0 = 0;
+    if (dist_suffix_array(ws, n, nranks, rank, ops, d_xsend, d_xrecv, xcap, offsets, &m0) != 0)
+        return -1;
+    if (m0) {
+        SALZ_HIP(hipMemcpyAsync(d_sa_piece, ws.sa, (size_t)m0 * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+        if (ws.lcps_ok)
+            SALZ_HIP(hipMemcpyAsync(d_lcp_piece, ws.lcps, (size_t)m0 * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                    st));
+    }
+    SALZ_HIP(hipStreamSynchronize(st));
+    *lcp_ok = m0 == 0 || ws.lcps_ok ? 1 : 0;
+    return 0;
+}
+
+int salz_gpu_encode_from_sa(salz_gpu_ctx *ctx, const uint8_t *d_src, size_t N, const uint32_t *d_sa,
+                            const uint32_t *d_lcp, const uint64_t *lcp_fix, size_t nfix, uint8_t *d_dst,
+                            size_t dst_cap, size_t *dst_len)
+{
+    if (!ctx || !d_src || !d_sa || !d_dst || !dst_len || (nfix && !lcp_fix)) {
+        set_error("NULL argument");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    Workspace &ws = ctx->ws;
+    if (N > ws.cap_N && workspace_alloc(ws, ws.device, N) != 0)
+        return -1;
+    const ExtSa ext{d_sa, d_lcp, lcp_fix, nfix};
+    size_t len = 0;
+    if (encode_core(ws, d_src, true, N, N, d_dst, 0, dst_cap, &len, nullptr, &ext) != 0)
+        return -1;
+    *dst_len = len;
     return 0;
 }
 

@@ -57,6 +57,19 @@ __global__ void k_sa_init(const uint8_t *__restrict__ T, Blocks g, Alpha a, uint
     val[c] = i;
 }
 
+// Round-0 pairs of a split block's own suffixes (list order: short ones first, shortest first,
+// then text order).
+__global__ void k_list_init(const uint8_t *__restrict__ T, const uint32_t *__restrict__ list, uint32_t m,
+                            uint32_t n, Alpha a, uint64_t *__restrict__ key, uint32_t *__restrict__ val)
+{
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (c >= m)
+        return;
+    const uint32_t i = list[c];
+    key[c] = round0_key(T, i, n, a);
+    val[c] = i;
+}
+
 // Tm[i] = symbol of T[i] (and 64 zero bytes of padding past P), for round0_key_mapped.
 __global__ void k_map_text(const uint8_t *__restrict__ T, size_t P, Alpha a, uint8_t *__restrict__ Tm)
 {
@@ -286,7 +299,7 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
                          uint32_t *__restrict__ nval, uint32_t *__restrict__ ngid,
                          uint32_t *__restrict__ rank, uint32_t *__restrict__ sa, GroupTab tab,
                          uint32_t m, uint32_t n, uint32_t nsa, int kb_old, int round0, uint32_t *err,
-                         uint32_t ihi, uint32_t *__restrict__ later)
+                         uint32_t ihi, uint32_t *__restrict__ later, uint32_t gbase)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
@@ -306,7 +319,7 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     // rounds write only the ranks of i < ihi here and leave every update in list order in
     // `later` for the split passes (k_rank_upper) or the staged scatter (k_rank_stage /
     // k_rank_apply); small ones write rank directly (ihi = ~0, no `later`).
-    const uint32_t rv = same ? 0xffffffffu : hp + o + 1u;
+    const uint32_t rv = same ? 0xffffffffu : gbase + hp + o + 1u;  // (gbase: a split block's bucket)
     if (!same && i < ihi)
         rank[i] = rv;
     if (later)
@@ -821,10 +834,11 @@ __global__ void k_keys(const uint32_t *__restrict__ nval, const uint32_t *__rest
 
 }  // namespace
 
-int stage_suffix_array(Workspace &ws, const Blocks &bl)
+int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
 {
     hipStream_t st = ws.stream;
-    const uint32_t n = bl.npos, nsa = bl.nsa();  // position space, live suffixes
+    // position space, live suffixes (a split block: this rank's bucket)
+    const uint32_t n = bl.npos, nsa = dist ? dist->m0 : bl.nsa();
     if (nsa == 0)
         return 0;
     uint64_t *K = ws.keyA;
@@ -862,8 +876,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
     // with more than 3/4 of its suffixes still unfinished (long repeats: the following rounds stay
     // that wide; text keeps ~17% at depth 32, Fibonacci and periodic blocks all of them).
     const char *algo_env = getenv("SALZ_SA_ALGO");
-    const bool dc3_force = algo_env && !strcmp(algo_env, "dc3") && bl.nb == 1 && n >= 2;
-    const bool dc3_auto = !(algo_env && !strcmp(algo_env, "doubling")) && bl.nb == 1 && n >= (1u << 20);
+    const bool dc3_force = algo_env && !strcmp(algo_env, "dc3") && bl.nb == 1 && n >= 2 && !dist;
+    const bool dc3_auto = !(algo_env && !strcmp(algo_env, "doubling")) && bl.nb == 1 && n >= (1u << 20) && !dist;
     // SALZ_SA_PROBE=0: no repetition probe (only the depth-32 switch)
     const bool dc3_probe_off = getenv("SALZ_SA_PROBE") && atoi(getenv("SALZ_SA_PROBE")) == 0;
     bool dc3_now = false;
@@ -920,12 +934,16 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
     // Round 0's first radix pass reads the text itself (radix.hip, TextSrc); the initial
     // key/value arrays are only materialised for the per-round checks, and for n = 1 (the
     // sort has nothing to do and would leave them unwritten).
-    const bool text_first = !dbg_rounds && nsa > 1;
-    if (!text_first) {
+    const bool text_first = !dbg_rounds && nsa > 1 && !dist;
+    if (dist) {
+        hipLaunchKernelGGL(k_list_init, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.text, dist->list, nsa, n, alpha,
+                           K, V);
+        SALZ_LAUNCH_CHECK();
+    } else if (!text_first) {
         hipLaunchKernelGGL(k_sa_init, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.text, bl, alpha, K, V);
         SALZ_LAUNCH_CHECK();
     }
-    if (dbg_rounds && bl.nb == 1) {
+    if (dbg_rounds && bl.nb == 1 && !dist) {
         hipLaunchKernelGGL(k_dbg_pairs, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, K, V, ws.rank, ws.text, nsa, bl,
                            alpha, 0u, 0, 1, derr);
         SALZ_LAUNCH_CHECK();
@@ -1081,7 +1099,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
         const uint32_t ihi = mode == 0 ? 0xffffffffu : mode == 1 ? span : 0u;
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, headpos,
                            gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, nsa, kb_old,
-                           round0, derr, ihi, mode ? later : nullptr);
+                           round0, derr, ihi, mode ? later : nullptr, dist ? dist->gbase : 0u);
         SALZ_LAUNCH_CHECK();
         for (uint32_t q = 1; q < parts; q++) {
             hipLaunchKernelGGL(k_rank_upper, dim3(grid_for(m, kT)), dim3(kT), 0, st, V, later, m,
@@ -1120,17 +1138,36 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
                     mnew, Gnew, std::chrono::duration<double, std::milli>(now - t_round).count());
             t_round = now;
         }
-        if (mnew == 0)
+        if (dist) {  // a split block ends when every rank's bucket is sorted
+            uint64_t g = mnew;
+            if (dist->ops->allreduce_sum(dist->ops->user, &g) != 0) {
+                set_error("split suffix sort: allreduce failed");
+                return -1;
+            }
+            if (g == 0)
+                break;
+            if (mnew == 0) {  // sorted here: keep answering the other ranks' rank requests
+                if (dist_idle_rounds(ws, *dist) != 0)
+                    return -1;
+                break;
+            }
+        } else if (mnew == 0) {
             break;
+        }
         if (dc3_auto && h >= 32 && (uint64_t)mnew * 4 > (uint64_t)n * 3)
             return stage_suffix_array_dc3(ws, bl, codes, codes_raw);
         if (h >= n || Gnew == 0) {
             set_error("suffix sort did not converge (h=%u n=%u m=%u)", h, n, mnew);
             return -1;
         }
-        hipLaunchKernelGGL(k_keys, dim3(grid_for(mnew, kT)), dim3(kT), 0, st, Vx, ngid, ws.rank,
-                           mnew, n, h, kb, Kx, derr);
-        SALZ_LAUNCH_CHECK();
+        if (dist) {  // rank[i + h] lives with the rank that owns suffix i + h
+            if (dist_keys(ws, *dist, Vx, ngid, mnew, h, kb, Kx) != 0)
+                return -1;
+        } else {
+            hipLaunchKernelGGL(k_keys, dim3(grid_for(mnew, kT)), dim3(kT), 0, st, Vx, ngid, ws.rank,
+                               mnew, n, h, kb, Kx, derr);
+            SALZ_LAUNCH_CHECK();
+        }
         K = Kx;
         V = Vx;
         m = mnew;
@@ -1145,7 +1182,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl)
         offn = t;
     }
     static const bool check = getenv("SALZ_CHECK_SA") != nullptr;
-    if (check) {
+    if (check && !dist) {
         SALZ_HIP(hipMemsetAsync(ws.u0, 0, sizeof(uint32_t) * n, st));
         hipLaunchKernelGGL(k_sa_check, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.sa, nsa, n, ws.u0, derr);
         SALZ_LAUNCH_CHECK();

@@ -18,6 +18,7 @@ HBM. The same code runs on gloo with CPU tensors (tests/test_dist.py, world 2 an
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Callable, Optional, Sequence
 
 import numpy as np
@@ -146,3 +147,150 @@ def encode_container(src: np.ndarray, block_size: int, encode_block: Callable[[n
                      for s in streams], lens, packed)
     out = gather_container(packed, n, block_size, rank, world, group)
     return None if out is None else out.numpy().tobytes()
+
+
+# ---- one block's suffix array split over the ranks (dsa.hip) -------------------
+
+class _Collectives:
+    """The all-to-all and allreduce the library's split suffix sort calls back (salz_dist_ops),
+    over torch.distributed: device tensors straight through RCCL (nccl backend, xGMI), or staged
+    through host memory for gloo (the tests: several ranks on one GPU)."""
+
+    def __init__(self, xsend, xrecv, world: int, group=None):
+        import torch
+        import torch.distributed as dist
+
+        import salz_amd
+
+        self.xsend, self.xrecv, self.world, self.group = xsend, xrecv, world, group
+        self.host = dist.get_backend(group) == "gloo"
+        self.cdev = torch.device("cpu") if self.host else xsend.device
+        self.error = None
+        self._a2a = salz_amd.DIST_ALLTOALL(self._alltoall)
+        self._ar = salz_amd.DIST_ALLREDUCE(self._allreduce)
+        self.ops = salz_amd.DistOps(None, self._a2a, self._ar)
+
+    def _alltoall(self, _user, send_counts, recv_counts):
+        import torch
+        import torch.distributed as dist
+
+        try:
+            sc = [int(send_counts[i]) for i in range(self.world)]
+            t = torch.tensor(sc, dtype=torch.int64, device=self.cdev)
+            r = torch.empty_like(t)
+            dist.all_to_all_single(r, t, group=self.group)
+            rc = [int(v) for v in r.tolist()]
+            for i, v in enumerate(rc):
+                recv_counts[i] = v
+            ns, nr = sum(sc), sum(rc)
+            if self.host:
+                recv = torch.empty(nr, dtype=torch.int32)
+                dist.all_to_all_single(recv, self.xsend[:ns].cpu(), rc, sc, group=self.group)
+                self.xrecv[:nr].copy_(recv)
+            else:
+                dist.all_to_all_single(self.xrecv[:nr], self.xsend[:ns], rc, sc, group=self.group)
+            if self.xsend.is_cuda:
+                torch.cuda.synchronize(self.xsend.device)
+            return 0
+        except Exception as e:  # reported by the caller; the library fails the call
+            self.error = e
+            return -1
+
+    def _allreduce(self, _user, value):
+        import torch
+        import torch.distributed as dist
+
+        try:
+            t = torch.tensor([int(value[0])], dtype=torch.int64, device=self.cdev)
+            dist.all_reduce(t, group=self.group)
+            value[0] = int(t.item())
+            return 0
+        except Exception as e:
+            self.error = e
+            return -1
+
+
+def _gather_pieces(piece, offsets, rank: int, world: int, full, group=None, host: bool = False):
+    """Rank r's piece (int32 tensor, offsets[r+1] - offsets[r] entries) into full[offsets[r]:...]
+    on rank 0, point to point."""
+    import torch
+    import torch.distributed as dist
+
+    lens = [offsets[r + 1] - offsets[r] for r in range(world)]
+    if rank != 0:
+        if lens[rank]:
+            src = piece[:lens[rank]].cpu() if host else piece[:lens[rank]]
+            dist.send(src, 0, group=group)
+        return
+    full[:lens[0]].copy_(piece[:lens[0]])
+    for r in range(1, world):
+        if lens[r]:
+            if host:
+                buf = torch.empty(lens[r], dtype=torch.int32)
+                dist.recv(buf, r, group=group)
+                full[offsets[r]:offsets[r + 1]].copy_(buf)
+            else:
+                dist.recv(full[offsets[r]:offsets[r + 1]], r, group=group)
+
+
+def encode_block_split(src: np.ndarray, device: int = 0, group=None, ctx=None) -> Optional[bytes]:
+    """One block encoded with its suffix array split over the ranks of `group` (every rank
+    passes the same block). Each rank sorts its two-byte-prefix bucket on its GPU, exchanging
+    only rank[i + h] requests per doubling round; rank 0 gathers the pieces (and their LCPs) and
+    runs the rest of the pipeline. Returns the stream on rank 0 (bit-identical to
+    salz_encode_safe), None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    import salz_amd
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    s = np.ascontiguousarray(np.asarray(src, dtype=np.uint8).reshape(-1))
+    N = len(s)
+    n = N - 8
+    dev = torch.device("cuda", device)
+    own = ctx is None
+    if own:
+        ctx = salz_amd.Context(device, N)
+    try:
+        text = torch.from_numpy(s.copy()).to(dev)
+        xcap = N + 64
+        xsend = torch.empty(xcap, dtype=torch.int32, device=dev)
+        xrecv = torch.empty(xcap, dtype=torch.int32, device=dev)
+        sa_piece = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        lcp_piece = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)
+        coll = _Collectives(xsend, xrecv, world, group)
+        offs = (ctypes.c_uint64 * (world + 1))()
+        lcp_ok = ctypes.c_int(0)
+        rc = salz_amd.lib.salz_gpu_dist_suffix_array(
+            ctx.handle, text.data_ptr(), N, world, rank, ctypes.byref(coll.ops), xsend.data_ptr(),
+            xrecv.data_ptr(), xcap, sa_piece.data_ptr(), lcp_piece.data_ptr(), offs, ctypes.byref(lcp_ok))
+        if rc != 0:
+            raise salz_amd.SalzError(f"split suffix sort failed: {salz_amd.last_error()} {coll.error or ''}")
+        offsets = [int(offs[i]) for i in range(world + 1)]
+        ok = torch.tensor([lcp_ok.value], dtype=torch.int64, device=coll.cdev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        with_lcp = bool(ok.item())
+        full_sa = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if rank == 0 else None
+        full_lcp = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if rank == 0 and with_lcp else None
+        _gather_pieces(sa_piece, offsets, rank, world, full_sa, group, coll.host)
+        if with_lcp:
+            _gather_pieces(lcp_piece, offsets, rank, world, full_lcp, group, coll.host)
+        if rank != 0:
+            return None
+        fix = [o for o in offsets[:world] if o < n]  # every piece's first entry
+        fixa = (ctypes.c_uint64 * max(len(fix), 1))(*fix)
+        cap = salz_amd.encoded_len_max(N)
+        out = torch.empty(cap, dtype=torch.uint8, device=dev)
+        olen = ctypes.c_size_t(0)
+        torch.cuda.synchronize(dev)
+        if salz_amd.lib.salz_gpu_encode_from_sa(ctx.handle, text.data_ptr(), N, full_sa.data_ptr(),
+                                                full_lcp.data_ptr() if with_lcp else None, fixa,
+                                                len(fix) if with_lcp else 0, out.data_ptr(), cap,
+                                                ctypes.byref(olen)) != 0:
+            raise salz_amd.SalzError(f"encode from suffix array failed: {salz_amd.last_error()}")
+        return out[:olen.value].cpu().numpy().tobytes()
+    finally:
+        if own:
+            ctx.close()

@@ -1,0 +1,40 @@
+"""One rank of a split-suffix-array encode (salz_amd.dist.encode_block_split), for
+tests/test_dist_split.py: every rank encodes the same blocks over gloo on one GPU; rank 0 writes
+the streams.
+
+  python tests/split_worker.py RANK WORLD PORT IN.npz OUT.npz
+"""
+import os
+import sys
+
+import numpy as np
+
+
+def main():
+    rank, world, port = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    src_path, out_path = sys.argv[4], sys.argv[5]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch.distributed as dist
+
+    import salz_amd
+    from salz_amd.dist import encode_block_split
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    data = np.load(src_path)
+    names = sorted(data.files)
+    ctx = salz_amd.Context(0, max(len(data[k]) for k in names))
+    out = {}
+    for k in names:
+        s = encode_block_split(data[k], 0, ctx=ctx)
+        if rank == 0:
+            out[k] = np.frombuffer(s, np.uint8)
+    ctx.close()
+    if rank == 0:
+        np.savez(out_path, **out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

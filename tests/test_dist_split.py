@@ -1,0 +1,64 @@
+"""One block's suffix array split over several ranks (dsa.hip,
+salz_amd.dist.encode_block_split): each rank sorts its two-byte-prefix bucket on the GPU and
+exchanges rank requests per doubling round; rank 0 gathers the pieces and encodes. The stream
+must equal the CPU port's. The ranks run gloo with host-staged buffers, all on the box's one
+GPU (RCCL refuses two ranks on one device); the RCCL path differs only in the backend."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from tests.helpers import ROOT, gen, oracle_encode
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _inputs():
+    rng = np.random.default_rng(3)
+    return {
+        "text": gen("text", 2_000_003, 5),
+        "mixed": gen("mixed", 1_500_000, 6),
+        "fib": gen("fib", 1_048_575),  # long repeats: LCPs from the PLCP stage
+        "small": gen("text", 1000, 2),
+        "zeros": np.zeros(50_000, np.uint8),  # one class: every other bucket is empty
+        "rand": rng.integers(0, 256, 100_000, dtype=np.uint8),  # PLAIN
+        "smx4": gen("smx", 300_000, 2, 4),
+    }
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_suffix_array_matches_oracle(tmp_path, world):
+    inputs = _inputs()
+    src = tmp_path / "in.npz"
+    out = tmp_path / "out.npz"
+    np.savez(src, **inputs)
+    port = _port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "split_worker.py"), str(r), str(world),
+                               str(port), str(src), str(out)], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT)
+             for r in range(world)]
+    logs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=180)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("split workers timed out")
+        logs.append(o.decode(errors="replace"))
+    assert all(p.returncode == 0 for p in procs), "\n".join(logs)
+    got = np.load(out)
+    for k, s in inputs.items():
+        rc, ref = oracle_encode(s)
+        assert rc == 0
+        assert got[k].tobytes() == ref, k
