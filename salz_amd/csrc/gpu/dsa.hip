@@ -84,23 +84,23 @@ __global__ void k_dist_req(const uint32_t *__restrict__ nval, uint32_t m, uint32
     val[c] = (uint32_t)c;
 }
 
-// Requests per destination (sorted by destination) and the packed request words.
-__global__ void k_dist_pack(const uint64_t *__restrict__ key, uint32_t m, uint32_t *__restrict__ words,
-                            unsigned long long *__restrict__ counts)
+// The packed request words, and where each destination's run starts in the list (sorted by
+// destination): start[d] for d in (dest(c - 1), dest(c)] is c; past the last one, m.
+__global__ void k_dist_pack(const uint64_t *__restrict__ key, uint32_t m, uint32_t nranks,
+                            uint32_t *__restrict__ words, unsigned long long *__restrict__ start)
 {
-    __shared__ uint32_t cnt[256];
-    if (threadIdx.x < 256)
-        cnt[threadIdx.x] = 0;
-    __syncthreads();
     const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (c < m) {
-        const uint64_t k = key[c];
-        words[c] = (uint32_t)k;
-        atomicAdd(&cnt[(uint32_t)(k >> 32) & 255u], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < 256 && cnt[threadIdx.x])
-        atomicAdd(&counts[threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+    if (c >= m)
+        return;
+    const uint64_t k = key[c];
+    words[c] = (uint32_t)k;
+    const uint32_t d = (uint32_t)(k >> 32);
+    const int dp = c ? (int)(uint32_t)(key[c - 1] >> 32) : -1;
+    for (int e = dp + 1; e <= (int)d; e++)
+        start[e] = c;
+    if (c + 1 == m)
+        for (uint32_t e = d + 1; e <= nranks; e++)
+            start[e] = m;
 }
 
 __global__ void k_dist_answer(const uint32_t *__restrict__ req, uint64_t total, uint32_t n,
@@ -184,13 +184,15 @@ int dist_keys(Workspace &ws, const DistSa &d, const uint32_t *nval, const uint32
     const int obits = bit_width((uint64_t)(d.nranks > 1 ? d.nranks - 1 : 1));
     if (radix_sort_pairs(&rk, &rv, rk_alt, rv_alt, m, 32, 32 + obits, ws, st) != 0)
         return -1;
-    unsigned long long *cnt = reinterpret_cast<unsigned long long *>(ws.dscal) + 400;
-    SALZ_HIP(hipMemsetAsync(cnt, 0, 256 * sizeof(uint64_t), st));
-    hipLaunchKernelGGL(k_dist_pack, dim3(grid_for(m, kT)), dim3(kT), 0, st, rk, m, d.xsend, cnt);
+    unsigned long long *start = reinterpret_cast<unsigned long long *>(ws.dscal) + 400;
+    hipLaunchKernelGGL(k_dist_pack, dim3(grid_for(m, kT)), dim3(kT), 0, st, rk, m, (uint32_t)d.nranks, d.xsend,
+                       start);
     SALZ_LAUNCH_CHECK();
-    if (read_scalars(ws, 400 * 8, (size_t)d.nranks * 8, "dsa.counts") != 0)
+    if (read_scalars(ws, 400 * 8, ((size_t)d.nranks + 1) * 8, "dsa.counts") != 0)
         return -1;
-    std::vector<uint64_t> send(ws.hscal + 400, ws.hscal + 400 + d.nranks);
+    std::vector<uint64_t> send(d.nranks);
+    for (int r = 0; r < d.nranks; r++)
+        send[r] = ws.hscal[400 + r + 1] - ws.hscal[400 + r];
     if (dist_answer_round(ws, d, send.data()) != 0)
         return -1;
     hipLaunchKernelGGL(k_dist_place, dim3(grid_for(m, kT)), dim3(kT), 0, st, rv, d.xrecv, m, ngid, kb, key);

@@ -62,11 +62,14 @@ __global__ void k_sa_init(const uint8_t *__restrict__ T, Blocks g, Alpha a, uint
 __global__ void k_list_init(const uint8_t *__restrict__ T, const uint32_t *__restrict__ list, uint32_t m,
                             uint32_t n, Alpha a, uint64_t *__restrict__ key, uint32_t *__restrict__ val)
 {
+    __shared__ uint8_t code[256];
+    load_codes(code, a);
+    __syncthreads();
     const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
         return;
     const uint32_t i = list[c];
-    key[c] = round0_key(T, i, n, a);
+    key[c] = round0_key(T, i, n, a, code);
     val[c] = i;
 }
 
