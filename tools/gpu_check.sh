@@ -3,7 +3,7 @@
 # Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
 export TMPDIR=/tmp
-out=gpurun_out/${TAG:-run}
+out=gpurun_out/${TAG:-r02w}
 mkdir -p $out
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $out/pytest.log 2>&1 &&
 timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke()' > $out/smoke.log 2>&1 &&
