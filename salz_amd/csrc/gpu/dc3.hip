@@ -28,6 +28,7 @@
 // Symbols and ranks of a level are interleaved (TR[q] = {t[q], rank[q]}), so the merge's
 // comparison operands of one suffix are one 24-byte run.
 #include "internal.hpp"
+#include "scatter.hpp"
 
 #include <cstdlib>
 #include <cstring>
@@ -120,6 +121,30 @@ __global__ void k_dc3_rank(const uint32_t *__restrict__ sar, uint32_t ns, uint32
     if (p < n)
         tr[p].y = (uint32_t)r + 1u;
 }
+
+// The same two scatters for scatter_staged (scatter.hpp): TR as u32 words, index = position.
+struct RankSrc {
+    const uint32_t *sar;
+    uint32_t ns, n1, n;
+    __device__ __forceinline__ bool operator()(size_t r, uint32_t &idx, uint32_t &val) const
+    {
+        const uint32_t j = sar[r];
+        idx = dc3_pos(j, n1);
+        val = (uint32_t)r + 1u;
+        return j < ns && idx < n;
+    }
+};
+
+struct NameSrc {
+    const uint32_t *v, *name;
+    uint32_t ns;
+    __device__ __forceinline__ bool operator()(size_t c, uint32_t &idx, uint32_t &val) const
+    {
+        idx = v[c];
+        val = name[c];
+        return idx < ns;
+    }
+};
 
 __global__ void k_dc3_mod0_flags(const uint32_t *__restrict__ sar, uint32_t ns, uint32_t n1,
                                  uint32_t *__restrict__ flag)
@@ -327,17 +352,30 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
             set_error("dc3: arena exhausted at level %d (n=%u)", d.levels, n);
             return -1;
         }
-        SALZ_HIP(hipMemsetAsync(child + ns, 0, 8 * sizeof(uint2), st));
-        hipLaunchKernelGGL(k_dc3_names, dim3(grid_for(ns, kT)), dim3(kT), 0, st, V, name, ns, child);
-        SALZ_LAUNCH_CHECK();
+        if (scatter_stage_wanted((size_t)ns * sizeof(uint2))) {  // x = name, y = 0
+            SALZ_HIP(hipMemsetAsync(child, 0, ((size_t)ns + 8) * sizeof(uint2), st));
+            if (scatter_staged(NameSrc{V, name, ns}, ns, ns, reinterpret_cast<uint32_t *>(child), 2u, 0u,
+                               reinterpret_cast<uint2 *>(ws.lsc), 2 * ws.cap_s, ws.radix_counts, st) != 0)
+                return -1;
+        } else {
+            SALZ_HIP(hipMemsetAsync(child + ns, 0, 8 * sizeof(uint2), st));
+            hipLaunchKernelGGL(k_dc3_names, dim3(grid_for(ns, kT)), dim3(kT), 0, st, V, name, ns, child);
+            SALZ_LAUNCH_CHECK();
+        }
         if (dc3_level(d, child, ns, bit_width(D), sar) != 0)
             return -1;
     } else {
         sar = ws.u2;  // the sorted sample is the order (survives the mod-0 sort below)
         SALZ_HIP(hipMemcpyAsync(sar, V, (size_t)ns * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
     }
-    hipLaunchKernelGGL(k_dc3_rank, dim3(grid_for(ns, kT)), dim3(kT), 0, st, sar, ns, n1, n, tr, d.derr);
-    SALZ_LAUNCH_CHECK();
+    if (scatter_stage_wanted((size_t)n * sizeof(uint2))) {
+        if (scatter_staged(RankSrc{sar, ns, n1, n}, ns, n, reinterpret_cast<uint32_t *>(tr), 2u, 1u,
+                           reinterpret_cast<uint2 *>(ws.lsc), 2 * ws.cap_s, ws.radix_counts, st) != 0)
+            return -1;
+    } else {
+        hipLaunchKernelGGL(k_dc3_rank, dim3(grid_for(ns, kT)), dim3(kT), 0, st, sar, ns, n1, n, tr, d.derr);
+        SALZ_LAUNCH_CHECK();
+    }
     // mod-0 list, then its stable sort by t[i]
     hipLaunchKernelGGL(k_dc3_mod0_flags, dim3(grid_for(ns, kT)), dim3(kT), 0, st, sar, ns, n1, flag);
     SALZ_LAUNCH_CHECK();

@@ -14,6 +14,7 @@
 // split into 512-byte wave tasks (64 lanes x 8 bytes), so a single 10^8-byte match is
 // spread over the whole chip instead of serialising one lane.
 #include "internal.hpp"
+#include "scatter.hpp"
 
 namespace salz {
 namespace {
@@ -37,6 +38,20 @@ __global__ void k_phi(const uint32_t *__restrict__ sa, Blocks bl, uint32_t *__re
     const uint32_t j = r ? sa[r - 1] : kNone;
     phi[i] = j != kNone && bl.blk(j) == bl.blk(i) ? j : kNone;
 }
+
+// The same pairs for the staged scatter (scatter.hpp): index SA[r], value Phi.
+struct PhiSrc {
+    const uint32_t *sa;
+    Blocks bl;
+    __device__ __forceinline__ bool operator()(size_t r, uint32_t &idx, uint32_t &val) const
+    {
+        const uint32_t i = sa[r], jr = sa[r ? r - 1 : 0];  // (unconditional loads)
+        const uint32_t j = r ? jr : kNone;
+        idx = i;
+        val = j != kNone && bl.blk(j) == bl.blk(i) ? j : kNone;
+        return i < bl.npos;
+    }
+};
 
 __global__ void k_plcp_short(const uint8_t *__restrict__ T, const uint32_t *__restrict__ phi,
                              Blocks bl, uint32_t *__restrict__ plv, uint32_t *__restrict__ queue,
@@ -163,8 +178,14 @@ int stage_lcp(Workspace &ws, const Blocks &bl, uint32_t *lcp_out)
 
     ws.stats.lcp_long_bytes = 0;
     uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
-    hipLaunchKernelGGL(k_phi, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.sa, bl, phi, derr);
-    SALZ_LAUNCH_CHECK();
+    if (scatter_stage_wanted((size_t)n * sizeof(uint32_t))) {  // (lsc and the radix counts are free here)
+        if (scatter_staged(PhiSrc{ws.sa, bl}, nsa, n, phi, 1u, 0u, reinterpret_cast<uint2 *>(ws.lsc),
+                           2 * ws.cap_s, ws.radix_counts, st) != 0)
+            return -1;
+    } else {
+        hipLaunchKernelGGL(k_phi, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.sa, bl, phi, derr);
+        SALZ_LAUNCH_CHECK();
+    }
     SALZ_HIP(hipMemsetAsync(cnt, 0, 8, st));
     hipLaunchKernelGGL(k_plcp_short, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, phi, bl, plv,
                        qa, cnt);

@@ -276,6 +276,25 @@ def test_dc3_matches_oracle(ctx, monkeypatch, keys, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
+@pytest.mark.parametrize("kind,n,seed,alpha", [("fib", 400_000, 0, 0), ("text", 300_001, 4, 0),
+                                               ("zeros", 70_000, 0, 0), ("smx", 200_000, 2, 4)])
+def test_staged_scatters(ctx, monkeypatch, kind, n, seed, alpha):
+    """The staged scatters (scatter.hpp: Phi of the PLCP stage, the DC3 levels' rank and name
+    arrays), forced on with SALZ_SCATTER_STAGE=1 (by default only past 256 MB), give the same
+    suffix array, LCPs and stream."""
+    monkeypatch.setenv("SALZ_SCATTER_STAGE", "1")
+    monkeypatch.setenv("SALZ_SA_ALGO", "dc3")
+    monkeypatch.setenv("SALZ_LCP_SA", "0")
+    src = _make(kind, n, seed, alpha)
+    out, d = ctx.encode_dump(src)
+    o = oracle_stages(src)
+    for k in ("sa", "lp", "ln"):
+        i = _first_diff(d[k], o[k])
+        assert i < 0, f"{k} differs at {i}"
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and out == ref
+
+
 def test_dc3_edge_sizes(ctx, monkeypatch):
     """DC3 at every suffix count 1..200 (each n mod 3, the dummy sample, one-level and
     recursing strings) and around powers of two."""
