@@ -130,7 +130,7 @@ def main():
     total = args.size or total
     sharded = block is not None
     child = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the CPU baseline is an N=1 figure
         first = min(block, total) if sharded else total
         sample = first if args.cpu_sample <= 0 else min(args.cpu_sample, first)
         child, _ = start_cpu_child(kind, total, 0, sample)
