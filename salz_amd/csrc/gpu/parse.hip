@@ -120,11 +120,12 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
     const uint4 *__restrict__ cand, const uint32_t *__restrict__ cin, uint64_t *__restrict__ pst,
     const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, Blocks bl, uint32_t klog,
     uint32_t *__restrict__ changed, uint32_t *err, uint8_t *__restrict__ eflag,
-    const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum)
+    const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum, uint32_t *__restrict__ reach)
 {
     const uint32_t c = blockIdx.x * kT + threadIdx.x;  // chunk
     const uint64_t a64 = (uint64_t)c << klog;
     uint32_t diff = 0, errw = 0;
+    uint32_t far_end = 0;  // farthest candidate target (first pass: k_parse_mark's range test)
     if (c == 0)
         eflag[sidx(n, klog)] = 1u;  // the root of the exit forest
     if (a64 < n) {
@@ -176,11 +177,17 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             win[k] = q <= n ? (((uint64_t)v << 32) | q) : 0;
         }
         uint32_t last_ex = 0xffffffffu;
+        far_end = b;
 #pragma unroll 8
         for (uint32_t j = K; j-- > 0;) {
             const uint32_t p = a + j;
             const bool live = p < b;
             const uint4 c0 = cr[0];
+            if (reach) {
+                const uint32_t tp = live && c0.y >= 3u ? p + c0.y : 0u, tn = live && c0.w >= 3u ? p + c0.w : 0u;
+                far_end = tp > far_end ? tp : far_end;
+                far_end = tn > far_end ? tn : far_end;
+            }
             uint32_t best = 9u + (uint32_t)(win[0] >> 32), ex = (uint32_t)win[0];
             uint8_t ch = 0;
             if (p != b0) {  // a block's first position is a literal (lib/salz.c:547-548)
@@ -266,6 +273,8 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             cr[kCDepth] = cand[slot(j >= kCDepth + 1 ? j - kCDepth - 1 : 0u)];
         }
     }
+    if (reach && a64 < n)
+        reach[c] = far_end;
     if (errw)
         atomicOr(err, errw);  // a candidate past the end (reported once per lane)
     // one atomic per wave
@@ -275,50 +284,36 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         atomicAdd(changed, diff);
 }
 
-// Farthest target of each chunk's candidates (at least its end b): the candidates do not change
-// between passes, so this is computed once per parse. One lane per chunk, row by row.
-__global__ __launch_bounds__(kT) void k_chunk_reach(const uint4 *__restrict__ cand, uint32_t n, Blocks bl,
-                                                    uint32_t klog, uint32_t *__restrict__ reach)
-{
-    const uint32_t c = blockIdx.x * kT + threadIdx.x;
-    const uint64_t a64 = (uint64_t)c << klog;
-    if (a64 >= n)
-        return;
-    const uint32_t a = (uint32_t)a64, K = 1u << klog;
-    const uint32_t e = bl.end(a);
-    const uint32_t b = (e - a) < K ? e : a + K;
-    const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
-    uint32_t r = b;
-    for (uint32_t j = 0; j < b - a; j++) {
-        const uint4 cd = cand[base + ((size_t)j << 6)];
-        const uint32_t p = a + j;
-        if (cd.y >= 3u && p + cd.y > r)
-            r = p + cd.y;
-        if (cd.w >= 3u && p + cd.w > r)
-            r = p + cd.w;
-    }
-    reach[c] = r;
-}
-
+constexpr uint32_t kRowsBrk = 8;
 // Breaks of the cost shift d[q] = cnew[q] - cold[q] (q >= 1 with d[q] != d[q - 1], or a cost at
-// or above 2^30), counted per chunk k over q in (kK, (k + 1)K]: one lane per chunk, row by row.
+// or above 2^30): flag[k] = 1 when chunk k holds one at some q in (kK, (k + 1)K] (flags cleared
+// beforehand). A thread takes 8 rows of one chunk, the 64 lanes of a wave 64 neighbouring chunks,
+// so every row is one contiguous run.
 __global__ __launch_bounds__(kT) void k_shift_breaks(const uint32_t *__restrict__ cnew,
                                                      const uint32_t *__restrict__ cold, uint32_t n,
-                                                     uint32_t klog, uint32_t nchunks, uint32_t *__restrict__ cnt)
+                                                     uint32_t klog, uint32_t nchunks, uint32_t *__restrict__ flag)
 {
-    const uint32_t c = blockIdx.x * kT + threadIdx.x;
+    const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
+    const uint32_t lane = (uint32_t)(x & 63u), groups = (1u << klog) / kRowsBrk;
+    const size_t rest = x >> 6;
+    const uint32_t c = (uint32_t)((rest / groups) * 64 + lane), g = (uint32_t)(rest % groups);
     if (c >= nchunks)
         return;
-    const uint32_t K = 1u << klog, a = c << klog;
-    const uint32_t last = a + K <= n ? a + K : n;  // q in (a, last]
-    uint32_t prev = cnew[sidx(a, klog)] - cold[sidx(a, klog)], k = 0;
-    for (uint32_t q = a + 1; q <= last; q++) {
+    const uint32_t q0 = (c << klog) + g * kRowsBrk;  // compares q in (q0, q0 + 8]
+    if (q0 >= n)
+        return;
+    uint32_t prev = cnew[sidx(q0, klog)] - cold[sidx(q0, klog)];
+    bool brk = false;
+#pragma unroll
+    for (uint32_t r = 1; r <= kRowsBrk; r++) {
+        const uint32_t q = q0 + r <= n ? q0 + r : n;  // (clamped: q = n repeats, no break)
         const size_t sq = sidx(q, klog);
         const uint32_t v = cnew[sq], d = v - cold[sq];
-        k += (d != prev) | (v >= (1u << 30));
+        brk |= d != prev || v >= (1u << 30);
         prev = d;
     }
-    cnt[c] = k;
+    if (brk)
+        flag[c] = 1u;
 }
 
 // Uniform-shift test, one chunk per lane, before every pass from the third on: every target
@@ -574,7 +569,6 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     const bool range_on = !getenv("SALZ_PARSE_RANGE") || atoi(getenv("SALZ_PARSE_RANGE")) != 0;
     uint32_t *reach = dsum + 2 * ((size_t)ps.nchunks + 64);
     uint32_t *brk = reach + ps.nchunks + 64, *pbrk = brk + ps.nchunks + 64;
-    bool reach_done = false;
     // Large blocks test for skipping only late in the iteration (SALZ_PARSE_EARLY=1: from the
     // third pass like smaller blocks; mixed 100 MB: 22.3 -> 23.7 ms, text 4.5 -> 5.0 ms)
     const bool early = getenv("SALZ_PARSE_EARLY") && atoi(getenv("SALZ_PARSE_EARLY")) != 0;
@@ -606,16 +600,11 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         if (skipping) {
             SALZ_HIP(hipMemsetAsync(ndirty, 0, 4, st));
             if (range_on) {
-                if (!reach_done) {
-                    hipLaunchKernelGGL(k_chunk_reach, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand, n,
-                                       bl, klog, reach);
-                    SALZ_LAUNCH_CHECK();
-                    reach_done = true;
-                }
-                hipLaunchKernelGGL(k_shift_breaks, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, cin, cout, n,
-                                   klog, ps.nchunks, brk);
+                SALZ_HIP(hipMemsetAsync(brk, 0, sizeof(uint32_t) * ((size_t)ps.nchunks + 1), st));
+                const size_t bthreads = (size_t)((ps.nchunks + 63) / 64) * 64 * (ps.chunk / kRowsBrk);
+                hipLaunchKernelGGL(k_shift_breaks, dim3(grid_for(bthreads, kT)), dim3(kT), 0, st, cin, cout, n, klog,
+                                   ps.nchunks, brk);
                 SALZ_LAUNCH_CHECK();
-                SALZ_HIP(hipMemsetAsync(brk + ps.nchunks, 0, sizeof(uint32_t), st));
                 if (scan_sum_u32(brk, pbrk, (size_t)ps.nchunks + 1, false, nullptr, ws, st) != 0)
                     return -1;
             }
@@ -642,7 +631,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         hipLaunchKernelGGL(k_parse_chunk, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
                            cin, ws.pst, chold, chnew, n, bl, klog, changed,
                            reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord, eflag,
-                           skipping && skip_on ? wdirty : nullptr, dsum);
+                           skipping && skip_on ? wdirty : nullptr, dsum, it == 0 && range_on ? reach : nullptr);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 256, "parse.changed") != 0)
             return -1;
