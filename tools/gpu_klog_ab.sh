@@ -3,5 +3,5 @@
 # (K = 512 from 32 MiB + 8) against K = 256 and 128.
 set -o pipefail
 export TMPDIR=/tmp
-R=2 ARGS="--kind mixed --size 67108864" bash tools/ab_env.sh "SALZ_PARSE_KLOG=7" "SALZ_PARSE_KLOG=8" "-" &&
-R=1 ARGS="--workload enwik9 --kind mixed --size 268435456 --steps 1" bash tools/ab_env.sh "SALZ_PARSE_KLOG=8" "-"
+R=2 ARGS="--kind mixed --size 67108864" bash tools/ab_env.sh "SALZ_PARSE_KLOG=7" "SALZ_PARSE_KLOG=8" "-"
+
