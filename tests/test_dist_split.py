@@ -35,7 +35,7 @@ def _inputs():
     }
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_split_suffix_array_matches_oracle(tmp_path, world):
     inputs = _inputs()
     src = tmp_path / "in.npz"
