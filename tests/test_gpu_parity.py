@@ -295,6 +295,22 @@ def test_staged_scatters(ctx, monkeypatch, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
+@pytest.mark.parametrize("kind,n", [("fib", 6_000_001), ("period3", 4_000_000), ("runs", 5_000_000),
+                                    ("smx4", 3_000_000)])
+def test_dc3_large_blocks_match_oracle(ctx, monkeypatch, kind, n):
+    """DC3 at a few MB (several levels with staged-size arrays, forced on for the random
+    4-letter text) against the CPU port's suffix array and stream."""
+    monkeypatch.setenv("SALZ_SA_ALGO", "dc3")
+    src = gen("smx", n, 9, 4) if kind == "smx4" else _make(kind, n, 0, 0)
+    out, d = ctx.encode_dump(src)
+    assert ctx.stats()["sa_dc3_levels"] > 0
+    o = oracle_stages(src)
+    i = _first_diff(d["sa"], o["sa"])
+    assert i < 0, f"sa differs at rank {i}"
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and out == ref
+
+
 def test_dc3_edge_sizes(ctx, monkeypatch):
     """DC3 at every suffix count 1..200 (each n mod 3, the dummy sample, one-level and
     recursing strings) and around powers of two."""
