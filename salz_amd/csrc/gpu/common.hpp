@@ -93,6 +93,16 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
     return v;
 }
 
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        uint32_t o = shfl_xor_u32(v, m);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
 // ---- device index checks ---------------------------------------------------------------
 // Kernels whose addresses come from data (suffix ranks, group tables) check them and, on a
 // violation, set a bit in this device word and skip the access instead of faulting; the
@@ -130,6 +140,14 @@ __host__ __device__ __forceinline__ uint64_t spos(size_t s, uint32_t klog)
 {
     const size_t t = s >> (klog + 6), j = (s >> 6) & ((1u << klog) - 1u), l = s & 63u;
     return (((uint64_t)t * 64u + l) << klog) | j;
+}
+
+// Index of slot s in a set kept as bits in slot order (ExitBits, internal.hpp): the set bits
+// before s, from the word prefix counts wpre and s's word.
+__device__ __forceinline__ uint32_t bits_index(const uint64_t *mask, const uint32_t *wpre, size_t s)
+{
+    const uint64_t m = mask[s >> 6];
+    return wpre[s >> 6] + (uint32_t)__popcll(m & ((1ull << (s & 63u)) - 1ull));
 }
 
 // ---- batch geometry: several independent blocks encoded by one pipeline pass -------------

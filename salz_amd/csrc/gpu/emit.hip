@@ -66,14 +66,14 @@ __device__ __forceinline__ uint64_t vn_bits(uint32_t v, uint32_t k)
 }
 
 // exit of every block's first position (the start of its path)
-__global__ void k_mark_start(const uint32_t *__restrict__ eidx, const uint64_t *__restrict__ pst,
-                             uint32_t klog, uint32_t *__restrict__ emark, Blocks bl)
+__global__ void k_mark_start(ExitBits eb, const uint64_t *__restrict__ pst, uint32_t klog,
+                             uint32_t *__restrict__ emark, Blocks bl)
 {
     const uint32_t b = blockIdx.x * kT + threadIdx.x;
     if (b >= bl.nb)
         return;
     const uint32_t p0 = b * (bl.nb == 1 ? 0u : bl.bs);
-    emark[eidx[sidx((uint32_t)pst[sidx(p0, klog)], klog)]] = 1u;
+    emark[bits_index(eb.mask, eb.wpre, sidx((uint32_t)pst[sidx(p0, klog)], klog))] = 1u;
 }
 
 __global__ void k_mark_step(const uint32_t *__restrict__ jt, uint32_t *emark, uint32_t ne)
@@ -416,7 +416,7 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
         set_error("emit: %u blocks exceed the batch limit %u", nb, kMaxBatchBlocks);
         return -1;
     }
-    uint32_t *emark = ws.offA, *eidx = ws.offB, *entry = ws.sa;
+    uint32_t *emark = ws.offA, *entry = ws.sa;
     uint64_t *cbits = ws.g64, *cbytes = ws.g64 + (nch + 2);
     uint64_t *W = ws.keyA;
     uint32_t *Yk = ws.u2;
@@ -428,7 +428,7 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
     SALZ_HIP(hipMemsetAsync(entry, 0xff, sizeof(uint32_t) * ((size_t)nch + 1), st));
     if (ne) {
         SALZ_HIP(hipMemsetAsync(emark, 0, sizeof(uint32_t) * ne, st));
-        hipLaunchKernelGGL(k_mark_start, dim3(grid_for(nb, kT)), dim3(kT), 0, st, eidx, ps.pst, ws.klog,
+        hipLaunchKernelGGL(k_mark_start, dim3(grid_for(nb, kT)), dim3(kT), 0, st, ps.ebits, ps.pst, ws.klog,
                            emark, bl);
         SALZ_LAUNCH_CHECK();
         const uint32_t *lev = ps.jt0;  // parents 2^k steps up (level k)

@@ -29,7 +29,16 @@ struct StageStats {
 
 // Parse/emit scratch carving (parse.hip owns the layout, emit.hip reads it). Per-position
 // arrays are in the chunk-interleaved layout (common.hpp, sidx with Workspace::klog).
+// The parse's exit set E as bits in storage-slot order: one word per 64 slots, its popcount, and
+// the exclusive scan of those (a slot's index in E = wpre + the set bits below it in its word).
+struct ExitBits {
+    uint64_t *mask;
+    uint32_t *wcnt;
+    uint32_t *wpre;
+};
+
 struct ParseState {
+    ExitBits ebits;         // exit set of the last pass (read by emission's path marking)
     uint32_t chunk;         // positions per parse lane (1 << klog)
     uint32_t nchunks;
     uint8_t *choice;        // final decisions: 0 literal, 1 PSV, 2 NSV

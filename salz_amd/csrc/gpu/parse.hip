@@ -410,31 +410,58 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
         dsum[c] += d0;
 }
 
-// Exit flags (marked by the chunk pass) and the compacted exit index live in storage (slot)
-// order like the other parse arrays.
-
-// Compact E: node x = eidx[slot of q] for exit position q; parent = exit of q, weight =
-// in-chunk bit sum of q's path (estimate + dsum of q's chunk - cin[exit]).
-__global__ void k_compact_exits(const uint8_t *__restrict__ eflag,
-                                const uint32_t *__restrict__ eidx, const uint64_t *__restrict__ pst,
-                                const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog, size_t S,
-                                uint32_t *__restrict__ elist, uint32_t *__restrict__ jt0,
-                                uint32_t *__restrict__ js, const uint32_t *__restrict__ dsum)
+// Exit flags (bytes marked by the chunk pass, storage-slot order) -> ExitBits: the set as one
+// bit per slot, 64 slots a word (one row of a 64-chunk tile), and per-word popcounts for the
+// scan that numbers E. A thread packs 8 flag bytes, 8 lanes one word.
+__global__ __launch_bounds__(kT) void k_exit_pack(const uint64_t *__restrict__ eflag8, size_t S8, ExitBits eb)
 {
-    size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (s >= S || !eflag[s])
+    const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;  // slots [8x, 8x + 8)
+    uint64_t v = eflag8[x < S8 ? x : 0];  // (unconditional load, clamped)
+    v |= v >> 4;
+    v |= v >> 2;
+    v |= v >> 1;
+    v &= 0x0101010101010101ull;                                       // byte k's flag at bit 8k
+    const uint64_t m8 = (v * 0x0102040810204080ull) >> 56;            // ... moved to bit k
+    uint64_t w = m8 << (8u * (uint32_t)(x & 7u));
+    w |= ((uint64_t)shfl_xor_u32((uint32_t)(w >> 32), 1) << 32) | shfl_xor_u32((uint32_t)w, 1);
+    w |= ((uint64_t)shfl_xor_u32((uint32_t)(w >> 32), 2) << 32) | shfl_xor_u32((uint32_t)w, 2);
+    w |= ((uint64_t)shfl_xor_u32((uint32_t)(w >> 32), 4) << 32) | shfl_xor_u32((uint32_t)w, 4);
+    if ((x & 7u) == 0 && x < S8) {  // S8 is a multiple of 8 (slots come in 64-chunk tiles)
+        eb.mask[x >> 3] = w;
+        eb.wcnt[x >> 3] = (uint32_t)__popcll(w);
+    }
+}
+
+// Compact E: node xi = index of exit position q in E; parent = exit of q, weight = in-chunk bit
+// sum of q's path (estimate + dsum of q's chunk - cin[exit]). A thread takes 8 slots (one byte
+// of an ExitBits word) and numbers their exits in slot order.
+__global__ __launch_bounds__(kT) void k_compact_exits(ExitBits eb, const uint64_t *__restrict__ pst,
+                                                      const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog,
+                                                      size_t S8, uint32_t *__restrict__ elist,
+                                                      uint32_t *__restrict__ jt0, uint32_t *__restrict__ js,
+                                                      const uint32_t *__restrict__ dsum)
+{
+    const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (x >= S8)
         return;
-    const uint32_t q = (uint32_t)spos(s, klog);
-    uint32_t x = eidx[s];
-    elist[x] = q;
-    if (q == n) {
-        jt0[x] = x;
-        js[x] = 0;
-    } else {
+    const uint64_t word = eb.mask[x >> 3];
+    const uint32_t sh = 8u * (uint32_t)(x & 7u);
+    uint32_t bits = (uint32_t)(word >> sh) & 0xffu;
+    uint32_t xi = eb.wpre[x >> 3] + (uint32_t)__popcll(word & ((1ull << sh) - 1ull));
+    while (bits) {
+        const size_t s = 8 * x + (uint32_t)__builtin_ctz(bits);
+        bits &= bits - 1u;
+        const uint32_t q = (uint32_t)spos(s, klog);
+        // every load unconditional (the root's reads use its own slot, results unused)
         const uint64_t v = pst[s];
-        const size_t se = sidx((uint32_t)v, klog);
-        jt0[x] = eidx[se];
-        js[x] = (uint32_t)(v >> 32) + dsum[q >> klog] - cin[se];
+        const uint32_t ev = q == n ? n : (uint32_t)v;
+        const size_t se = sidx(ev, klog);
+        const uint32_t parent = bits_index(eb.mask, eb.wpre, se);
+        const uint32_t w = (uint32_t)(v >> 32) + dsum[(q < n ? q : 0u) >> klog] - cin[se];
+        elist[xi] = q;
+        jt0[xi] = q == n ? xi : parent;
+        js[xi] = q == n ? 0u : w;
+        xi++;
     }
 }
 
@@ -468,11 +495,9 @@ __global__ void k_jump2(const uint32_t *__restrict__ jt, const uint32_t *__restr
 // index in E), any other position adds its in-chunk bit sum to its exit's. A thread takes
 // kRows consecutive positions of one chunk (the 64 lanes of a wave: 64 neighbouring chunks, so
 // every row is one contiguous run); consecutive positions mostly share their exit, whose cost
-// (cin, eidx, js: a dependent pair of gathers) is then loaded once.
+// (cin and js through its index in E: dependent gathers) is then loaded once.
 constexpr uint32_t kRows = 8;
-__global__ __launch_bounds__(kT) void k_cost_rest(const uint8_t *__restrict__ eflag,
-                                                  const uint32_t *__restrict__ eidx,
-                                                  const uint32_t *__restrict__ js,
+__global__ __launch_bounds__(kT) void k_cost_rest(ExitBits eb, const uint32_t *__restrict__ js,
                                                   const uint64_t *__restrict__ pst,
                                                   const uint32_t *__restrict__ cin, uint32_t n,
                                                   uint32_t klog, size_t S, uint32_t *cost,
@@ -494,14 +519,14 @@ __global__ __launch_bounds__(kT) void k_cost_rest(const uint8_t *__restrict__ ef
         const uint64_t p = spos(s, klog);
         if (p > n)
             break;
-        if (eflag[s]) {
-            cost[s] = js[eidx[s]];
+        if ((eb.mask[s >> 6] >> lane) & 1u) {  // (the wave's 64 slots: one word)
+            cost[s] = js[bits_index(eb.mask, eb.wpre, s)];
             continue;
         }
         const uint64_t v = pst[s];
         const uint32_t se = (uint32_t)sidx((uint32_t)v, klog);
         if (se != last_se) {
-            base_cost = js[eidx[se]] - cin[se];
+            base_cost = js[bits_index(eb.mask, eb.wpre, se)] - cin[se];
             last_se = se;
         }
         cost[s] = (uint32_t)(v >> 32) + shift + base_cost;
@@ -547,7 +572,11 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     uint32_t *cost[2] = {ws.u0, ws.u1};
     uint8_t *choice[2] = {reinterpret_cast<uint8_t *>(ws.valA), reinterpret_cast<uint8_t *>(ws.valB)};
     uint8_t *eflag = reinterpret_cast<uint8_t *>(ws.offA);  // exit flags, one byte per slot
-    uint32_t *eidx = ws.offB;
+    // the same set as bits + word prefix counts (S / 4 bytes in offB; emission reads them)
+    ExitBits eb{reinterpret_cast<uint64_t *>(ws.offB), nullptr, nullptr};
+    eb.wcnt = reinterpret_cast<uint32_t *>(eb.mask + S / 64);
+    eb.wpre = eb.wcnt + S / 64;
+    ps.ebits = eb;
     uint32_t *elist = ws.rank;
     uint32_t *js[2] = {reinterpret_cast<uint32_t *>(ws.keyA),
                        reinterpret_cast<uint32_t *>(ws.keyA) + (ws.cap_n + 1)};
@@ -655,7 +684,10 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             return -1;
         }
         // Exact costs for the new decisions (E was marked by the chunk pass).
-        if (scan_sum_u8(eflag, eidx, S, false, etotal, ws, st) != 0)
+        hipLaunchKernelGGL(k_exit_pack, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st,
+                           reinterpret_cast<const uint64_t *>(eflag), S / 8, eb);
+        SALZ_LAUNCH_CHECK();
+        if (scan_sum_u32(eb.wcnt, eb.wpre, S / 64, false, etotal, ws, st) != 0)
             return -1;
         if (read_scalars(ws, 0, 256, "parse.ne") != 0)
             return -1;
@@ -669,8 +701,8 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             set_error("parse: exit set larger than the text (|E|=%u)", ne);
             return -1;
         }
-        hipLaunchKernelGGL(k_compact_exits, dim3(grid_for(S, kT)), dim3(kT), 0, st, eflag, eidx,
-                           ws.pst, cin, n, klog, S, elist, snap, js[0], dsum);
+        hipLaunchKernelGGL(k_compact_exits, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st, eb, ws.pst, cin, n, klog,
+                           S / 8, elist, snap, js[0], dsum);
         SALZ_LAUNCH_CHECK();
         int jc = 0;
         if (snaps) {
@@ -693,8 +725,8 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                 jc ^= 1;
             }
         }
-        hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(S / kRows, kT)), dim3(kT), 0, st, eflag, eidx, js[jc],
-                           ws.pst, cin, n, klog, S, cout, dsum);
+        hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(S / kRows, kT)), dim3(kT), 0, st, eb, js[jc], ws.pst, cin,
+                           n, klog, S, cout, dsum);
         SALZ_LAUNCH_CHECK();
         ps.n_exit = ne;
         ps.levels = K;

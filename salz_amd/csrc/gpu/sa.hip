@@ -627,12 +627,14 @@ __device__ __forceinline__ void seg_lsd(uint64_t *sk, uint32_t (*cnt)[256], uint
 // rank << 12 | slot; a stable 8-bit LSD pass per digit of the (group, rank) part.
 __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict__ K,
                                                            uint32_t *__restrict__ V, SegPlan plan,
-                                                           uint32_t m, int kb, uint32_t *err)
+                                                           const uint64_t *__restrict__ ginfo, uint32_t m,
+                                                           int kb, uint32_t tiny, uint32_t *err)
 {
     __shared__ uint64_t sk[kSegCap];  // keys; at the end the window's values (as u32)
     __shared__ uint32_t cnt[4][256];
     __shared__ uint32_t dstart[256];
     __shared__ uint32_t wsum[4];
+    __shared__ uint32_t smax;
 
     const unsigned tid = threadIdx.x;
     const uint32_t w = blockIdx.x;
@@ -646,16 +648,60 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
     const uint64_t mask = (1ull << kb) - 1ull;
     const uint32_t glast = (uint32_t)(K[hi - 1] >> kb);
     const int nbits = kb + (32 - __builtin_clz((glast - g0) | 1u));
+    if (tid == 0)
+        smax = 0;
 
     // slots actually sorted: count rounded up to 1024 (4 waves x 64 lanes x ITEMS / 4 steps)
     const int items = (int)((count + 1023u) / 1024u) * 4;
+    uint32_t gmax = 0;  // largest group among this thread's entries
     for (uint32_t i = tid; i < (uint32_t)items * kSegThreads; i += kSegThreads) {
         uint64_t key = ~0ull;  // padding sorts last in every digit
         if (i < count) {
             const uint64_t kk = K[lo + i];
             key = (((kk >> kb) - g0) << (kb + 12)) | ((kk & mask) << 12) | i;
+            if (tiny) {
+                const uint32_t s = (uint32_t)(ginfo[kk >> kb] >> 32);
+                gmax = s > gmax ? s : gmax;
+            }
         }
         sk[i] = key;
+    }
+    if (tiny) {
+        // Windows of tiny groups only: each entry's place is its group's start plus the members
+        // with smaller (rank, slot), counted in LDS (at most `tiny` reads per entry instead of
+        // nbits / 8 LSD passes). Same order as the stable LSD passes.
+        gmax = wave_max_u32(gmax);
+        __syncthreads();  // smax initialised
+        if (lane_id() == 0)
+            atomicMax(&smax, gmax);
+        __syncthreads();
+        if (smax <= tiny) {
+            constexpr uint32_t kPer = kSegCap / kSegThreads;
+            uint32_t dst[kPer], vv[kPer];
+            uint64_t nk[kPer];
+#pragma unroll
+            for (uint32_t j = 0; j < kPer; j++) {
+                const uint32_t i = tid + j * kSegThreads, ii = i < count ? i : 0u;
+                const uint64_t ki = sk[ii];
+                const uint64_t g = g0 + (ki >> (kb + 12));
+                const uint64_t gi = ginfo[g];  // unconditional loads (clamped entry)
+                vv[j] = V[lo + ii];
+                const uint32_t gs = (uint32_t)gi - lo, s = (uint32_t)(gi >> 32);
+                uint32_t r = 0;
+                for (uint32_t x = gs; x < gs + s; x++)
+                    r += sk[x] < ki ? 1u : 0u;
+                dst[j] = i < count ? lo + gs + r : 0xffffffffu;
+                nk[j] = (g << kb) | ((ki >> 12) & mask);
+            }
+            __syncthreads();  // every value read before any is overwritten
+#pragma unroll
+            for (uint32_t j = 0; j < kPer; j++)
+                if (dst[j] != 0xffffffffu) {
+                    K[dst[j]] = nk[j];
+                    V[dst[j]] = vv[j];
+                }
+            return;
+        }
     }
     switch (items) {
     case 4: seg_lsd<4>(sk, cnt, dstart, wsum, nbits); break;
@@ -965,6 +1011,9 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     const int kb = bit_width(n);
     static const bool verbose = getenv("SALZ_DEBUG_SA") != nullptr;
     const char *mode_env = getenv("SALZ_SA_MODE");  // tests: "global" or "segmented"
+    // k_seg_small windows whose groups all have at most seg_tiny members are ordered by counting
+    // (SALZ_SEG_TINY=0: LSD passes everywhere)
+    const uint32_t seg_tiny = getenv("SALZ_SEG_TINY") ? (uint32_t)atoi(getenv("SALZ_SEG_TINY")) : 32u;
     auto t_round = std::chrono::steady_clock::now();
     for (;;) {
         ws.stats.sa_rounds++;
@@ -1007,8 +1056,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                 hipLaunchKernelGGL(k_seg_plan, dim3(grid_for(G_act, kT)), dim3(kT), 0, st, tab.ginfo,
                                    G_act, plan);
                 SALZ_LAUNCH_CHECK();
-                hipLaunchKernelGGL(k_seg_small, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, m, kb,
-                                   derr);
+                hipLaunchKernelGGL(k_seg_small, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, tab.ginfo, m,
+                                   kb, seg_tiny, derr);
                 SALZ_LAUNCH_CHECK();
                 if (mL) {
                     hipLaunchKernelGGL(k_extract, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V,

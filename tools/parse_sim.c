@@ -70,31 +70,56 @@ int parse_sim(const int32_t *psv, const int32_t *lp, const int32_t *nsv, const i
     for (int32_t q = 0; q <= n; q++)
         cin[q] = seed_mode == 0 ? 9u * (uint32_t)(n - q) : (seed_mode == 1 ? 0u : 3u * (uint32_t)(n - q));
     memset(chold, 0xff, n);
+    /* PARSE_SIM_OVL=V, PARSE_SIM_OVL_IT=t: the first t passes walk V positions past each chunk's
+       end first (their states used only by that chunk, targets past them read cin) */
+    const int32_t ovl = getenv("PARSE_SIM_OVL") ? atoi(getenv("PARSE_SIM_OVL")) : 0;
+    const int ovl_it = getenv("PARSE_SIM_OVL_IT") ? atoi(getenv("PARSE_SIM_OVL_IT")) : 1;
+    uint32_t *oc = malloc(4ull * (ovl + 1)), *oe = malloc(4ull * (ovl + 1)), *os = malloc(4ull * (ovl + 1));
     int it;
     int64_t exits = 0;
     for (it = 0; it < 100000; it++) {
         long changed = 0;
+        const int32_t V = it < ovl_it ? ovl : 0;
         for (int32_t a = 0; a < n; a += chunk) {
             int32_t b = a + chunk < n ? a + chunk : n;
+            const int32_t bv = b + V < n ? b + V : n;
+            /* target q >= b: overlap state (cost, exit, sum) or cin */
+#define TC(q) ((q) < (uint32_t)bv ? oc[(q) - b] : cin[q])
+            for (int32_t p = bv - 1; p >= b; p--) {
+                uint32_t best = 9u + TC((uint32_t)p + 1), len = 1, w = 9;
+                if (lp[p] >= 3) {
+                    uint32_t q = p + lp[p], wf = fbits(p - psv[p], lp[p]), alt = wf + TC(q);
+                    if ((int32_t)alt < (int32_t)best) { best = alt; len = lp[p]; w = wf; }
+                }
+                if (ln[p] >= 3) {
+                    uint32_t q = p + ln[p], wf = fbits(p - nsv[p], ln[p]), alt = wf + TC(q);
+                    if ((int32_t)alt < (int32_t)best) { best = alt; len = ln[p]; w = wf; }
+                }
+                uint32_t nx = p + len;
+                oc[p - b] = best;
+                if (nx >= (uint32_t)bv) { oe[p - b] = nx; os[p - b] = w; }
+                else { oe[p - b] = oe[nx - b]; os[p - b] = w + os[nx - b]; }
+            }
             for (int32_t p = b - 1; p >= a; p--) {
                 uint32_t nx1 = p + 1;
-                uint32_t best = 9u + (nx1 >= (uint32_t)b ? cin[nx1] : cout[nx1]);
+                uint32_t best = 9u + (nx1 >= (uint32_t)b ? TC(nx1) : cout[nx1]);
                 uint32_t len = 1, w = 9;
                 uint8_t ch = 0;
                 if (p) {
                     if (lp[p] >= 3) {
                         uint32_t q = p + lp[p], wf = fbits(p - psv[p], lp[p]);
-                        uint32_t alt = wf + (q >= (uint32_t)b ? cin[q] : cout[q]);
+                        uint32_t alt = wf + (q >= (uint32_t)b ? TC(q) : cout[q]);
                         if ((int32_t)alt < (int32_t)best) { best = alt; len = lp[p]; w = wf; ch = 1; }
                     }
                     if (ln[p] >= 3) {
                         uint32_t q = p + ln[p], wf = fbits(p - nsv[p], ln[p]);
-                        uint32_t alt = wf + (q >= (uint32_t)b ? cin[q] : cout[q]);
+                        uint32_t alt = wf + (q >= (uint32_t)b ? TC(q) : cout[q]);
                         if ((int32_t)alt < (int32_t)best) { best = alt; len = ln[p]; w = wf; ch = 2; }
                     }
                 }
                 uint32_t nx = p + len;
-                if (nx >= (uint32_t)b) { ex[p] = nx; sm[p] = w; }
+                if (nx >= (uint32_t)bv) { ex[p] = nx; sm[p] = w; }
+                else if (nx >= (uint32_t)b) { ex[p] = oe[nx - b]; sm[p] = w + os[nx - b]; }
                 else { ex[p] = ex[nx]; sm[p] = w + sm[nx]; }
                 cout[p] = best;
                 changed += ch != chold[p];
@@ -106,7 +131,7 @@ int parse_sim(const int32_t *psv, const int32_t *lp, const int32_t *nsv, const i
             /* changed positions: how many, and the span of chunks they fall in */
             fprintf(stderr, "it %d changed %ld\n", it, changed);
         }
-        if (!changed)
+        if (!changed && it > ovl_it - 1 + (ovl ? 1 : 0))
             break;
         /* exact costs of the new decisions */
         memset(flag, 0, n + 1);
@@ -150,6 +175,6 @@ int parse_sim(const int32_t *psv, const int32_t *lp, const int32_t *nsv, const i
         if (chold[p] != refch[p]) { ok = 0; break; }
     *iters_out = it + 1;
     *exits_out = exits;
-    free(cin); free(cout); free(ex); free(sm); free(ref); free(chold); free(chnew); free(flag); free(refch);
+    free(oc); free(oe); free(os); free(cin); free(cout); free(ex); free(sm); free(ref); free(chold); free(chnew); free(flag); free(refch);
     return ok;
 }
