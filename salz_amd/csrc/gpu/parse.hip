@@ -53,6 +53,34 @@ __device__ __forceinline__ uint32_t factor_bits(uint32_t off, uint32_t len)
     return 1u + 8u + 4u * vn_size((off - 1u) >> 8) + ((len - 3u) >> 3) + 4u;
 }
 
+// Candidates as the parse reads them: the full {p - PSV, lenP, p - NSV, lenN} (uint4), or packed
+// per side as len | (vnibble size of the offset's high part) << 28 (uint2, half the bytes), for
+// blocks under 2^28 positions. The first pass reads the full form and writes the packed one, which
+// every later pass and skip test reads.
+constexpr uint32_t kPackLen = (1u << 28) - 1u;
+struct CandFull {
+    using T = uint4;
+    static __device__ __forceinline__ uint32_t lp(T c) { return c.y; }
+    static __device__ __forceinline__ uint32_t ln(T c) { return c.w; }
+    static __device__ __forceinline__ uint32_t bp(T c) { return factor_bits(c.x, c.y); }
+    static __device__ __forceinline__ uint32_t bn(T c) { return factor_bits(c.z, c.w); }
+};
+struct CandPacked {
+    using T = uint2;
+    static __device__ __forceinline__ uint32_t lp(T c) { return c.x & kPackLen; }
+    static __device__ __forceinline__ uint32_t ln(T c) { return c.y & kPackLen; }
+    // factor_bits: 13 + 4 vn_size((off - 1) >> 8) + ((len - 3) >> 3)
+    static __device__ __forceinline__ uint32_t bp(T c) { return 13u + 4u * (c.x >> 28) + (((c.x & kPackLen) - 3u) >> 3); }
+    static __device__ __forceinline__ uint32_t bn(T c) { return 13u + 4u * (c.y >> 28) + (((c.y & kPackLen) - 3u) >> 3); }
+};
+__device__ __forceinline__ uint2 pack_cand(uint4 c)
+{
+    const uint32_t x = c.y >= 3u ? (c.y & kPackLen) | vn_size((c.x - 1u) >> 8) << 28 : c.y & kPackLen;
+    const uint32_t y = c.w >= 3u ? (c.w & kPackLen) | vn_size((c.z - 1u) >> 8) << 28 : c.w & kPackLen;
+    return make_uint2(x, y);
+}
+__device__ __forceinline__ uint2 pack_cand(uint2 c) { return c; }  // (packed passes write none)
+
 // Storage slots 0..S-1 -> cost seed 3 * (n - p); slots past n unused. Any seed gives the
 // same fixed point (the final pass confirms every decision against exact costs); one near
 // the typical optimum (~3 bits per byte) needs fewer passes on mixed data (tools/parse_sim.c).
@@ -94,7 +122,7 @@ __device__ __forceinline__ uint64_t far_load(const uint64_t *pst, const uint32_t
                                              uint32_t a, uint32_t b, uint32_t klog, uint32_t p,
                                              uint32_t len, uint32_t n, uint32_t &lq, uint32_t &same)
 {
-    const bool far = len > kWin && len <= n - p;
+    const bool far = len > kWin && p < n && len <= n - p;  // (inert steps past n: never far)
     same = far && p + len == lq ? 1u : 0u;
     lq = far ? p + len : 0xffffffffu;
     const uint32_t q = far && !same ? p + len : a;
@@ -116,8 +144,10 @@ __device__ __forceinline__ uint64_t far_decode(uint64_t raw, uint32_t q, uint32_
 // wdirty (from the third pass on): one flag per wave of 64 chunks; a clean wave's chunks
 // would repeat their decisions (k_parse_mark), so they only carry their choices over, and
 // their states stay valid through dsum (the uniform cost shift added since their last pass).
+template <class C>
 __global__ __launch_bounds__(kT) void k_parse_chunk(
-    const uint4 *__restrict__ cand, const uint32_t *__restrict__ cin, uint64_t *__restrict__ pst,
+    const typename C::T *__restrict__ cand, uint2 *__restrict__ pack_out, const uint32_t *__restrict__ cin,
+    uint64_t *__restrict__ pst,
     const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, Blocks bl, uint32_t klog,
     uint32_t *__restrict__ changed, uint32_t *err, uint8_t *__restrict__ eflag,
     const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum, uint32_t *__restrict__ reach)
@@ -150,7 +180,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         // counter, no EXEC change inside the loop) and the loop is unrolled by the rings'
         // length. Positions past n lie inside the layout's last tile; their slots are never read.
         // Rings, index k = position p - k for the current p.
-        uint4 cr[kCDepth + 1];
+        typename C::T cr[kCDepth + 1];
         uint8_t orr[kDepth];
         uint64_t fP[kDepth], fN[kDepth];
         uint64_t win[kWin];  // win[k] = state of p + 1 + k
@@ -165,8 +195,8 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         for (uint32_t k = 0; k < kDepth; k++) {
             orr[k] = chold[slot(K - 1 - k)];
             uint32_t sp, sn;
-            fP[k] = far_load(pst, cin, base, a, b, klog, pK - k, cr[k].y, n, lqP, sp);
-            fN[k] = far_load(pst, cin, base, a, b, klog, pK - k, cr[k].w, n, lqN, sn);
+            fP[k] = far_load(pst, cin, base, a, b, klog, pK - k, C::lp(cr[k]), n, lqP, sp);
+            fN[k] = far_load(pst, cin, base, a, b, klog, pK - k, C::ln(cr[k]), n, lqN, sn);
             sameP |= sp << k;
             sameN |= sn << k;
         }
@@ -182,47 +212,50 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         for (uint32_t j = K; j-- > 0;) {
             const uint32_t p = a + j;
             const bool live = p < b;
-            const uint4 c0 = cr[0];
+            const typename C::T c0 = cr[0];
+            const uint32_t lenP = C::lp(c0), lenN = C::ln(c0);
+            if (pack_out)  // (kernel-uniform) the first pass leaves the packed candidates
+                pack_out[slot(j)] = pack_cand(cr[0]);
             if (reach) {
-                const uint32_t tp = live && c0.y >= 3u ? p + c0.y : 0u, tn = live && c0.w >= 3u ? p + c0.w : 0u;
+                const uint32_t tp = live && lenP >= 3u ? p + lenP : 0u, tn = live && lenN >= 3u ? p + lenN : 0u;
                 far_end = tp > far_end ? tp : far_end;
                 far_end = tn > far_end ? tn : far_end;
             }
             uint32_t best = 9u + (uint32_t)(win[0] >> 32), ex = (uint32_t)win[0];
             uint8_t ch = 0;
             if (p != b0) {  // a block's first position is a literal (lib/salz.c:547-548)
-                if (c0.y >= 3u) {
-                    errw |= live && c0.y > e - p ? kErrParse : 0u;
+                if (lenP >= 3u) {
+                    errw |= live && lenP > e - p ? kErrParse : 0u;
                     uint64_t t;
-                    if (c0.y <= kWin) {
+                    if (lenP <= kWin) {
                         t = win[1];
 #pragma unroll
                         for (uint32_t k = 2; k < kWin; k++)
-                            t = c0.y == k + 1 ? win[k] : t;
+                            t = lenP == k + 1 ? win[k] : t;
                     } else {
-                        t = (sameP & 1u) ? prevP : far_decode(fP[0], p + c0.y, b, klog);
+                        t = (sameP & 1u) ? prevP : far_decode(fP[0], p + lenP, b, klog);
                         prevP = t;
                     }
-                    const uint32_t alt = factor_bits(c0.x, c0.y) + (uint32_t)(t >> 32);
+                    const uint32_t alt = C::bp(c0) + (uint32_t)(t >> 32);
                     if ((int32_t)alt < (int32_t)best) {
                         best = alt;
                         ex = (uint32_t)t;
                         ch = 1;
                     }
                 }
-                if (c0.w >= 3u) {
-                    errw |= live && c0.w > e - p ? kErrParse : 0u;
+                if (lenN >= 3u) {
+                    errw |= live && lenN > e - p ? kErrParse : 0u;
                     uint64_t t;
-                    if (c0.w <= kWin) {
+                    if (lenN <= kWin) {
                         t = win[1];
 #pragma unroll
                         for (uint32_t k = 2; k < kWin; k++)
-                            t = c0.w == k + 1 ? win[k] : t;
+                            t = lenN == k + 1 ? win[k] : t;
                     } else {
-                        t = (sameN & 1u) ? prevN : far_decode(fN[0], p + c0.w, b, klog);
+                        t = (sameN & 1u) ? prevN : far_decode(fN[0], p + lenN, b, klog);
                         prevN = t;
                     }
-                    const uint32_t alt = factor_bits(c0.z, c0.w) + (uint32_t)(t >> 32);
+                    const uint32_t alt = C::bn(c0) + (uint32_t)(t >> 32);
                     if ((int32_t)alt < (int32_t)best) {
                         best = alt;
                         ex = (uint32_t)t;
@@ -263,11 +296,11 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             // targets (its candidate, cr[kDepth - 1], was loaded four steps ago), and position
             // p - 1 - kCDepth's candidate
             const uint32_t jd = j >= kDepth ? j - kDepth : 0u;
-            const uint4 cd = cr[kDepth - 1];
+            const typename C::T cd = cr[kDepth - 1];
             orr[kDepth - 1] = chold[slot(jd)];
             uint32_t sp, sn;
-            fP[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, cd.y, n, lqP, sp);
-            fN[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, cd.w, n, lqN, sn);
+            fP[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, C::lp(cd), n, lqP, sp);
+            fN[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, C::ln(cd), n, lqN, sn);
             sameP = (sameP >> 1) | (sp << (kDepth - 1));
             sameN = (sameN >> 1) | (sn << (kDepth - 1));
             cr[kCDepth] = cand[slot(j >= kCDepth + 1 ? j - kCDepth - 1 : 0u)];
@@ -326,7 +359,8 @@ __global__ __launch_bounds__(kT) void k_shift_breaks(const uint32_t *__restrict_
 // dirty waves; none left means the fixed point.
 // A chunk whose targets [b, reach] hold no break of the shift (prefix counts pbrk over chunks)
 // passes without looking at its candidates; only the others run the per-candidate test.
-__global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ cand,
+template <class C>
+__global__ __launch_bounds__(kT) void k_parse_mark(const typename C::T *__restrict__ cand,
                                                    const uint32_t *__restrict__ cnew,
                                                    const uint32_t *__restrict__ cold, uint32_t n,
                                                    Blocks bl,
@@ -365,7 +399,8 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
         // of 8: a batch's candidates are loaded while the previous batch's costs are checked
         // (two register sets, so no in-flight register is moved), and the loop count is
         // wave-uniform.
-        auto load = [&](uint4(&cd)[8], uint32_t j0) {
+        using CT = typename C::T;
+        auto load = [&](CT(&cd)[8], uint32_t j0) {
 #pragma unroll
             for (uint32_t u = 0; u < 8; u++) {
                 const uint32_t j = j0 + u < jn ? j0 + u : (jn ? jn - 1u : 0u);
@@ -375,23 +410,24 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const uint4 *__restrict__ can
         // a target equal to the previous row's (one match's end) was checked already: such a row
         // reads b's costs instead (which pass by definition)
         uint32_t lqp = 0xffffffffu, lqn = 0xffffffffu;
-        auto check = [&](const uint4(&cd)[8], uint32_t j0) {
+        auto check = [&](const CT(&cd)[8], uint32_t j0) {
 #pragma unroll
             for (uint32_t u = 0; u < 8; u++) {
                 const uint32_t p = a + j0 + u;
                 const bool on = j0 + u < jn && p != b0;
-                const uint32_t qp = p + cd[u].y, qn = p + cd[u].w;
-                const bool xp = on && cd[u].y >= 3u && qp >= b && qp != lqp;
-                const bool xn = on && cd[u].w >= 3u && qn >= b && qn != lqn;
-                lqp = on && cd[u].y >= 3u ? qp : 0xffffffffu;
-                lqn = on && cd[u].w >= 3u ? qn : 0xffffffffu;
+                const uint32_t lp = C::lp(cd[u]), ln = C::ln(cd[u]);
+                const uint32_t qp = p + lp, qn = p + ln;
+                const bool xp = on && lp >= 3u && qp >= b && qp != lqp;
+                const bool xn = on && ln >= 3u && qn >= b && qn != lqn;
+                lqp = on && lp >= 3u ? qp : 0xffffffffu;
+                lqn = on && ln >= 3u ? qn : 0xffffffffu;
                 const size_t sp = sidx(xp ? qp : b, klog), sn = sidx(xn ? qn : b, klog);
                 const uint32_t vp = cnew[sp], vn = cnew[sn];
                 bad |= vp - cold[sp] != d0 || vp >= (1u << 30);
                 bad |= vn - cold[sn] != d0 || vn >= (1u << 30);
             }
         };
-        uint4 A[8], B[8];
+        CT A[8], B[8];
         load(A, 0);
         for (uint32_t j0 = 0; j0 < rows; j0 += 16) {
             load(B, j0 + 8);
@@ -601,6 +637,10 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     // Large blocks test for skipping only late in the iteration (SALZ_PARSE_EARLY=1: from the
     // third pass like smaller blocks; mixed 100 MB: 22.3 -> 23.7 ms, text 4.5 -> 5.0 ms)
     const bool early = getenv("SALZ_PARSE_EARLY") && atoi(getenv("SALZ_PARSE_EARLY")) != 0;
+    // Packed candidates from the second pass on (g64 is free during the parse; SALZ_PARSE_PACK=0:
+    // the full ones every pass)
+    const bool pack = n < kPackLen && (!getenv("SALZ_PARSE_PACK") || atoi(getenv("SALZ_PARSE_PACK")) != 0);
+    uint2 *cand8 = pack ? reinterpret_cast<uint2 *>(ws.g64) : nullptr;
 
     hipLaunchKernelGGL(k_cost_seed, dim3(grid_for(S, kT)), dim3(kT), 0, st, cost[0], bl, klog, S);
     SALZ_LAUNCH_CHECK();
@@ -637,9 +677,14 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                 if (scan_sum_u32(brk, pbrk, (size_t)ps.nchunks + 1, false, nullptr, ws, st) != 0)
                     return -1;
             }
-            hipLaunchKernelGGL(k_parse_mark, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st,
-                               ws.cand, cin, cout, n, bl, klog, wdirty, dsum, ndirty,
-                               range_on ? reach : nullptr, pbrk);
+            if (pack)
+                hipLaunchKernelGGL(k_parse_mark<CandPacked>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st,
+                                   cand8, cin, cout, n, bl, klog, wdirty, dsum, ndirty, range_on ? reach : nullptr,
+                                   pbrk);
+            else
+                hipLaunchKernelGGL(k_parse_mark<CandFull>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st,
+                                   ws.cand, cin, cout, n, bl, klog, wdirty, dsum, ndirty,
+                                   range_on ? reach : nullptr, pbrk);
             SALZ_LAUNCH_CHECK();
             if (read_scalars(ws, 0, 256, "parse.mark") != 0)
                 return -1;
@@ -657,10 +702,16 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         // from the pass that chose them (stale exits only add nodes to the forest).
         if (!skipping)
             SALZ_HIP(hipMemsetAsync(eflag, 0, S, st));
-        hipLaunchKernelGGL(k_parse_chunk, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
-                           cin, ws.pst, chold, chnew, n, bl, klog, changed,
-                           reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord, eflag,
-                           skipping && skip_on ? wdirty : nullptr, dsum, it == 0 && range_on ? reach : nullptr);
+        uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
+        uint8_t *wd = skipping && skip_on ? wdirty : nullptr;
+        uint32_t *rch = it == 0 && range_on ? reach : nullptr;
+        if (pack && it > 0)
+            hipLaunchKernelGGL(k_parse_chunk<CandPacked>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, cand8,
+                               nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr, eflag, wd, dsum, rch);
+        else
+            hipLaunchKernelGGL(k_parse_chunk<CandFull>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
+                               it == 0 ? cand8 : nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr,
+                               eflag, wd, dsum, rch);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 256, "parse.changed") != 0)
             return -1;
