@@ -142,6 +142,32 @@ __host__ __device__ __forceinline__ uint64_t spos(size_t s, uint32_t klog)
     return (((uint64_t)t * 64u + l) << klog) | j;
 }
 
+// vnibble_size (lib/salz.c:565-588)
+__device__ __forceinline__ uint32_t vn_size(uint32_t v)
+{
+    uint32_t k = 1;
+    k += v >= 8u;
+    k += v >= 72u;
+    k += v >= 584u;
+    k += v >= 4680u;
+    k += v >= 37448u;
+    k += v >= 299592u;
+    k += v >= 2396744u;
+    k += v >= 19173960u;
+    k += v >= 153391688u;
+    k += v >= 1227133512u;
+    return k;
+}
+
+// A parse candidate side packed into one word: len | vn_size((off - 1) >> 8) << 28, the two
+// things the cost model needs (parse.hip CandPacked); len < 3 (no factor) is kept alone. Only
+// for blocks under 2^28 positions (len <= n).
+constexpr uint32_t kPackLen = (1u << 28) - 1u;
+__device__ __forceinline__ uint32_t pack_side(uint32_t off, uint32_t len)
+{
+    return len >= 3u ? (len & kPackLen) | vn_size((off - 1u) >> 8) << 28 : len & kPackLen;
+}
+
 // Index of slot s in a set kept as bits in slot order (ExitBits, internal.hpp): the set bits
 // before s, from the word prefix counts wpre and s's word.
 __device__ __forceinline__ uint32_t bits_index(const uint64_t *mask, const uint32_t *wpre, size_t s)

@@ -30,22 +30,6 @@ namespace {
 constexpr int kT = 256;
 constexpr uint32_t kNone = 0xffffffffu;
 
-__device__ __forceinline__ uint32_t vn_size(uint32_t v)
-{
-    uint32_t k = 1;
-    k += v >= 8u;
-    k += v >= 72u;
-    k += v >= 584u;
-    k += v >= 4680u;
-    k += v >= 37448u;
-    k += v >= 299592u;
-    k += v >= 2396744u;
-    k += v >= 19173960u;
-    k += v >= 153391688u;
-    k += v >= 1227133512u;
-    return k;
-}
-
 // Closed form of encode_vnibble_le (lib/salz.c:352-445): k octal digits of
 // v - S_{k-1} (S_j = sum_{i=1..j} 8^i), most significant first, terminator bit on the last.
 __device__ __forceinline__ uint64_t vn_bits(uint32_t v, uint32_t k)

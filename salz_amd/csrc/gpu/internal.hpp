@@ -8,6 +8,7 @@
 #include "common.hpp"
 #include "../../../include/salz_gpu.h"
 
+#include <cstdlib>
 #include <vector>
 
 namespace salz {

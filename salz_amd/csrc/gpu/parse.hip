@@ -30,23 +30,6 @@ namespace {
 
 constexpr int kT = 256;
 
-// vnibble_size (lib/salz.c:565-588)
-__device__ __forceinline__ uint32_t vn_size(uint32_t v)
-{
-    uint32_t k = 1;
-    k += v >= 8u;
-    k += v >= 72u;
-    k += v >= 584u;
-    k += v >= 4680u;
-    k += v >= 37448u;
-    k += v >= 299592u;
-    k += v >= 2396744u;
-    k += v >= 19173960u;
-    k += v >= 153391688u;
-    k += v >= 1227133512u;
-    return k;
-}
-
 // token bit + vnibble + offset byte + gr3 length (lib/salz.c:595-608, :632-634)
 __device__ __forceinline__ uint32_t factor_bits(uint32_t off, uint32_t len)
 {
@@ -57,7 +40,6 @@ __device__ __forceinline__ uint32_t factor_bits(uint32_t off, uint32_t len)
 // per side as len | (vnibble size of the offset's high part) << 28 (uint2, half the bytes), for
 // blocks under 2^28 positions. The first pass reads the full form and writes the packed one, which
 // every later pass and skip test reads.
-constexpr uint32_t kPackLen = (1u << 28) - 1u;
 struct CandFull {
     using T = uint4;
     static __device__ __forceinline__ uint32_t lp(T c) { return c.y; }
@@ -73,12 +55,7 @@ struct CandPacked {
     static __device__ __forceinline__ uint32_t bp(T c) { return 13u + 4u * (c.x >> 28) + (((c.x & kPackLen) - 3u) >> 3); }
     static __device__ __forceinline__ uint32_t bn(T c) { return 13u + 4u * (c.y >> 28) + (((c.y & kPackLen) - 3u) >> 3); }
 };
-__device__ __forceinline__ uint2 pack_cand(uint4 c)
-{
-    const uint32_t x = c.y >= 3u ? (c.y & kPackLen) | vn_size((c.x - 1u) >> 8) << 28 : c.y & kPackLen;
-    const uint32_t y = c.w >= 3u ? (c.w & kPackLen) | vn_size((c.z - 1u) >> 8) << 28 : c.w & kPackLen;
-    return make_uint2(x, y);
-}
+__device__ __forceinline__ uint2 pack_cand(uint4 c) { return make_uint2(pack_side(c.x, c.y), pack_side(c.z, c.w)); }
 __device__ __forceinline__ uint2 pack_cand(uint2 c) { return c; }  // (packed passes write none)
 
 // Storage slots 0..S-1 -> cost seed 3 * (n - p); slots past n unused. Any seed gives the

@@ -366,7 +366,7 @@ def test_lcp_paths(ctx, monkeypatch, lcp_sa, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
-@pytest.mark.parametrize("skip", ["1", "1r0", "0"])
+@pytest.mark.parametrize("skip", ["1", "1r0", "0", "1p0"])
 @pytest.mark.parametrize("kind,n,seed,alpha,klog", [("mixed", 3_000_000, 3, 0, "6"),
                                                     ("mixed", 2_000_001, 7, 0, "9"),
                                                     ("text", 1_500_000, 2, 0, "7"),
@@ -376,9 +376,11 @@ def test_parse_wave_skip(ctx, monkeypatch, skip, kind, n, seed, alpha, klog):
     """From the third pass on, waves of chunks whose decisions would repeat skip the pass
     (parse.hip k_parse_mark, SALZ_PARSE_SKIP=1, the default): decisions, the exact suffix
     costs and the stream match the oracle with and without skipping, with the chunk range test
-    (SALZ_PARSE_RANGE=1, the default) and the per-candidate test alone ("1r0")."""
+    (SALZ_PARSE_RANGE=1, the default) and the per-candidate test alone ("1r0"), on the packed
+    candidates (SALZ_PARSE_PACK=1, the default) and the full ones ("1p0")."""
     monkeypatch.setenv("SALZ_PARSE_SKIP", skip[0])
     monkeypatch.setenv("SALZ_PARSE_RANGE", "0" if skip == "1r0" else "1")
+    monkeypatch.setenv("SALZ_PARSE_PACK", "0" if skip == "1p0" else "1")
     monkeypatch.setenv("SALZ_PARSE_KLOG", klog)
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
