@@ -257,7 +257,7 @@ __global__ __launch_bounds__(kT) void k_grpscan(const uint32_t *__restrict__ hea
                                                 const uint32_t *__restrict__ Gp, uint32_t nwv,
                                                 const uint64_t *__restrict__ wg,
                                                 const uint64_t *__restrict__ wl,
-                                                uint64_t *__restrict__ gsc, uint64_t *__restrict__ lsc)
+                                                uint64_t *__restrict__ gsc, uint64_t *__restrict__ lsc, int all)
 {
     const uint32_t G = *Gp, lane = threadIdx.x & 63u;
     const uint32_t nw = (uint32_t)(((uint64_t)G + 63) / 64) < nwv ? (uint32_t)(((uint64_t)G + 63) / 64) : nwv;
@@ -279,10 +279,12 @@ __global__ __launch_bounds__(kT) void k_grpscan(const uint32_t *__restrict__ hea
             }
         }
         const uint64_t pg = wg[w], pl = wl[w];
-        if (g < G) {
+        // k_commit reads gsc only for survivors and lsc only for large groups (every group's
+        // entry only for the per-round checks): most groups of a wide round are singletons
+        if (g < G && (gc || all))
             gsc[g] = pg + ((uint64_t)(xs - gs) << 32 | (xc - gc));
+        if (g < G && (lc || all))
             lsc[g] = pl + ((uint64_t)(ys - ls) << 32 | (yc - lc));
-        }
     }
 }
 
@@ -528,11 +530,11 @@ __global__ void k_rank_upper(const uint32_t *__restrict__ val, const uint32_t *_
 
 // Window plan of the LDS sort, one thread per surviving group (groups are in list order, so
 // the groups that start in one window are consecutive ids): the first group starting in a
-// window writes the window's lo and first group id, the last one its hi. A large group can
-// only be the last to start in its window (it runs past the window's end), so the owned
-// small groups are [lo, hi) with hi = the large group's start in that case.
+// window writes the window's lo and first group id, the last one its hi and last small group
+// id. A large group can only be the last to start in its window (it runs past the window's
+// end), so the owned small groups are [lo, hi) with hi = the large group's start in that case.
 struct SegPlan {
-    uint32_t *lo, *hi, *g0;
+    uint32_t *lo, *hi, *g0, *g1;
 };
 
 __global__ void k_seg_plan(const uint64_t *__restrict__ ginfo, uint32_t G, SegPlan plan)
@@ -540,22 +542,24 @@ __global__ void k_seg_plan(const uint64_t *__restrict__ ginfo, uint32_t G, SegPl
     size_t g = (size_t)blockIdx.x * kT + threadIdx.x;
     if (g >= G)
         return;
-    const uint64_t gi = ginfo[g];
+    // unconditional loads (clamped neighbours)
+    const uint64_t gi = ginfo[g], gp = ginfo[g ? g - 1 : 0], gn = ginfo[g + 1 < G ? g + 1 : g];
     const uint32_t size = (uint32_t)(gi >> 32), cs = (uint32_t)gi;
     const uint32_t w = cs / kSegT;
-    if ((g == 0 || (uint32_t)ginfo[g - 1] / kSegT != w) && size <= kSmall) {
+    if ((g == 0 || (uint32_t)gp / kSegT != w) && size <= kSmall) {
         plan.lo[w] = cs;
         plan.g0[w] = (uint32_t)g;
     }
-    if (g + 1 == G || (uint32_t)ginfo[g + 1] / kSegT != w)
+    if (g + 1 == G || (uint32_t)gn / kSegT != w) {
         plan.hi[w] = size <= kSmall ? cs + size : cs;
+        plan.g1[w] = size <= kSmall ? (uint32_t)g : (uint32_t)g - 1u;
+    }
 }
 
 // Stable 8-bit LSD passes over bits [12, 12 + nbits) of ITEMS * 256 LDS keys; wave-striped:
 // wave w owns slots [w * ITEMS * 64, (w + 1) * ITEMS * 64), item j covers 64 of them.
 template <int ITEMS>
-__device__ __forceinline__ void seg_lsd(uint64_t *sk, uint32_t (*cnt)[256], uint32_t *dstart,
-                                        uint32_t *wsum, int nbits)
+__device__ __forceinline__ void seg_lsd(uint64_t *sk, uint32_t (*cnt)[256], uint32_t *wsum, int nbits)
 {
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     __syncthreads();
@@ -604,17 +608,17 @@ __device__ __forceinline__ void seg_lsd(uint64_t *sk, uint32_t (*cnt)[256], uint
             uint32_t pre = 0;
             for (unsigned w = 0; w < wave; w++)
                 pre += wsum[w];
-            dstart[tid] = pre + x - tot;
-            cnt[0][tid] = 0;
-            cnt[1][tid] = c0;
-            cnt[2][tid] = c0 + c1;
-            cnt[3][tid] = c0 + c1 + c2;
+            const uint32_t ds = pre + x - tot;  // the digit's start; the waves' starts follow
+            cnt[0][tid] = ds;
+            cnt[1][tid] = ds + c0;
+            cnt[2][tid] = ds + c0 + c1;
+            cnt[3][tid] = ds + c0 + c1 + c2;
         }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < ITEMS; j++) {
             const unsigned d = (unsigned)(k[j] >> shift) & 255u;
-            sk[dstart[d] + cnt[wave][d] + lrank[j]] = k[j];
+            sk[cnt[wave][d] + lrank[j]] = k[j];
         }
         __syncthreads();
     }
@@ -630,108 +634,92 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
                                                            const uint64_t *__restrict__ ginfo, uint32_t m,
                                                            int kb, uint32_t tiny, uint32_t *err)
 {
-    __shared__ uint64_t sk[kSegCap];  // keys; at the end the window's values (as u32)
+    __shared__ uint64_t sk[kSegCap];  // keys
+    __shared__ uint32_t sv[kSegCap];  // the window's values, loaded with the keys
     __shared__ uint32_t cnt[4][256];
-    __shared__ uint32_t dstart[256];
     __shared__ uint32_t wsum[4];
-    __shared__ uint32_t smax;
 
     const unsigned tid = threadIdx.x;
     const uint32_t w = blockIdx.x;
     const uint32_t lo = plan.lo[w];
     if (lo == 0xffffffffu)
         return;  // uniform: no small group starts in this window
-    const uint32_t hi = plan.hi[w], g0 = plan.g0[w];
-    if (bad_index(hi > m || hi <= lo || hi - lo >= kSegCap, err, kErrSeg))
+    const uint32_t hi = plan.hi[w], g0 = plan.g0[w], g1 = plan.g1[w];
+    if (bad_index(hi > m || hi <= lo || hi - lo >= kSegCap || g1 < g0, err, kErrSeg))
         return;
     const uint32_t count = hi - lo;
     const uint64_t mask = (1ull << kb) - 1ull;
-    const uint32_t glast = (uint32_t)(K[hi - 1] >> kb);
-    const int nbits = kb + (32 - __builtin_clz((glast - g0) | 1u));
-    if (tid == 0)
-        smax = 0;
+    const int nbits = kb + (32 - __builtin_clz((g1 - g0) | 1u));
 
     // slots actually sorted: count rounded up to 1024 (4 waves x 64 lanes x ITEMS / 4 steps)
     const int items = (int)((count + 1023u) / 1024u) * 4;
-    uint32_t gmax = 0;  // largest group among this thread's entries
     for (uint32_t i = tid; i < (uint32_t)items * kSegThreads; i += kSegThreads) {
         uint64_t key = ~0ull;  // padding sorts last in every digit
         if (i < count) {
             const uint64_t kk = K[lo + i];
+            sv[i] = V[lo + i];
             key = (((kk >> kb) - g0) << (kb + 12)) | ((kk & mask) << 12) | i;
-            if (tiny) {
-                const uint32_t s = (uint32_t)(ginfo[kk >> kb] >> 32);
-                gmax = s > gmax ? s : gmax;
-            }
         }
         sk[i] = key;
     }
+    // the largest owned group (its sizes are contiguous in ginfo), for the counting order
+    uint32_t gmax = 0;
     if (tiny) {
+        for (uint32_t g = g0 + tid; g <= g1; g += kSegThreads) {
+            const uint32_t s = (uint32_t)(ginfo[g] >> 32);
+            gmax = s > gmax ? s : gmax;
+        }
+        gmax = wave_max_u32(gmax);
+        if (lane_id() == 0)
+            wsum[tid >> 6] = gmax;
+    }
+    __syncthreads();
+    const uint32_t m01 = wsum[0] > wsum[1] ? wsum[0] : wsum[1], m23 = wsum[2] > wsum[3] ? wsum[2] : wsum[3];
+    if (tiny && (m01 > m23 ? m01 : m23) <= tiny) {
         // Windows of tiny groups only: each entry's place is its group's start plus the members
         // with smaller (rank, slot), counted in LDS (at most `tiny` reads per entry instead of
         // nbits / 8 LSD passes). Same order as the stable LSD passes.
-        gmax = wave_max_u32(gmax);
-        __syncthreads();  // smax initialised
-        if (lane_id() == 0)
-            atomicMax(&smax, gmax);
-        __syncthreads();
-        if (smax <= tiny) {
-            constexpr uint32_t kPer = kSegCap / kSegThreads;
-            uint32_t dst[kPer], vv[kPer];
-            uint64_t nk[kPer];
+        // (every key and value of the window is staged: the stores below may overwrite them)
+        constexpr uint32_t kPer = kSegCap / kSegThreads;
+        uint32_t dst[kPer];
+        uint64_t nk[kPer];
 #pragma unroll
-            for (uint32_t j = 0; j < kPer; j++) {
-                const uint32_t i = tid + j * kSegThreads, ii = i < count ? i : 0u;
-                const uint64_t ki = sk[ii];
-                const uint64_t g = g0 + (ki >> (kb + 12));
-                const uint64_t gi = ginfo[g];  // unconditional loads (clamped entry)
-                vv[j] = V[lo + ii];
-                const uint32_t gs = (uint32_t)gi - lo, s = (uint32_t)(gi >> 32);
-                uint32_t r = 0;
-                for (uint32_t x = gs; x < gs + s; x++)
-                    r += sk[x] < ki ? 1u : 0u;
-                dst[j] = i < count ? lo + gs + r : 0xffffffffu;
-                nk[j] = (g << kb) | ((ki >> 12) & mask);
-            }
-            __syncthreads();  // every value read before any is overwritten
-#pragma unroll
-            for (uint32_t j = 0; j < kPer; j++)
-                if (dst[j] != 0xffffffffu) {
-                    K[dst[j]] = nk[j];
-                    V[dst[j]] = vv[j];
-                }
-            return;
+        for (uint32_t j = 0; j < kPer; j++) {
+            const uint32_t i = tid + j * kSegThreads, ii = i < count ? i : 0u;
+            const uint64_t ki = sk[ii];
+            const uint64_t g = g0 + (ki >> (kb + 12));
+            const uint64_t gi = ginfo[g];  // unconditional loads (clamped entry)
+            const uint32_t gs = (uint32_t)gi - lo, s = (uint32_t)(gi >> 32);
+            uint32_t r = 0;
+            for (uint32_t x = gs; x < gs + s; x++)
+                r += sk[x] < ki ? 1u : 0u;
+            dst[j] = lo + gs + r;
+            nk[j] = (g << kb) | ((ki >> 12) & mask);
         }
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j++) {
+            const uint32_t i = tid + j * kSegThreads;
+            if (i < count) {
+                K[dst[j]] = nk[j];
+                V[dst[j]] = sv[i];
+            }
+        }
+        return;
     }
     switch (items) {
-    case 4: seg_lsd<4>(sk, cnt, dstart, wsum, nbits); break;
-    case 8: seg_lsd<8>(sk, cnt, dstart, wsum, nbits); break;
-    case 12: seg_lsd<12>(sk, cnt, dstart, wsum, nbits); break;
-    default: seg_lsd<16>(sk, cnt, dstart, wsum, nbits); break;
+    case 4: seg_lsd<4>(sk, cnt, wsum, nbits); break;
+    case 8: seg_lsd<8>(sk, cnt, wsum, nbits); break;
+    case 12: seg_lsd<12>(sk, cnt, wsum, nbits); break;
+    default: seg_lsd<16>(sk, cnt, wsum, nbits); break;
     }
 
-    // Sorted keys to registers, then the same LDS bytes take the window's values (read only
-    // now: a separate 16 KB value stage would leave room for 3 workgroups per CU instead of 4).
-    uint64_t outk[kSegCap / kSegThreads];
-#pragma unroll
-    for (uint32_t j = 0; j < kSegCap / kSegThreads; j++) {
-        const uint32_t i = tid + j * kSegThreads;
-        outk[j] = i < count ? sk[i] : 0ull;
-    }
-    __syncthreads();
-    uint32_t *sv = reinterpret_cast<uint32_t *>(sk);
-    for (uint32_t i = tid; i < count; i += kSegThreads)
-        sv[i] = V[lo + i];
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < kSegCap / kSegThreads; j++) {
-        const uint32_t i = tid + j * kSegThreads;
-        if (i < count) {
-            const uint64_t key = outk[j];
-            const uint64_t g = g0 + (key >> (kb + 12));
-            K[lo + i] = (g << kb) | ((key >> 12) & mask);
-            V[lo + i] = sv[key & 0xfffu];
-        }
+    // The values were staged with the keys (a separate 16 KB stage: their HBM load overlaps the
+    // keys' instead of following the sort, and no sorted keys wait in registers).
+    for (uint32_t i = tid; i < count; i += kSegThreads) {
+        const uint64_t key = sk[i];
+        const uint64_t g = g0 + (key >> (kb + 12));
+        K[lo + i] = (g << kb) | ((key >> 12) & mask);
+        V[lo + i] = sv[key & 0xfffu];
     }
 }
 
@@ -1051,7 +1039,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                 seg_round = true;
                 const uint32_t nwin = grid_for(m, kSegT);
                 uint32_t *pw = reinterpret_cast<uint32_t *>(ws.lsc);  // free during the sort
-                SegPlan plan{pw, pw + nwin, pw + 2 * nwin};
+                SegPlan plan{pw, pw + nwin, pw + 2 * nwin, pw + 3 * nwin};
                 SALZ_HIP(hipMemsetAsync(plan.lo, 0xff, sizeof(uint32_t) * nwin, st));
                 hipLaunchKernelGGL(k_seg_plan, dim3(grid_for(G_act, kT)), dim3(kT), 0, st, tab.ginfo,
                                    G_act, plan);
@@ -1113,7 +1101,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             // per-wave group sums in u1 (u0 holds the head ballots until k_commit)
             uint64_t *wg = reinterpret_cast<uint64_t *>(ws.u1), *wl = wg + nw_max;
             const uint32_t nwg = (uint32_t)(((uint64_t)(need_G ? G : m) + 63) / 64);
-            const unsigned ggrid = grid_for((size_t)nwg * 64, kT) < 8192u ? grid_for((size_t)nwg * 64, kT) : 8192u;
+            const unsigned ggrid = grid_for((size_t)nwg * 64, kT);  // one wave per 64 groups
             hipLaunchKernelGGL(k_grpsum, dim3(ggrid), dim3(kT), 0, st, headpos, d32 + 0, nwg, wg, wl);
             SALZ_LAUNCH_CHECK();
             if (scan_sum_u64(wg, wg, nwg, false, d64, ws, st) != 0)
@@ -1121,7 +1109,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             if (scan_sum_u64(wl, wl, nwg, false, d64 + 1, ws, st) != 0)
                 return -1;
             hipLaunchKernelGGL(k_grpscan, dim3(ggrid), dim3(kT), 0, st, headpos, d32 + 0, nwg, wg,
-                               wl, gsc, ws.lsc);
+                               wl, gsc, ws.lsc, dbg_rounds ? 1 : 0);
             SALZ_LAUNCH_CHECK();
         }
         if (dbg_rounds) {
