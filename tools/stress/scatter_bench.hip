@@ -45,6 +45,39 @@ __global__ void k_gather4(const uint32_t *idx, uint32_t count, const uint32_t *s
         out[i] = src[idx[i]];
 }
 
+// ILP variants: each thread handles U elements (i, i + G, ..., G = grid threads), every index
+// and gathered word loaded before any is used, so U random accesses are in flight per lane.
+template <int U>
+__global__ void k_gather4_ilp(const uint32_t *idx, uint32_t count, const uint32_t *src, uint32_t *out)
+{
+    const uint32_t G = gridDim.x * 256, i0 = blockIdx.x * 256 + threadIdx.x;
+    uint32_t x[U], v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        x[u] = idx[i0 + u * G < count ? i0 + u * G : 0];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        v[u] = src[x[u]];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        if (i0 + u * G < count)
+            out[i0 + u * G] = v[u];
+}
+
+template <int U>
+__global__ void k_scatter4_ilp(const uint32_t *idx, uint32_t count, uint32_t *dst)
+{
+    const uint32_t G = gridDim.x * 256, i0 = blockIdx.x * 256 + threadIdx.x;
+    uint32_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        x[u] = idx[i0 + u * G < count ? i0 + u * G : 0];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        if (i0 + u * G < count)
+            dst[x[u]] = i0 + u * G;
+}
+
 __global__ void k_copy4(const uint32_t *a, uint32_t count, uint32_t *b)
 {
     uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -89,6 +122,15 @@ int main()
         float g4 = timeit([&] { hipLaunchKernelGGL(k_gather4, g, dim3(256), 0, 0, idx, count, big, out); });
         printf("%-28s %10llu %10.3f %12.4f\n", "scatter 4B", (unsigned long long)(span >> 20), s4, s4 * 1e6 / count);
         printf("%-28s %10llu %10.3f %12.4f\n", "gather 4B", (unsigned long long)(span >> 20), g4, g4 * 1e6 / count);
+        dim3 q2((count + 511) / 512), q4((count + 1023) / 1024), q8((count + 2047) / 2048);
+        float a2 = timeit([&] { hipLaunchKernelGGL(k_gather4_ilp<2>, q2, dim3(256), 0, 0, idx, count, big, out); });
+        float a4 = timeit([&] { hipLaunchKernelGGL(k_gather4_ilp<4>, q4, dim3(256), 0, 0, idx, count, big, out); });
+        float a8 = timeit([&] { hipLaunchKernelGGL(k_gather4_ilp<8>, q8, dim3(256), 0, 0, idx, count, big, out); });
+        float b4 = timeit([&] { hipLaunchKernelGGL(k_scatter4_ilp<4>, q4, dim3(256), 0, 0, idx, count, big); });
+        printf("%-28s %10llu %10.3f %12.4f\n", "gather 4B x2/thread", (unsigned long long)(span >> 20), a2, a2 * 1e6 / count);
+        printf("%-28s %10llu %10.3f %12.4f\n", "gather 4B x4/thread", (unsigned long long)(span >> 20), a4, a4 * 1e6 / count);
+        printf("%-28s %10llu %10.3f %12.4f\n", "gather 4B x8/thread", (unsigned long long)(span >> 20), a8, a8 * 1e6 / count);
+        printf("%-28s %10llu %10.3f %12.4f\n", "scatter 4B x4/thread", (unsigned long long)(span >> 20), b4, b4 * 1e6 / count);
         uint32_t slots16 = (uint32_t)(span / 16);
         hipLaunchKernelGGL(k_idx, g, dim3(256), 0, 0, idx, count, slots16, 9u);
         float s16 = timeit([&] { hipLaunchKernelGGL(k_scatter16, g, dim3(256), 0, 0, idx, count, (uint4 *)big); });
