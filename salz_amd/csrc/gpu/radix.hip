@@ -1,7 +1,8 @@
 // radix.hip - stable LSD radix sort of (u64 key, u32 value) pairs for gfx950.
 //
 // One 8-bit digit per pass, 4096-element tiles (256 threads x 16 items), reduce-then-scan:
-//   k_radix_hist    per-tile digit counts (LDS atomics into per-wave sub-histograms)
+//   k_radix_hist    per-tile digit counts (LDS atomics into per-wave sub-histograms), from the
+//                   keys or, after a pass that wrote them, from a byte array of this pass's digits
 //   k_radix_rowscan per-digit prefixes of the counts over the tiles (+ digit totals; the
 //                   scatter adds the digit bases)
 //   k_radix_scatter stable tile-local ranking with wave ballots (8 ballots build the peer
@@ -52,7 +53,8 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
                                                          const uint32_t *__restrict__ vals,
                                                          uint32_t m, int shift,
                                                          uint32_t *__restrict__ counts,
-                                                         uint32_t ntiles, TextSrc txt)
+                                                         uint32_t ntiles, TextSrc txt,
+                                                         const uint8_t *__restrict__ dig)
 {
     // 32 sub-histograms (8 per wave, by lane & 7), 257 words apart so the copies of one digit
     // sit in different banks: lanes of a wave adding to a hot digit (text keys' leading bytes
@@ -86,6 +88,21 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
         for (int j = 0; j < kItems; j++)
             if ((size_t)j * kThreads + tid < left)
                 atomicAdd(&mine[(unsigned)(kk[j] >> shift) & 255u], 1u);
+    } else if (dig) {
+        // this pass's digits as bytes (written by the previous scatter): 16 per thread, one
+        // 16-byte load, instead of 16 keys of 8 bytes
+        const uint8_t *d = dig + base + (size_t)tid * kItems;
+        if (left >= (size_t)kTile) {
+            const uint4 x = *reinterpret_cast<const uint4 *>(d);
+            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int j = 0; j < kItems; j++)
+                atomicAdd(&mine[(w[j >> 2] >> (8 * (j & 3))) & 255u], 1u);
+        } else {
+            for (int j = 0; j < kItems; j++)
+                if ((size_t)tid * kItems + j < left)
+                    atomicAdd(&mine[d[j]], 1u);
+        }
     } else if (left >= (size_t)kTile) {
         uint4 x[kItems / 2];
 #pragma unroll
@@ -170,7 +187,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
     uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t m, int shift,
     const uint32_t *__restrict__ offs, uint32_t ntiles, const uint32_t *__restrict__ totals,
-    TextSrc txt)
+    TextSrc txt, uint8_t *__restrict__ dout, int nshift)
 {
     // Keys and values are staged one after the other in the same 32 KB (4 workgroups per CU
     // instead of 2 with a 48 KB key + value stage).
@@ -313,6 +330,8 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
             unsigned d = (unsigned)(key >> shift) & 255u;
             gdst[j] = gbase[d] + (s - dstart[d]);
             kout[gdst[j]] = key;
+            if (dout)  // the next pass's digit, for its histogram
+                dout[gdst[j]] = (uint8_t)(key >> nshift);
         }
     }
     __syncthreads();  // keys out of LDS; the same bytes now stage the values
@@ -335,7 +354,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
 
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
-                     const uint8_t *text, const Blocks *blocks, const Alpha *alpha)
+                     const uint8_t *text, const Blocks *blocks, const Alpha *alpha, uint8_t *digits)
 {
     if (m <= 1 || bit_hi <= bit_lo)
         return 0;
@@ -356,17 +375,21 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
         const int mode = pass >= passes_key ? 2 : (text && pass == 0) ? 1 : 0;
         const int shift = mode == 2 ? 8 * (pass - passes_key) : bit_lo + 8 * pass;
         TextSrc txt{text, g, Alpha{}};
+        // digit bytes: written by a key pass for the next key pass, read by that pass's histogram
+        const uint8_t *dig_in = digits && pass > 0 && mode == 0 ? digits : nullptr;
+        uint8_t *dig_out = digits && pass + 1 < passes_key ? digits : nullptr;
+        const int nshift = bit_lo + 8 * (pass + 1);
         if (alpha)
             txt.a = *alpha;
         if (mode == 1)
             hipLaunchKernelGGL(k_radix_hist<1>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
-                               shift, ws.radix_counts, ntiles, txt);
+                               shift, ws.radix_counts, ntiles, txt, dig_in);
         else if (mode == 2)
             hipLaunchKernelGGL(k_radix_hist<2>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
-                               shift, ws.radix_counts, ntiles, txt);
+                               shift, ws.radix_counts, ntiles, txt, dig_in);
         else
             hipLaunchKernelGGL(k_radix_hist<0>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
-                               shift, ws.radix_counts, ntiles, txt);
+                               shift, ws.radix_counts, ntiles, txt, dig_in);
         SALZ_LAUNCH_CHECK();
         uint32_t *totals = ws.radix_counts + ncounts;
         hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(kRowThreads), 0, st, ws.radix_counts,
@@ -379,13 +402,13 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used], st));
         if (mode == 1)
             hipLaunchKernelGGL(k_radix_scatter<1>, dim3(ntiles), dim3(kThreads), 0, st, kin,
-                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt);
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
         else if (mode == 2)
             hipLaunchKernelGGL(k_radix_scatter<2>, dim3(ntiles), dim3(kThreads), 0, st, kin,
-                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt);
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
         else
             hipLaunchKernelGGL(k_radix_scatter<0>, dim3(ntiles), dim3(kThreads), 0, st, kin,
-                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt);
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
         SALZ_LAUNCH_CHECK();
         if (timed) {
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used + 1], st));

@@ -1002,6 +1002,10 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // k_seg_small windows whose groups all have at most seg_tiny members are ordered by counting
     // (SALZ_SEG_TINY=0: LSD passes everywhere)
     const uint32_t seg_tiny = getenv("SALZ_SEG_TINY") ? (uint32_t)atoi(getenv("SALZ_SEG_TINY")) : 32u;
+    // Digit bytes of the radix passes (radix.hip) in u2, free during every sort (the head
+    // positions are written after it); SALZ_RADIX_DIGITS=0: histograms read the keys
+    uint8_t *rdig = getenv("SALZ_RADIX_DIGITS") && atoi(getenv("SALZ_RADIX_DIGITS")) == 0
+                        ? nullptr : reinterpret_cast<uint8_t *>(ws.u2);
     auto t_round = std::chrono::steady_clock::now();
     for (;;) {
         ws.stats.sa_rounds++;
@@ -1017,7 +1021,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             }
             const int key_bits = alpha.bits ? (int)(alpha.k * alpha.bits) : 64;
             const uint8_t *src_text = !text_first ? nullptr : tmapped ? tmapped : ws.text;
-            if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, key_bits, ws, st, src_text, &bl, &alpha) != 0)
+            if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, key_bits, ws, st, src_text, &bl, &alpha, rdig) != 0)
                 return -1;
         } else {
             // Global sort of every active suffix on (group, rank) vs. LDS sort of the small
@@ -1032,7 +1036,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             if (mode_env)
                 seg = strcmp(mode_env, "segmented") == 0;
             if (!seg) {
-                if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, bits_all, ws, st) != 0)
+                if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, bits_all, ws, st, nullptr, nullptr, nullptr, rdig) != 0)
                     return -1;
             } else {
                 how = "segmented";
@@ -1053,7 +1057,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                     SALZ_LAUNCH_CHECK();
                     uint64_t *KS = KC;
                     uint32_t *VS = VC;
-                    if (radix_sort_pairs(&KS, &VS, Kx, Vx, mL, 0, bits_large, ws, st) != 0)
+                    if (radix_sort_pairs(&KS, &VS, Kx, Vx, mL, 0, bits_large, ws, st, nullptr, nullptr, nullptr, rdig) != 0)
                         return -1;
                     hipLaunchKernelGGL(k_putback, dim3(grid_for(mL, kT)), dim3(kT), 0, st, KS, VS,
                                        tab.lrec, tab.lg2g, mL, GL, m, kb, K, V, derr);

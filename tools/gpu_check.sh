@@ -15,6 +15,7 @@ tail -3 $out/pytest.log; cat $out/smoke.log $out/bench.json 2>/dev/null
 [ $rc -ne 0 ] && exit $rc
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc_fetch -o pmc -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 > $out/pmc_fetch.json 2> $out/pmc_fetch.err &&
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc_write -o pmc -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 > $out/pmc_write.json 2> $out/pmc_write.err &&
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $out/pmc_sq -o pmc -- python3 bench.py --no-cpu-baseline --no-e2e --steps 1 --warmup 0 > $out/pmc_sq.json 2> $out/pmc_sq.err &&
 SALZ_DEBUG_SA=1 timeout -k 10 120 python bench.py --no-cpu-baseline --steps 1 --warmup 0 > $out/text_sa.json 2> $out/text_sa.log &&
 SALZ_DEBUG_SA=1 timeout -k 10 200 python bench.py --no-cpu-baseline --workload fib256 --steps 2 --warmup 1 > $out/fib.json 2> $out/fib_sa.log &&
 timeout -k 10 200 python bench.py --no-cpu-baseline --kind mixed --steps 2 --warmup 1 > $out/mixed.json 2> $out/mixed.err &&
