@@ -23,8 +23,11 @@
 //               the LCP of every new head with its predecessor (see the comment there; k_heads
 //               once the LCP is left to the Phi/PLCP stage)
 //   scan        of the per-wave head counts; k_headpos -> group ids and head index per group
-//   k_grpsum /  groups of size >= 2 survive; exclusive scans (per-wave sums, then per group)
-//   k_grpscan   pack (compact start, new gid) and (start in the extracted array, large-group id)
+//   k_surv      groups of size >= 2 survive: per wave of the list, the survivor entries and the
+//               survivor heads as bit masks (from the head ballots alone: a head whose successor
+//               is a head too is a singleton); their counts are scanned, so an entry's compact
+//               index and new group id are prefix + popcount (large groups take their ids and
+//               extraction ranges with one atomic per group in k_commit)
 //   k_commit    rank update for every active suffix (in large rounds staged by text range
 //               and applied window by window: k_rank_stage / k_rank_apply), SA write for
 //               singletons, compaction
@@ -208,84 +211,32 @@ __global__ void k_headpos(HeadBits hb, uint32_t m, uint32_t *__restrict__ headpo
         headpos[g] = m;
 }
 
-// Per group: (size << 32 | 1) for survivors (size >= 2) in gsc and for large groups
-// (size > kSmall) in lsc; k_commit reads their exclusive scans. Both halves sum below 2^32
-// (sizes sum to at most m, counts to at most G), so a wave sums them as two u32 lanes.
-// k_grpsum leaves one (gsc, lsc) sum per wave of groups; after a scan of those, k_grpscan
-// writes the per-group exclusive prefixes.
-__device__ __forceinline__ void grp_vals(const uint32_t *__restrict__ headpos, size_t g, uint32_t G,
-                                         uint32_t &gs, uint32_t &gc, uint32_t &ls, uint32_t &lc)
+// Survivor masks of wave word w of the list (entries 64w .. 64w + 63): entry c is in a
+// singleton group iff it is a head and so is c + 1 (or c is the last entry). se: entries of
+// groups of size >= 2; sh: heads of those groups. Both loads unconditional (clamped word).
+__device__ __forceinline__ void surv_masks(const HeadBits &hb, size_t w, uint32_t m, uint64_t &se, uint64_t &sh)
 {
-    const size_t gg = g < G ? g : 0;  // unconditional loads (clamped)
-    const uint32_t size = headpos[gg + 1] - headpos[gg];
-    const bool in = g < G;
-    gc = in && size >= 2 ? 1u : 0u;
-    gs = gc ? size : 0u;
-    lc = in && size > kSmall ? 1u : 0u;
-    ls = lc ? size : 0u;
+    const size_t nw = ((size_t)m + 63) / 64;
+    const bool more = w + 1 < nw;
+    const uint64_t h = hb.hmask[w], hn = hb.hmask[more ? w + 1 : w];
+    uint64_t nh = (h >> 1) | (more ? (hn & 1ull) << 63 : 0ull);
+    const uint64_t left = (uint64_t)m - (uint64_t)w * 64;  // >= 1
+    const uint64_t valid = left >= 64 ? ~0ull : (1ull << left) - 1ull;
+    if (left <= 64)
+        nh |= 1ull << (left - 1);  // the last entry's successor is past the list
+    se = valid & ~(h & nh);
+    sh = valid & h & ~nh;
 }
 
-// G is read on the device (the host does not wait for it in most rounds); both kernels loop
-// over waves of groups, nwv waves at most (the scan runs over all nwv wave sums).
-__global__ __launch_bounds__(kT) void k_grpsum(const uint32_t *__restrict__ headpos,
-                                               const uint32_t *__restrict__ Gp, uint32_t nwv,
-                                               uint64_t *__restrict__ wg, uint64_t *__restrict__ wl)
+// Per wave word: (survivor entries << 32 | survivor heads); k_commit reads their exclusive scan.
+__global__ __launch_bounds__(kT) void k_surv(HeadBits hb, uint32_t m, uint64_t *__restrict__ P)
 {
-    const uint32_t G = *Gp, lane = threadIdx.x & 63u;
-    for (uint32_t w = blockIdx.x * (kT / 64) + (threadIdx.x >> 6); w < nwv;
-         w += gridDim.x * (kT / 64)) {
-        const size_t g = (size_t)w * 64 + lane;
-        uint32_t gs = 0, gc = 0, ls = 0, lc = 0;
-        if ((size_t)w * 64 < G) {  // wave-uniform
-            grp_vals(headpos, g, G, gs, gc, ls, lc);
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                gs += shfl_xor_u32(gs, d);
-                gc += shfl_xor_u32(gc, d);
-                ls += shfl_xor_u32(ls, d);
-                lc += shfl_xor_u32(lc, d);
-            }
-        }
-        if (lane == 0) {
-            wg[w] = (uint64_t)gs << 32 | gc;
-            wl[w] = (uint64_t)ls << 32 | lc;
-        }
-    }
-}
-
-__global__ __launch_bounds__(kT) void k_grpscan(const uint32_t *__restrict__ headpos,
-                                                const uint32_t *__restrict__ Gp, uint32_t nwv,
-                                                const uint64_t *__restrict__ wg,
-                                                const uint64_t *__restrict__ wl,
-                                                uint64_t *__restrict__ gsc, uint64_t *__restrict__ lsc, int all)
-{
-    const uint32_t G = *Gp, lane = threadIdx.x & 63u;
-    const uint32_t nw = (uint32_t)(((uint64_t)G + 63) / 64) < nwv ? (uint32_t)(((uint64_t)G + 63) / 64) : nwv;
-    for (uint32_t w = blockIdx.x * (kT / 64) + (threadIdx.x >> 6); w < nw;
-         w += gridDim.x * (kT / 64)) {
-        const size_t g = (size_t)w * 64 + lane;
-        uint32_t gs, gc, ls, lc;
-        grp_vals(headpos, g, G, gs, gc, ls, lc);
-        uint32_t xs = gs, xc = gc, ys = ls, yc = lc;  // inclusive wave scans
-#pragma unroll
-        for (unsigned d = 1; d < 64; d <<= 1) {
-            const uint32_t a = shfl_up_u32(xs, d), b = shfl_up_u32(xc, d);
-            const uint32_t e = shfl_up_u32(ys, d), f = shfl_up_u32(yc, d);
-            if (lane >= d) {
-                xs += a;
-                xc += b;
-                ys += e;
-                yc += f;
-            }
-        }
-        const uint64_t pg = wg[w], pl = wl[w];
-        // k_commit reads gsc only for survivors and lsc only for large groups (every group's
-        // entry only for the per-round checks): most groups of a wide round are singletons
-        if (g < G && (gc || all))
-            gsc[g] = pg + ((uint64_t)(xs - gs) << 32 | (xc - gc));
-        if (g < G && (lc || all))
-            lsc[g] = pl + ((uint64_t)(ys - ls) << 32 | (yc - lc));
-    }
+    const size_t w = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (w >= ((size_t)m + 63) / 64)
+        return;
+    uint64_t se, sh;
+    surv_masks(hb, w, m, se, sh);
+    P[w] = ((uint64_t)__popcll(se) << 32) | (uint64_t)__popcll(sh);
 }
 
 // Next round's group table (ginfo: size << 32 | compact start, gl: large-group id) is
@@ -299,7 +250,7 @@ struct GroupTab {
 
 __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
                          HeadBits hb, const uint32_t *__restrict__ headpos,
-                         const uint64_t *__restrict__ gsc, const uint64_t *__restrict__ lsc,
+                         const uint64_t *__restrict__ P, unsigned long long *__restrict__ lcount,
                          const uint32_t *__restrict__ off_old, uint32_t *__restrict__ off_new,
                          uint32_t *__restrict__ nval, uint32_t *__restrict__ ngid,
                          uint32_t *__restrict__ rank, uint32_t *__restrict__ sa, GroupTab tab,
@@ -332,19 +283,22 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     if (size == 1) {
         sa[c + o] = i;
     } else {
-        uint64_t p = gsc[g];
-        uint32_t ng = (uint32_t)p, cs = (uint32_t)(p >> 32);
-        uint32_t idx = cs + ((uint32_t)c - hp);
+        // compact index = survivor entries before c, new group id = survivor heads up to c - 1
+        uint64_t se, sh;
+        surv_masks(hb, c >> 6, m, se, sh);
+        const uint64_t pw = P[c >> 6], below = (1ull << (c & 63u)) - 1ull;
+        const uint32_t idx = (uint32_t)(pw >> 32) + (uint32_t)__popcll(se & below);
+        const uint32_t ng = (uint32_t)pw + (uint32_t)__popcll(sh & (below | (below + 1ull))) - 1u;
         nval[idx] = i;
         ngid[idx] = ng;
-        if ((uint32_t)c == hp) {
-            off_new[ng] = hp + o - cs;
-            tab.ginfo[ng] = ((uint64_t)size << 32) | cs;
-            if (size > kSmall) {
-                const uint64_t l = lsc[g];
+        if ((uint32_t)c == hp) {  // (idx is the group's compact start)
+            off_new[ng] = hp + o - idx;
+            tab.ginfo[ng] = ((uint64_t)size << 32) | idx;
+            if (size > kSmall) {  // large-group id and extraction range (any order serves)
+                const uint64_t l = atomicAdd(lcount, ((unsigned long long)size << 32) | 1ull);
                 const uint32_t lg = (uint32_t)l;
                 tab.gl[ng] = lg;
-                tab.lrec[lg] = (l & 0xffffffff00000000ull) | cs;
+                tab.lrec[lg] = (l & 0xffffffff00000000ull) | idx;
                 tab.lg2g[lg] = ng;
             }
         }
@@ -797,20 +751,6 @@ __global__ void k_dbg_heads(HeadBits hb, const uint32_t *__restrict__ headpos, u
         atomicOr(err, 0x4000u);
 }
 
-__global__ void k_dbg_gsc(const uint32_t *__restrict__ headpos, const uint64_t *__restrict__ gsc,
-                          uint32_t G, uint64_t total, uint32_t *err)
-{
-    size_t g = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (g >= G)
-        return;
-    const uint32_t size = headpos[g + 1] - headpos[g];
-    const uint64_t want = size >= 2 ? (((uint64_t)size << 32) | 1ull) : 0ull;
-    const uint64_t nv = gsc[g + 1];  // in bounds: the scan arrays hold n + 2 entries
-    const uint64_t nxt = g + 1 < G ? nv : total;
-    if (nxt - gsc[g] != want)
-        atomicOr(err, 0x8000u);
-}
-
 // Members of large groups -> contiguous extracted array, key (large-group id, rank).
 __global__ void k_extract(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
                           const uint64_t *__restrict__ ginfo, const uint32_t *__restrict__ gl,
@@ -884,7 +824,6 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     uint32_t *headpos = ws.u2, *ngid = ws.u3;
     const size_t nw_max = ((size_t)n + 63) / 64;  // head ballots of up to n list entries, in u0
     HeadBits hb{reinterpret_cast<uint64_t *>(ws.u0), ws.u0 + 2 * nw_max, ws.u0 + 3 * nw_max};
-    uint64_t *gsc = ws.g64;
     uint32_t *d32 = reinterpret_cast<uint32_t *>(ws.dscal);
     uint64_t *d64 = ws.dscal + 8;
     uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
@@ -1101,26 +1040,17 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             SALZ_LAUNCH_CHECK();
         }
 
+        // Survivor counts per wave of the list (u1: free once round 0's text pass is done; u0
+        // holds the head ballots until k_commit), scanned: d64[0] = survivors << 32 | groups.
+        // d64[1] counts the large groups (size << 32 | 1 per group, k_commit's atomics).
+        uint64_t *P = reinterpret_cast<uint64_t *>(ws.u1);
         {
-            // per-wave group sums in u1 (u0 holds the head ballots until k_commit)
-            uint64_t *wg = reinterpret_cast<uint64_t *>(ws.u1), *wl = wg + nw_max;
-            const uint32_t nwg = (uint32_t)(((uint64_t)(need_G ? G : m) + 63) / 64);
-            const unsigned ggrid = grid_for((size_t)nwg * 64, kT);  // one wave per 64 groups
-            hipLaunchKernelGGL(k_grpsum, dim3(ggrid), dim3(kT), 0, st, headpos, d32 + 0, nwg, wg, wl);
+            const size_t nw = ((size_t)m + 63) / 64;
+            hipLaunchKernelGGL(k_surv, dim3(grid_for(nw, kT)), dim3(kT), 0, st, hb, m, P);
             SALZ_LAUNCH_CHECK();
-            if (scan_sum_u64(wg, wg, nwg, false, d64, ws, st) != 0)
+            if (scan_sum_u64(P, P, nw, false, d64, ws, st) != 0)
                 return -1;
-            if (scan_sum_u64(wl, wl, nwg, false, d64 + 1, ws, st) != 0)
-                return -1;
-            hipLaunchKernelGGL(k_grpscan, dim3(ggrid), dim3(kT), 0, st, headpos, d32 + 0, nwg, wg,
-                               wl, gsc, ws.lsc, dbg_rounds ? 1 : 0);
-            SALZ_LAUNCH_CHECK();
-        }
-        if (dbg_rounds) {
-            if (read_scalars(ws, 0, 256, "sa.dbg") != 0)
-                return -1;
-            hipLaunchKernelGGL(k_dbg_gsc, dim3(grid_for(G, kT)), dim3(kT), 0, st, headpos, gsc, G, ws.hscal[8], derr);
-            SALZ_LAUNCH_CHECK();
+            SALZ_HIP(hipMemsetAsync(d64 + 1, 0, sizeof(uint64_t), st));
         }
         // Rank updates (SALZ_RANK_MODE=direct|split|stage for experiments):
         //   direct  k_commit writes rank[i] (small rounds);
@@ -1142,7 +1072,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         uint32_t *later = reinterpret_cast<uint32_t *>(Kx);  // free until k_keys
         const uint32_t ihi = mode == 0 ? 0xffffffffu : mode == 1 ? span : 0u;
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, headpos,
-                           gsc, ws.lsc, offo, offn, Vx, ngid, ws.rank, ws.sa, tab, m, n, nsa, kb_old,
+                           P, reinterpret_cast<unsigned long long *>(d64 + 1), offo, offn, Vx, ngid, ws.rank,
+                           ws.sa, tab, m, n, nsa, kb_old,
                            round0, derr, ihi, mode ? later : nullptr, dist ? dist->gbase : 0u);
         SALZ_LAUNCH_CHECK();
         for (uint32_t q = 1; q < parts; q++) {
