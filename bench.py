@@ -314,7 +314,8 @@ def main():
     # Roofline of the dominant kernel (radix scatter): algorithmic bytes / event-timed duration.
     launches = max(int(st["radix_scatter_launches"]), 1)
     ms_rx = float(st["ms_radix_scatter"])
-    bytes_rx = RADIX_BYTES_PER_ELEM * float(st["radix_scatter_elems"])
+    # (24 B per element, + 1 B where a pass also writes the next pass's digit byte, radix.hip)
+    bytes_rx = float(st.get("radix_scatter_bytes") or RADIX_BYTES_PER_ELEM * float(st["radix_scatter_elems"]))
     achieved = bytes_rx / (ms_rx * 1e-3) / 1e9 if ms_rx > 0 else 0.0
     # HBM traffic of the same kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
     # command (tools/pmc_traffic.py -> bench_traffic.json), when they were taken on this workload.

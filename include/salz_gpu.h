@@ -131,6 +131,8 @@ typedef struct {
     double ms_radix_scatter;
     uint64_t radix_scatter_elems;
     int32_t sa_dc3_levels; /* > 0: the suffix array came from the DC3 sorter (repetitive block) */
+    uint64_t radix_scatter_bytes; /* algorithmic bytes of the timed scatter launches (24 per element,
+                                     + 1 where the next pass's digit byte is written) */
 } salz_gpu_stats;
 
 /* Per-stage HIP-event timing of subsequent calls (small overhead when on). */

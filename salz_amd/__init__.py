@@ -133,7 +133,8 @@ class Stats(ctypes.Structure):
                 ("lcp_long_bytes", ctypes.c_uint64), ("emit_bits", ctypes.c_uint64),
                 ("emit_bytes", ctypes.c_uint64), ("exit_nodes", ctypes.c_uint32),
                 ("radix_scatter_launches", ctypes.c_uint32), ("ms_radix_scatter", ctypes.c_double),
-                ("radix_scatter_elems", ctypes.c_uint64), ("sa_dc3_levels", ctypes.c_int32)]
+                ("radix_scatter_elems", ctypes.c_uint64), ("sa_dc3_levels", ctypes.c_int32),
+                ("radix_scatter_bytes", ctypes.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -25,6 +25,7 @@ struct StageStats {
     float ms_radix_scatter;   // summed over every radix scatter launch (HIP events)
     uint32_t radix_scatter_launches;
     uint64_t radix_scatter_elems;
+    uint64_t radix_scatter_bytes;
     uint64_t emit_bits, emit_bytes;
 };
 

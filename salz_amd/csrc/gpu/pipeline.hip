@@ -742,6 +742,7 @@ int salz_gpu_get_stats(const salz_gpu_ctx *ctx, salz_gpu_stats *o)
     o->ms_radix_scatter = s.ms_radix_scatter;
     o->radix_scatter_elems = s.radix_scatter_elems;
     o->sa_dc3_levels = s.sa_dc3_levels;
+    o->radix_scatter_bytes = s.radix_scatter_bytes;
     return 0;
 }
 

@@ -415,6 +415,7 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
             ws.rx_used += 2;
             ws.stats.radix_scatter_launches++;
             ws.stats.radix_scatter_elems += m;
+            ws.stats.radix_scatter_bytes += (uint64_t)m * (dig_out ? 25u : 24u);
         }
         uint64_t *tk = kin;
         kin = kout;

@@ -11,8 +11,9 @@ traffic = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 per dispatch. Reads narrower
 ratio to the algorithmic bytes as the signal.
 
 Algorithmic bytes of k_radix_scatter: 24 B per element (read 8 B key + 4 B value, write
-8 B key + 4 B value); elements per dispatch = Grid_Size / 256 * 4096 (4096-element tiles,
-the last tile may be partial, so this is an upper bound within one tile).
+8 B key + 4 B value; passes followed by another key pass also write the next digit byte, 25 B,
+which bench.py counts exactly); elements per dispatch = Grid_Size / 256 * 4096 (4096-element
+tiles, the last tile may be partial, so this is an upper bound within one tile).
 """
 import argparse
 import collections
