@@ -128,11 +128,12 @@ constexpr int kRadixTile = 4096;
 // every live suffix of `blocks`; *keys / *vals are not read); a batch of several blocks then
 // gets extra passes on the block of each value, so the result is ordered by (block, key).
 // With `digits` (m bytes of scratch) every scatter pass also writes the next pass's digit of
-// each key at its output position, and the next histogram reads those bytes instead of the keys.
+// each key at its output position, and the next histogram reads those bytes instead of the keys
+// (digits_ready: the caller wrote the first pass's digits as well).
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
                      const uint8_t *text = nullptr, const Blocks *blocks = nullptr,
-                     const Alpha *alpha = nullptr, uint8_t *digits = nullptr);
+                     const Alpha *alpha = nullptr, uint8_t *digits = nullptr, bool digits_ready = false);
 
 // Blocks per batch (one pipeline pass over several blocks, common.hpp Blocks).
 constexpr uint32_t kMaxBatchBlocks = 4096;

@@ -354,7 +354,8 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
 
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
-                     const uint8_t *text, const Blocks *blocks, const Alpha *alpha, uint8_t *digits)
+                     const uint8_t *text, const Blocks *blocks, const Alpha *alpha, uint8_t *digits,
+                     bool digits_ready)
 {
     if (m <= 1 || bit_hi <= bit_lo)
         return 0;
@@ -376,7 +377,7 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
         const int shift = mode == 2 ? 8 * (pass - passes_key) : bit_lo + 8 * pass;
         TextSrc txt{text, g, Alpha{}};
         // digit bytes: written by a key pass for the next key pass, read by that pass's histogram
-        const uint8_t *dig_in = digits && pass > 0 && mode == 0 ? digits : nullptr;
+        const uint8_t *dig_in = digits && (pass > 0 || digits_ready) && mode == 0 ? digits : nullptr;
         uint8_t *dig_out = digits && pass + 1 < passes_key ? digits : nullptr;
         const int nshift = bit_lo + 8 * (pass + 1);
         if (alpha)

@@ -49,15 +49,21 @@ constexpr uint32_t kSegCap = 4096;   // LDS slots: a window's groups span < kSeg
 constexpr int kSegThreads = 256;
 static_assert(kSegCap == 4096, "12-bit slot index in the LDS sort key");
 
-__global__ void k_sa_init(const uint8_t *__restrict__ T, Blocks g, Alpha a, uint64_t *__restrict__ key,
-                          uint32_t *__restrict__ val)
+// Round 0's (key, value) list in init_suffix order. Tm: the text mapped to symbols (alphabet
+// keys), else the raw text is read. dig: the first radix pass's digit of every key (its low
+// byte), so that pass's histogram reads bytes (radix.hip).
+__global__ void k_sa_init(const uint8_t *__restrict__ T, const uint8_t *__restrict__ Tm, Blocks g, Alpha a,
+                          uint64_t *__restrict__ key, uint32_t *__restrict__ val, uint8_t *__restrict__ dig)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= g.nsa())
         return;
     const uint32_t i = init_suffix(c, g);
-    key[c] = round0_key(T, i, g.end(i), a);
+    const uint64_t k = Tm ? round0_key_mapped(Tm, i, g.end(i), a) : round0_key(T, i, g.end(i), a);
+    key[c] = k;
     val[c] = i;
+    if (dig)
+        dig[c] = (uint8_t)k;
 }
 
 // Round-0 pairs of a split block's own suffixes (list order: short ones first, shortest first,
@@ -239,11 +245,10 @@ __global__ __launch_bounds__(kT) void k_surv(HeadBits hb, uint32_t m, uint64_t *
     P[w] = ((uint64_t)__popcll(se) << 32) | (uint64_t)__popcll(sh);
 }
 
-// Next round's group table (ginfo: size << 32 | compact start, gl: large-group id) is
-// written by each surviving group's head; large groups also get their extraction record.
+// Next round's group table (ginfo: size << 32 | compact start) is written by each surviving
+// group's head; large groups also get their extraction record.
 struct GroupTab {
     uint64_t *ginfo;
-    uint32_t *gl;
     uint64_t *lrec;
     uint32_t *lg2g;
 };
@@ -297,7 +302,6 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
             if (size > kSmall) {  // large-group id and extraction range (any order serves)
                 const uint64_t l = atomicAdd(lcount, ((unsigned long long)size << 32) | 1ull);
                 const uint32_t lg = (uint32_t)l;
-                tab.gl[ng] = lg;
                 tab.lrec[lg] = (l & 0xffffffff00000000ull) | idx;
                 tab.lg2g[lg] = ng;
             }
@@ -751,26 +755,46 @@ __global__ void k_dbg_heads(HeadBits hb, const uint32_t *__restrict__ headpos, u
         atomicOr(err, 0x4000u);
 }
 
-// Members of large groups -> contiguous extracted array, key (large-group id, rank).
-__global__ void k_extract(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
-                          const uint64_t *__restrict__ ginfo, const uint32_t *__restrict__ gl,
-                          const uint64_t *__restrict__ lrec, uint32_t m, uint32_t mL, int kb,
-                          uint64_t *__restrict__ KC, uint32_t *__restrict__ VC, uint32_t *err)
+// Members of large groups -> contiguous extracted array, key (large-group id, rank). Large
+// group lg owns extracted range [lrec[lg] >> 32, + size) (the ranges follow lg: one atomic
+// handed out both); k_tile_lg finds the group holding each 256-entry tile's first entry (a
+// binary search over GL ranges), and since a large group outlasts a tile, an entry of the tile
+// belongs to that group or the next. So only the mL extracted entries are visited.
+__global__ void k_tile_lg(const uint64_t *__restrict__ lrec, uint32_t GL, uint32_t mL, uint32_t *__restrict__ tmap)
 {
-    size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (c >= m)
+    const size_t t = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (t * kT >= mL)
         return;
-    const uint64_t key = K[c];
-    const uint32_t g = (uint32_t)(key >> kb);
-    const uint64_t gi = ginfo[g];
-    if ((uint32_t)(gi >> 32) <= kSmall)
+    const uint64_t x0 = t * kT;
+    uint32_t lo = 0, hi = GL - 1u;  // the last group whose range starts at or before x0
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1u) >> 1;
+        if ((lrec[mid] >> 32) <= x0)
+            lo = mid;
+        else
+            hi = mid - 1u;
+    }
+    tmap[t] = lo;
+}
+
+__global__ void k_extract(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
+                          const uint64_t *__restrict__ lrec, const uint32_t *__restrict__ tmap,
+                          uint32_t GL, uint32_t m, uint32_t mL, int kb, uint64_t *__restrict__ KC,
+                          uint32_t *__restrict__ VC, uint32_t *err)
+{
+    const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (x >= mL)
         return;
-    const uint32_t lg = gl[g];
-    const uint32_t dst = (uint32_t)(lrec[lg] >> 32) + ((uint32_t)c - (uint32_t)gi);
-    if (bad_index(dst >= mL, err, kErrExtract))
+    const uint32_t lg0 = tmap[blockIdx.x];
+    const uint64_t r0 = lrec[lg0], r1 = lrec[lg0 + 1u < GL ? lg0 + 1u : lg0];  // unconditional loads
+    const bool next = lg0 + 1u < GL && x >= (r1 >> 32);
+    const uint32_t lg = next ? lg0 + 1u : lg0;
+    const uint64_t r = next ? r1 : r0;
+    const uint32_t orig = (uint32_t)r + (uint32_t)(x - (r >> 32));
+    if (bad_index(orig >= m, err, kErrExtract))
         return;
-    KC[dst] = ((uint64_t)lg << kb) | (key & ((1ull << kb) - 1ull));
-    VC[dst] = V[c];
+    KC[x] = ((uint64_t)lg << kb) | (K[orig] & ((1ull << kb) - 1ull));
+    VC[x] = V[orig];
 }
 
 // Sorted large groups back to their places in the active list, original key format.
@@ -835,8 +859,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // extracted large groups live in pst (keys) and cand (values), the group table in cand.
     uint8_t *cb = reinterpret_cast<uint8_t *>(ws.cand);
     uint32_t *VC = reinterpret_cast<uint32_t *>(cb);
-    GroupTab tab{reinterpret_cast<uint64_t *>(cb + 4 * ws.cap_s),
-                 reinterpret_cast<uint32_t *>(cb + 12 * ws.cap_s), ws.lrec, ws.lg2g};
+    GroupTab tab{reinterpret_cast<uint64_t *>(cb + 4 * ws.cap_s), ws.lrec, ws.lg2g};
     uint64_t *KC = ws.pst;
 
     static const bool dbg_rounds = getenv("SALZ_CHECK_ROUNDS") != nullptr;
@@ -910,13 +933,21 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // Round 0's first radix pass reads the text itself (radix.hip, TextSrc); the initial
     // key/value arrays are only materialised for the per-round checks, and for n = 1 (the
     // sort has nothing to do and would leave them unwritten).
-    const bool text_first = !dbg_rounds && nsa > 1 && !dist;
+    // SALZ_TEXT_FIRST=0: a single block's list is materialised (k_sa_init, with the first
+    // pass's digit bytes) and every pass reads it
+    const bool text_src_env = !getenv("SALZ_TEXT_FIRST") || atoi(getenv("SALZ_TEXT_FIRST")) != 0;
+    const bool text_first = !dbg_rounds && nsa > 1 && !dist && (bl.nb > 1 || text_src_env);
+    // Digit bytes of the radix passes (radix.hip) in u2, free during every sort (the head
+    // positions are written after it); SALZ_RADIX_DIGITS=0: histograms read the keys
+    uint8_t *rdig = getenv("SALZ_RADIX_DIGITS") && atoi(getenv("SALZ_RADIX_DIGITS")) == 0
+                        ? nullptr : reinterpret_cast<uint8_t *>(ws.u2);
     if (dist) {
         hipLaunchKernelGGL(k_list_init, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.text, dist->list, nsa, n, alpha,
                            K, V);
         SALZ_LAUNCH_CHECK();
     } else if (!text_first) {
-        hipLaunchKernelGGL(k_sa_init, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.text, bl, alpha, K, V);
+        hipLaunchKernelGGL(k_sa_init, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.text, tmapped, bl, alpha, K, V,
+                           rdig);
         SALZ_LAUNCH_CHECK();
     }
     if (dbg_rounds && bl.nb == 1 && !dist) {
@@ -941,10 +972,6 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // k_seg_small windows whose groups all have at most seg_tiny members are ordered by counting
     // (SALZ_SEG_TINY=0: LSD passes everywhere)
     const uint32_t seg_tiny = getenv("SALZ_SEG_TINY") ? (uint32_t)atoi(getenv("SALZ_SEG_TINY")) : 32u;
-    // Digit bytes of the radix passes (radix.hip) in u2, free during every sort (the head
-    // positions are written after it); SALZ_RADIX_DIGITS=0: histograms read the keys
-    uint8_t *rdig = getenv("SALZ_RADIX_DIGITS") && atoi(getenv("SALZ_RADIX_DIGITS")) == 0
-                        ? nullptr : reinterpret_cast<uint8_t *>(ws.u2);
     auto t_round = std::chrono::steady_clock::now();
     for (;;) {
         ws.stats.sa_rounds++;
@@ -960,7 +987,9 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             }
             const int key_bits = alpha.bits ? (int)(alpha.k * alpha.bits) : 64;
             const uint8_t *src_text = !text_first ? nullptr : tmapped ? tmapped : ws.text;
-            if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, key_bits, ws, st, src_text, &bl, &alpha, rdig) != 0)
+            // (materialised list: k_sa_init wrote the first pass's digits too)
+            if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, key_bits, ws, st, src_text, &bl, &alpha, rdig,
+                                 !text_first && !dist && rdig) != 0)
                 return -1;
         } else {
             // Global sort of every active suffix on (group, rank) vs. LDS sort of the small
@@ -991,8 +1020,12 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                                    kb, seg_tiny, derr);
                 SALZ_LAUNCH_CHECK();
                 if (mL) {
-                    hipLaunchKernelGGL(k_extract, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V,
-                                       tab.ginfo, tab.gl, tab.lrec, m, mL, kb, KC, VC, derr);
+                    uint32_t *tmap = pw + 4 * nwin;  // (lsc, after the window plan)
+                    const uint32_t ntile = grid_for(mL, kT);
+                    hipLaunchKernelGGL(k_tile_lg, dim3(grid_for(ntile, kT)), dim3(kT), 0, st, tab.lrec, GL, mL, tmap);
+                    SALZ_LAUNCH_CHECK();
+                    hipLaunchKernelGGL(k_extract, dim3(ntile), dim3(kT), 0, st, K, V, tab.lrec, tmap, GL, m, mL, kb,
+                                       KC, VC, derr);
                     SALZ_LAUNCH_CHECK();
                     uint64_t *KS = KC;
                     uint32_t *VS = VC;
