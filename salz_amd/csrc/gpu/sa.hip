@@ -315,7 +315,7 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
 //   round 0 (8-byte keys):   LCP = leading equal bytes of the two keys, capped by both lengths;
 //   round t (keys compare rank[i + hk] within groups sharing hk bytes): LCP = hk + the equal
 //   bytes of T[i + hk ..] and T[j + hk ..], fewer than hk. Up to kLcpLane bytes one lane
-//   compares; longer compares take the whole wave, 512 bytes per step, one head at a time.
+//   compares; longer compares take 8 lanes each, 128 bytes per step, 8 heads at a time.
 // The host stops (and the PLCP stage takes over, lcp.hip) once hk exceeds kLcpMaxHk.
 constexpr uint32_t kLcpLane = 256;
 constexpr uint32_t kLcpMaxHk = 4096;
@@ -375,28 +375,42 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
             }
         }
     }
+    // Long compares: eight heads at a time, one per 8-lane group of the wave, 16 bytes per lane
+    // and 128 per group and step (a head's compare is bounded by the LCP, so most end in the
+    // first steps: the serial memory latencies per wave drop from one per head to about one per
+    // eight). Loads past a head's limit read its first bytes again (every load unconditional).
     uint64_t pend = wave_ballot(need);
-    const uint32_t lane = lane_id();
+    const uint32_t lane = lane_id(), sub = lane >> 3, sl8 = lane & 7u;
     while (pend) {
-        const int src = (int)__ffsll((unsigned long long)pend) - 1;
-        pend &= pend - 1;
+        uint64_t pk = pend;  // group `sub` takes the sub-th pending head in lane order
+        for (uint32_t u = 0; u < sub; u++)
+            pk &= pk - 1;
+        const bool have = pk != 0;
+        const int src = have ? (int)__ffsll((unsigned long long)pk) - 1 : 0;
+        for (uint32_t u = 0; u < 8; u++)
+            pend &= pend - 1;
         const uint32_t si = shfl_u32(i, src) + hk, sj = shfl_u32(j, src) + hk;
-        const uint32_t sl = shfl_u32(lim, src), sp = shfl_u32(pos, src);
-        uint32_t mis = sl;
-        for (uint32_t base = 0; base < sl; base += 64 * 8) {
-            const uint32_t off = base + lane * 8;
+        const uint32_t slv = shfl_u32(lim, src), sp = shfl_u32(pos, src);
+        const uint32_t sl = have ? slv : 0u;
+        uint32_t mis = 0xffffffffu;  // the group's first mismatch offset
+        for (uint32_t base = 0;; base += 8 * 16) {
+            const uint32_t off = base + sl8 * 16, offc = off < sl ? off : 0u;
+            const uint64_t x0 = load_u64_any(T, (size_t)si + offc) ^ load_u64_any(T, (size_t)sj + offc);
+            const uint64_t x1 = load_u64_any(T, (size_t)si + offc + 8) ^ load_u64_any(T, (size_t)sj + offc + 8);
             uint32_t mm = 0xffffffffu;
-            const uint64_t x = load_u64_any(T, (size_t)si + off) ^ load_u64_any(T, (size_t)sj + off);
-            if (off < sl && x)
-                mm = off + ((uint32_t)__builtin_ctzll(x) >> 3);
-            mm = wave_min_u32(mm);
-            if (mm != 0xffffffffu) {
-                mis = umin_(mm, sl);
+            if (off < sl && (x0 | x1))
+                mm = x0 ? off + ((uint32_t)__builtin_ctzll(x0) >> 3) : off + 8u + ((uint32_t)__builtin_ctzll(x1) >> 3);
+            mm = umin_(mm, shfl_xor_u32(mm, 1));
+            mm = umin_(mm, shfl_xor_u32(mm, 2));
+            mm = umin_(mm, shfl_xor_u32(mm, 4));
+            if (mis == 0xffffffffu)
+                mis = mm;
+            const bool done = mis != 0xffffffffu || base + 8 * 16 >= sl;
+            if (!wave_ballot(!done))
                 break;
-            }
         }
-        if ((int)lane == src)
-            lcps[sp] = hk + mis;
+        if (have && sl8 == 0)
+            lcps[sp] = hk + umin_(mis, sl);
     }
 }
 
