@@ -317,7 +317,7 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
 //   bytes of T[i + hk ..] and T[j + hk ..], fewer than hk. Up to kLcpLane bytes one lane
 //   compares; longer compares take 8 lanes each, 128 bytes per step, 8 heads at a time.
 // The host stops (and the PLCP stage takes over, lcp.hip) once hk exceeds kLcpMaxHk.
-constexpr uint32_t kLcpLane = 256;
+constexpr uint32_t kLcpLane = 32;
 constexpr uint32_t kLcpMaxHk = 4096;
 
 // k_heads with the LCP of every new head (writes the head ballots like k_heads).
