@@ -623,8 +623,10 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
     const uint64_t mask = (1ull << kb) - 1ull;
     const int nbits = kb + (32 - __builtin_clz((g1 - g0) | 1u));
 
-    // slots actually sorted: count rounded up to 1024 (4 waves x 64 lanes x ITEMS / 4 steps)
-    const int items = (int)((count + 1023u) / 1024u) * 4;
+    // slots actually sorted: count rounded up to 256 (4 waves x 64 lanes x ITEMS), at least 1024
+    // (a window's owned span is about 2048 entries, so windows a little over it sort 2304 or 2560
+    // slots, not 3072)
+    const int items = count <= 1024u ? 4 : (int)((count + 255u) / 256u);
     for (uint32_t i = tid; i < (uint32_t)items * kSegThreads; i += kSegThreads) {
         uint64_t key = ~0ull;  // padding sorts last in every digit
         if (i < count) {
@@ -680,8 +682,17 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
     }
     switch (items) {
     case 4: seg_lsd<4>(sk, cnt, wsum, nbits); break;
+    case 5: seg_lsd<5>(sk, cnt, wsum, nbits); break;
+    case 6: seg_lsd<6>(sk, cnt, wsum, nbits); break;
+    case 7: seg_lsd<7>(sk, cnt, wsum, nbits); break;
     case 8: seg_lsd<8>(sk, cnt, wsum, nbits); break;
+    case 9: seg_lsd<9>(sk, cnt, wsum, nbits); break;
+    case 10: seg_lsd<10>(sk, cnt, wsum, nbits); break;
+    case 11: seg_lsd<11>(sk, cnt, wsum, nbits); break;
     case 12: seg_lsd<12>(sk, cnt, wsum, nbits); break;
+    case 13: seg_lsd<13>(sk, cnt, wsum, nbits); break;
+    case 14: seg_lsd<14>(sk, cnt, wsum, nbits); break;
+    case 15: seg_lsd<15>(sk, cnt, wsum, nbits); break;
     default: seg_lsd<16>(sk, cnt, wsum, nbits); break;
     }
 
