@@ -89,9 +89,21 @@ __global__ void k_map_text(const uint8_t *__restrict__ T, size_t P, Alpha a, uin
     load_codes(code, a);
     __syncthreads();
     for (size_t i = ((size_t)blockIdx.x * kT + threadIdx.x) * 16; i < P + 64; i += (size_t)gridDim.x * kT * 16) {
+        // 16 bytes per thread in one load and one store (the text buffer is padded past P + 64)
+        const uint4 x = *reinterpret_cast<const uint4 *>(T + i);
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+        uint32_t o[4];
 #pragma unroll
-        for (int j = 0; j < 16; j++)
-            Tm[i + j] = i + j < P ? code[T[i + j]] : 0u;
+        for (int q = 0; q < 4; q++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const size_t at = i + 4 * q + b;
+                v |= (at < P ? (uint32_t)code[(w[q] >> (8 * b)) & 255u] : 0u) << (8 * b);
+            }
+            o[q] = v;
+        }
+        *reinterpret_cast<uint4 *>(Tm + i) = make_uint4(o[0], o[1], o[2], o[3]);
     }
 }
 
@@ -102,10 +114,16 @@ __global__ void k_alpha_presence(const uint8_t *__restrict__ T, size_t P, uint32
     if (threadIdx.x < 8)
         w[threadIdx.x] = 0;
     __syncthreads();
-    for (size_t i = (size_t)blockIdx.x * kT + threadIdx.x; i < P; i += (size_t)gridDim.x * kT) {
-        const uint32_t c = T[i];
-        if (!(w[c >> 5] & (1u << (c & 31))))
-            atomicOr(&w[c >> 5], 1u << (c & 31));
+    // 16 bytes per thread and step (one load); bits already present are not written again
+    for (size_t i = ((size_t)blockIdx.x * kT + threadIdx.x) * 16; i < P; i += (size_t)gridDim.x * kT * 16) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(T + i);  // (padded buffer)
+        const uint32_t v[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            const uint32_t c = (v[b >> 2] >> (8 * (b & 3))) & 255u;
+            if (i + b < P && !(w[c >> 5] & (1u << (c & 31))))
+                atomicOr(&w[c >> 5], 1u << (c & 31));
+        }
     }
     __syncthreads();
     if (threadIdx.x < 8 && w[threadIdx.x])
