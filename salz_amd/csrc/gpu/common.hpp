@@ -207,6 +207,8 @@ struct Blocks {
 // List entry c -> its suffix. (One block: c < s -> n - 1 - c, else c - s.)
 __host__ __device__ __forceinline__ uint32_t init_suffix(size_t c, const Blocks &g)
 {
+    if (g.nb == 1 && g.npos >= 7)  // (one block: the 7 short suffixes, then text order)
+        return c < 7 ? g.npos - 1u - (uint32_t)c : (uint32_t)c - 7u;
     const uint32_t nl = g.n_last();
     const uint32_t full = g.nb - 1u;  // blocks with n_b = bs - 8 >= 7
     uint32_t cc = (uint32_t)c;
@@ -297,10 +299,13 @@ __device__ __forceinline__ uint64_t round0_key_mapped(const uint8_t *Tm, uint32_
         uint64_t w = load_u64_any(Tm, i);
         if (left < 8)
             w &= (1ull << (8u * left)) - 1ull;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++)
-            key = (key << a.bits) | ((w >> (8 * j)) & 255u);
-        return key;
+        // 8 symbols of `bits` bits (first symbol most significant), packed pairwise: byte pairs,
+        // then 16-bit pairs, then the two halves (three mask-shift-or steps, not eight)
+        const uint32_t b = a.bits;
+        uint64_t x = __builtin_bswap64(w);
+        x = (x & 0x00FF00FF00FF00FFull) | (((x >> 8) & 0x00FF00FF00FF00FFull) << b);
+        x = (x & 0x0000FFFF0000FFFFull) | (((x >> 16) & 0x0000FFFF0000FFFFull) << (2 * b));
+        return (x & 0xFFFFFFFFull) | ((x >> 32) << (4 * b));
     }
     for (uint32_t j0 = 0; j0 < a.k; j0 += 8) {
         uint64_t w = load_u64_any(Tm, (size_t)i + j0);
