@@ -233,7 +233,7 @@ def test_encode_blocks_container(salz, block, size):
     assert salz.decode_blocks(got, size) == src.tobytes()
 
 
-@pytest.mark.parametrize("keys", ["1", "0", "1d0", "1t0"])
+@pytest.mark.parametrize("keys", ["1", "0", "1d0", "1t0", "1s0", "1s2048"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
                                                ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
@@ -245,11 +245,16 @@ def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
     default for texts of <= 127 distinct bytes: 2 to 32 symbols per key) or raw bytes, give the
     unique suffix array; the radix histograms from the digit bytes (the default) or from the
     keys ("1d0", SALZ_RADIX_DIGITS=0); round 0's first pass from the text (the default) or from
-    the materialised list ("1t0", SALZ_TEXT_FIRST=0)."""
+    the materialised list ("1t0", SALZ_TEXT_FIRST=0); LDS windows placed by counting up to the
+    default group size, never ("1s0") or always ("1s2048", SALZ_SEG_TINY)."""
     monkeypatch.setenv("SALZ_SA_MODE", mode)
     monkeypatch.setenv("SALZ_ALPHA", keys[0])
     monkeypatch.setenv("SALZ_RADIX_DIGITS", "0" if keys == "1d0" else "1")
     monkeypatch.setenv("SALZ_TEXT_FIRST", "0" if keys == "1t0" else "1")
+    if keys.startswith("1s"):
+        monkeypatch.setenv("SALZ_SEG_TINY", keys[2:])
+    else:
+        monkeypatch.delenv("SALZ_SEG_TINY", raising=False)
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
     o = oracle_stages(src)
