@@ -222,17 +222,35 @@ __device__ __forceinline__ uint32_t gid1(const HeadBits &hb, size_t c, uint32_t 
 }
 
 // Head position per group (plus the sentinel headpos[G] = m).
+// A wave takes kHpWords words of the list (lane l: entry 64 w + l of each), so a quarter of the
+// waves per launch; every word's loads are issued before its stores.
+constexpr uint32_t kHpWords = 4;
 __global__ void k_headpos(HeadBits hb, uint32_t m, uint32_t *__restrict__ headpos)
 {
-    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (c >= m)
-        return;
-    uint32_t bit;
-    const uint32_t g = gid1(hb, c, bit);
-    if (bit)
-        headpos[g - 1u] = (uint32_t)c;
-    if (c == m - 1)
-        headpos[g] = m;
+    const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
+    const size_t w0 = (x >> 6) * kHpWords;
+    const uint32_t lane = (uint32_t)(x & 63u);
+    const size_t nw = ((size_t)m + 63) / 64;
+    uint64_t mk[kHpWords];
+    uint32_t pre[kHpWords];
+#pragma unroll
+    for (uint32_t k = 0; k < kHpWords; k++) {  // unconditional loads (clamped word)
+        const size_t w = w0 + k < nw ? w0 + k : nw - 1;
+        mk[k] = hb.hmask[w];
+        pre[k] = hb.wpre[w];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kHpWords; k++) {
+        const size_t c = (w0 + k) * 64 + lane;
+        if (c >= m)
+            break;
+        const uint32_t bit = (uint32_t)(mk[k] >> lane) & 1u;
+        const uint32_t g = pre[k] + (uint32_t)__popcll(mk[k] & ((1ull << lane) - 1ull)) + bit;
+        if (bit)
+            headpos[g - 1u] = (uint32_t)c;
+        if (c == m - 1)
+            headpos[g] = m;
+    }
 }
 
 // Survivor masks of wave word w of the list (entries 64w .. 64w + 63): entry c is in a
@@ -1102,7 +1120,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u32(hb.wcnt, hb.wpre, ((size_t)m + 63) / 64, false, d32 + 0, ws, st) != 0)
             return -1;
-        hipLaunchKernelGGL(k_headpos, dim3(grid_for(m, kT)), dim3(kT), 0, st, hb, m, headpos);
+        hipLaunchKernelGGL(k_headpos, dim3(grid_for(((size_t)m + 64 * kHpWords - 1) / (64 * kHpWords) * 64, kT)),
+                           dim3(kT), 0, st, hb, m, headpos);
         SALZ_LAUNCH_CHECK();
         // The host needs G only for the debug checks; no round waits for it.
         const bool need_G = dbg_rounds || verbose;
