@@ -14,16 +14,25 @@ Other BASELINE configs (--workload):
   fib256   configs[4]: the 268,435,456-byte Fibonacci word as one block per GPU
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload enwik8|enwik9|silesia|fib256]
-  (N > 1: launched by torch.distributed.run, one rank per GPU; weak scaling for the one-block
-   workloads, strong for the sharded ones. A step is encode + the exchange step of
-   salz_amd/dist.py: RCCL all-gather of each rank's packed frame bytes, then every rank's run of
-   frames straight into rank 0's container in HBM over xGMI (point-to-point). No collective
-   touches the encode itself.)
+                  [--dist-backend nccl|gloo] [--launch] [--no-pmc]
+  N > 1: one rank per GPU. Under an outside launcher (torch.distributed.run sets WORLD_SIZE)
+  this process is one rank; otherwise it starts `python -m torch.distributed.run
+  --nproc-per-node N bench.py ...` as a child process (before it touches any GPU), relays rank
+  0's JSON line and exits non-zero when the line's n_gpus differs from N. Weak scaling for the
+  one-block workloads, strong for the sharded ones. A step is encode + the exchange step of
+  salz_amd/dist.py: RCCL all-gather of each rank's packed frame bytes, then every rank's run of
+  frames straight into rank 0's container in HBM over xGMI (point-to-point). No collective
+  touches the encode itself. --dist-backend gloo runs the same launch, shard and exchange code
+  with the payload staged through host memory, so several ranks can share one GPU (rehearsal on
+  a one-GPU box); --launch goes through the launcher at N = 1 too (the RCCL path at world 1).
 
 Prints ONE JSON line (rank 0). `roofline` prices the dominant kernel (the suffix sorter's
 radix scatter) by algorithmic bytes / HIP-event-measured launch time on the library's own
-stream; `cpu_baseline` times the CPU port of the reference (oracle/liboracle.so, 1 thread) on
-one block of the same input, which also checks full-block parity of the GPU stream.
+stream; its `traffic` (HBM bytes per launch) comes from two rocprofv3 PMC passes (FETCH_SIZE,
+WRITE_SIZE) of one encode of the same input, run as child processes of this run before it
+touches the GPU (`traffic_source` says so, or names the file it fell back to).
+`cpu_baseline` times the CPU port of the reference (oracle/liboracle.so, 1 thread) on one block
+of the same input after the timed region, which also checks full-block parity of the GPU stream.
 """
 from __future__ import annotations
 
@@ -66,6 +75,14 @@ def parse_args():
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the host-buffer (salz_encode_safe-style) end-to-end timing")
     ap.add_argument("--cpu-child", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the rocprofv3 PMC passes that measure roofline.traffic in this run")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="N > 1 exchange backend: nccl (RCCL over xGMI, one GPU per rank) or gloo "
+                         "(payload staged through host memory; ranks may share a GPU)")
+    ap.add_argument("--launch", action="store_true",
+                    help="go through torch.distributed.run even at --gpus 1 (world-1 RCCL path)")
     ap.add_argument("--slots", type=int, default=0,
                     help="concurrent encoder contexts per GPU for the sharded workloads "
                          "(0 = auto: 4; one block per GPU: 1)")
@@ -92,6 +109,11 @@ def cpu_child(spec: str) -> None:
 
     src = gen(kind, total, 1, 16 if kind == "smx" else 256)
     blk = np.ascontiguousarray(src[start:start + sample])
+    del src
+    # Wait for the parent's go (sent after its timed region), so the CPU work never overlaps
+    # the GPU measurement; an empty read means the parent is gone.
+    if sys.stdin.readline().strip() != "go":
+        return
     c0 = time.perf_counter()
     rc, ref = oracle_encode(blk)
     c1 = time.perf_counter()
@@ -105,15 +127,132 @@ def cpu_child(spec: str) -> None:
 
 
 def start_cpu_child(kind, total, start, sample):
-    """Start the pinned CPU-baseline child before this process makes any GPU call (it runs
-    beside the GPU timing on a core of its own and is collected at the end)."""
+    """Start the pinned CPU-baseline child before this process makes any GPU call. It prepares
+    its input, then blocks until the parent writes "go" (after the timed region and the e2e
+    timing), so the baseline's CPU work never overlaps a GPU measurement."""
     import subprocess
 
     cores = sorted(os.sched_getaffinity(0))
     core = cores[-1]
     spec = f"{kind},{total},{start},{sample},{core}"
     return subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-child", spec],
-                            stdout=subprocess.PIPE, text=True), core
+                            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True), core
+
+
+def launch_ranks(args) -> int:
+    """--gpus N without an outside launcher: one rank per GPU through torch.distributed.run,
+    started as a CHILD process before this process touches any GPU (never an exec). Relays rank
+    0's JSON line; fails when the ranks' world differs from N."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool (RCCL)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        sys.stdout.write(p.stdout)
+        print(f"bench.py: torch.distributed.run exited with {p.returncode}", file=sys.stderr)
+        return p.returncode or 1
+    line = json.loads(lines[-1])
+    if line.get("n_gpus") != args.gpus:
+        print(f"bench.py: the ranks reported n_gpus={line.get('n_gpus')}, expected {args.gpus}",
+              file=sys.stderr)
+        return 3
+    print(lines[-1], flush=True)
+    return 0
+
+
+def pmc_child(args) -> None:
+    """One encode of the workload's first block with the library's launch timing on, for the
+    rocprofv3 --pmc passes (no torch, no extra encodes: the counters cover exactly one encode).
+    Prints the kernel-level statistics as one JSON line."""
+    import salz_amd
+    from tests.helpers import gen
+
+    config, kind, total, block = WORKLOADS[args.workload]
+    kind = args.kind or kind
+    total = args.size or total
+    n = min(block, total) if block else total
+    src = gen(kind, total, 1, 16 if kind == "smx" else 256)[:n]
+    ctx = salz_amd.Context(0, n)
+    ctx.set_timing(True)
+    ctx.encode(src)
+    st = ctx.stats()
+    print(json.dumps({"radix_scatter_launches": st["radix_scatter_launches"],
+                      "radix_scatter_bytes": st["radix_scatter_bytes"]}), flush=True)
+
+
+def measure_traffic(args):
+    """roofline.traffic measured in this run: two rocprofv3 --pmc passes (FETCH_SIZE, then
+    WRITE_SIZE; one pass cannot hold both on gfx950) over `bench.py --pmc-child`, corrected as
+    /opt/skills/guides/MI355X_MICROARCH.md prescribes (tools/pmc_traffic.py). Runs BEFORE this
+    process makes any GPU call (the profiler children start from a process without GPU state).
+    Returns (per-launch traffic dict, error string)."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_traffic import load  # noqa: E402
+
+    tmp = tempfile.mkdtemp(prefix="salz_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    child_args = ["--pmc-child", "--workload", args.workload]
+    if args.kind:
+        child_args += ["--kind", args.kind]
+    if args.size:
+        child_args += ["--size", str(args.size)]
+    res, stats = {}, None
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(tmp, counter)
+        cmd = [prof, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+               sys.executable, os.path.abspath(__file__), *child_args]
+        try:
+            p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
+                               env=env, cwd="/tmp", timeout=150)
+        except subprocess.TimeoutExpired:
+            return None, f"rocprofv3 --pmc {counter} timed out"
+        if p.returncode != 0:
+            return None, f"rocprofv3 --pmc {counter} exited with {p.returncode}"
+        js = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        stats = json.loads(js[-1]) if js else stats
+        csvp = os.path.join(d, "pmc_counter_collection.csv")
+        if not os.path.exists(csvp):
+            return None, f"no counter file from the {counter} pass"
+        rows = load(csvp).get("k_radix_scatter", [])
+        if not rows:
+            return None, f"no k_radix_scatter dispatches in the {counter} pass"
+        res[counter] = (sum(v for _, v, _ in rows), len(rows))
+    shutil.rmtree(tmp, ignore_errors=True)
+    fetch = 2 * res["FETCH_SIZE"][0] * 1024 / res["FETCH_SIZE"][1]
+    write = res["WRITE_SIZE"][0] * 1024 / res["WRITE_SIZE"][1]
+    out = {"traffic_per_launch": round(fetch + write), "fetch_bytes_per_launch": round(fetch),
+           "write_bytes_per_launch": round(write), "pmc_launches": res["FETCH_SIZE"][1]}
+    if stats and stats.get("radix_scatter_launches"):
+        out["pmc_alg_bytes_per_launch"] = round(stats["radix_scatter_bytes"] / stats["radix_scatter_launches"])
+        out["pmc_timed_launches"] = stats["radix_scatter_launches"]
+    return out, None
+
+
+def git_head() -> str:
+    try:
+        import subprocess
+
+        return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True, timeout=10).stdout.strip() or "unknown"
+    except Exception:
+        return "unknown"
 
 
 def main():
@@ -121,9 +260,17 @@ def main():
     if args.cpu_child:
         cpu_child(args.cpu_child)
         return
+    if args.pmc_child:
+        pmc_child(args)
+        return
+    launched = "WORLD_SIZE" in os.environ  # a rank of torch.distributed.run (ours or the driver's)
+    if not launched and (args.gpus > 1 or args.launch):
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if launched and world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
 
     config, kind, total, block = WORKLOADS[args.workload]
     kind = args.kind or kind
@@ -134,6 +281,10 @@ def main():
         first = min(block, total) if sharded else total
         sample = first if args.cpu_sample <= 0 else min(args.cpu_sample, first)
         child, _ = start_cpu_child(kind, total, 0, sample)
+    # roofline.traffic of this run: PMC passes in profiler children, before any GPU call here
+    traffic_meas, traffic_err = None, "not measured (--no-pmc, N > 1 or a sharded workload)"
+    if rank == 0 and world == 1 and not sharded and not args.no_pmc:
+        traffic_meas, traffic_err = measure_traffic(args)
 
     # torch first: libsalz then shares torch's HIP runtime (one runtime per process), and
     # torch owns the HBM buffers the encoder reads and writes and RCCL moves.
@@ -141,7 +292,7 @@ def main():
 
     dist = None
     cpu_group = None
-    if world > 1:
+    if launched:
         import torch.distributed as dist
 
         torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
@@ -150,10 +301,14 @@ def main():
         saved, null = os.dup(1), os.open(os.devnull, os.O_WRONLY)
         os.dup2(null, 1)
         try:
-            # nccl = RCCL over xGMI for the exchange step (lengths + payload runs, HBM to HBM);
-            # a gloo side group carries the host-side barrier and timing reductions.
-            dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
-            cpu_group = dist.new_group(backend="gloo")
+            if args.dist_backend == "nccl":
+                # nccl = RCCL over xGMI for the exchange step (lengths + payload runs, HBM to
+                # HBM); a gloo side group carries the host-side barrier and timing reductions.
+                dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+                cpu_group = dist.new_group(backend="gloo")
+            else:  # rehearsal: everything over gloo, payload staged through host memory
+                dist.init_process_group("gloo")
+                cpu_group = dist.group.WORLD
             dist.barrier(group=cpu_group)
         finally:
             os.dup2(saved, 1)
@@ -300,12 +455,15 @@ def main():
     # rank 0 the assembled container (every rank's blocks) through the threaded decoder.
     ok = all(salz_amd.decode_safe(s_, e - s, frame=True) == src[s:e].tobytes()
              for s_, (s, e) in zip(streams, spans))
-    container_ok = None
+    container_ok, container_sha = None, None
     if rank == 0:
         cbytes = cont.cpu().numpy().tobytes()
         want_len = total * world if not sharded else total
         back = salz_amd.decode_blocks(cbytes, want_len)
         container_ok = back == (src.tobytes() * world if not sharded else src.tobytes())
+        import hashlib
+
+        container_sha = hashlib.sha256(cbytes).hexdigest()
     roundtrip_ok = allreduce([0.0 if ok else 1.0], SUM)[0] == 0
 
     value = in_bytes * args.steps / dt / 1e6
@@ -317,15 +475,38 @@ def main():
     # (24 B per element, + 1 B where a pass also writes the next pass's digit byte, radix.hip)
     bytes_rx = float(st.get("radix_scatter_bytes") or RADIX_BYTES_PER_ELEM * float(st["radix_scatter_elems"]))
     achieved = bytes_rx / (ms_rx * 1e-3) / 1e9 if ms_rx > 0 else 0.0
-    # HBM traffic of the same kernel from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
-    # command (tools/pmc_traffic.py -> bench_traffic.json), when they were taken on this workload.
-    traffic = None
-    tpath = os.path.join(ROOT, "bench_traffic.json")
-    if os.path.exists(tpath):
-        t = json.load(open(tpath))
-        if (t.get("kernel") == "k_radix_scatter" and t.get("kind") == kind and t.get("size") == total
-                and not sharded):
-            traffic = t["traffic_per_launch"]
+    # HBM traffic of the same kernel: the rocprofv3 --pmc passes of this run (measure_traffic),
+    # per launch, against the same algorithmic-byte definition as alg_bytes_per_launch (the PMC
+    # child's own launch statistics of the same encode). Without them, the last committed
+    # measurement (bench_traffic.json), labelled with its file, build and date.
+    alg_per_launch = bytes_rx / launches
+    traffic, traffic_info = None, {"traffic_source": traffic_err}
+    if traffic_meas is not None:
+        traffic = traffic_meas["traffic_per_launch"]
+        basis = traffic_meas.get("pmc_alg_bytes_per_launch") or alg_per_launch
+        traffic_info = {
+            "traffic_source": "measured in this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE "
+                              "passes over one encode of the same input (bench.py --pmc-child), "
+                              "before the timed region",
+            "traffic_fetch_per_launch": traffic_meas["fetch_bytes_per_launch"],
+            "traffic_write_per_launch": traffic_meas["write_bytes_per_launch"],
+            "traffic_launches": traffic_meas["pmc_launches"],
+            "traffic_alg_basis_per_launch": int(basis),
+            "traffic_over_alg": round(traffic / basis, 3),
+        }
+    else:
+        tpath = os.path.join(ROOT, "bench_traffic.json")
+        if os.path.exists(tpath) and not sharded:
+            t = json.load(open(tpath))
+            if t.get("kernel") == "k_radix_scatter" and t.get("kind") == kind and t.get("size") == total:
+                traffic = t["traffic_per_launch"]
+                basis = t.get("alg_bytes_per_launch") or alg_per_launch
+                traffic_info = {
+                    "traffic_source": f"bench_traffic.json (build {t.get('head', 'unknown')}, "
+                                      f"{t.get('date', 'undated')}; not this run: {traffic_err})",
+                    "traffic_alg_basis_per_launch": int(basis),
+                    "traffic_over_alg": round(traffic / basis, 3),
+                }
     roofline = {
         "kernel": "k_radix_scatter",
         "bound": "hbm",
@@ -334,10 +515,13 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": traffic,
-        "traffic_unit": "bytes/launch (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 PMC)",
+        "traffic_unit": "bytes/launch (2*FETCH_SIZE*1024 + WRITE_SIZE*1024, rocprofv3 PMC)",
+        **traffic_info,
         "launches": launches,
         "avg_launch_us": round(ms_rx * 1e3 / launches, 2),
-        "alg_bytes_per_launch": int(bytes_rx / launches),
+        "alg_bytes_per_launch": int(alg_per_launch),
+        "alg_bytes_definition": "24 B per element (8 B key + 4 B value read and written) + 1 B per "
+                                "element where the pass also writes the next pass's digit byte",
     }
 
     # Whole-pipeline roofline: A(N) = 66 n + m compulsory bytes per block
@@ -384,7 +568,8 @@ def main():
     if child is not None:
         import hashlib
 
-        out_txt, _ = child.communicate(timeout=900)
+        # the CPU baseline runs now, after every GPU measurement of this run
+        out_txt, _ = child.communicate("go\n", timeout=900)
         r = json.loads(out_txt.strip().splitlines()[-1])
         first = spans[0][1] - spans[0][0]
         sample = first if args.cpu_sample <= 0 else min(args.cpu_sample, first)
@@ -400,7 +585,8 @@ def main():
             "kind": "port",
             "sample": f"one {sample:,}-byte block of the same {kind} input, oracle/liboracle.so "
                       f"(clean-room C restatement of lib/salz.c + own SA-IS), 1 thread pinned to "
-                      f"core {r['core']} (sched_setaffinity in a child started before any GPU call), "
+                      f"core {r['core']} (sched_setaffinity in a child started before any GPU call, "
+                      f"run after the GPU timing), "
                       f"{r['enc_s']:.2f} s",
             "pinned_core": r["core"],
             "sa_s": round(r["sa_s"], 3),
@@ -410,6 +596,13 @@ def main():
         if sample == first and r["sha256"] is not None:
             parity_full = r["sha256"] == hashlib.sha256(streams[0]).hexdigest()
 
+    if dist is None:
+        exchange_desc = "local"
+    elif args.dist_backend == "nccl":
+        exchange_desc = (f"RCCL all-gather of run lengths + xGMI point-to-point payload runs, "
+                         f"world {world}")
+    else:
+        exchange_desc = f"gloo all-gather + point-to-point runs staged through host memory, world {world}"
     if rank == 0:
         line = {
             "metric": "compress MB/s + achieved HBM GB/s, enwik8 block, 1/2/4/8 MI355X",
@@ -433,7 +626,7 @@ def main():
                 "parallelism": f"independent blocks over {world} GPU(s), {nslots} encoder slot(s) per GPU"
                                f"{f', {bpb} blocks per pipeline pass' if use_batch else ''}; "
                                f"step = encode + frame packing + exchange ("
-                               f"{'RCCL all-gather of run lengths + xGMI point-to-point payload runs' if world > 1 else 'local'}"
+                               f"{exchange_desc}"
                                f") + container assembly in rank 0's HBM",
             },
             "roofline": roofline,
@@ -443,6 +636,7 @@ def main():
             "e2e": e2e,
             "encoded_bytes": int(out_bytes),
             "container_bytes": int(cont.numel()),
+            "container_sha256": container_sha,
             "ratio": round(in_bytes / out_bytes, 4),
             "roundtrip_ok": bool(roundtrip_ok),
             "container_roundtrip_ok": container_ok,

@@ -226,12 +226,14 @@ int dist_suffix_array(Workspace &ws, uint32_t n, int nranks, int rank, const sal
         return -1;
     }
     if (!ws.dist_owner) {
+        // owner byte per class, then the class histogram (its own room: a workspace sized for
+        // a small block has fewer than kClasses words in any of its per-slot arrays)
         void *p = nullptr;
-        SALZ_HIP(hipMalloc(&p, kClasses));
+        SALZ_HIP(hipMalloc(&p, kClasses + kClasses * sizeof(uint32_t)));
         ws.dist_owner = static_cast<uint8_t *>(p);
     }
-    // class histogram (u0), read back; the plan is computed identically on every rank
-    uint32_t *hist = ws.u0;
+    // class histogram, read back; the plan is computed identically on every rank
+    uint32_t *hist = reinterpret_cast<uint32_t *>(ws.dist_owner + kClasses);
     SALZ_HIP(hipMemsetAsync(hist, 0, kClasses * sizeof(uint32_t), st));
     const unsigned g = grid_for(n, kT * 64) < 1024u ? grid_for(n, kT * 64) : 1024u;
     for (uint32_t lo = 0; lo < kClasses; lo += kClassPart) {

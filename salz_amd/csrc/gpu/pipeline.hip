@@ -16,6 +16,7 @@
 #include "../../../include/salz_gpu.h"
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstring>
@@ -958,17 +959,106 @@ static salz_gpu_ctx *default_ctx(int device, size_t need, int slot = 0)
     return c;
 }
 
+// salz_encode_safe's context pool. The reference encoder keeps no state between calls
+// (lib/salz.c:175-256, :777-823), so T threads calling it encode T blocks at once. Here a call
+// takes any idle cached context: first an idle one on the caller's current device, then one on
+// another device, then a new context on the device with the fewest (the caller's own on a tie),
+// up to SALZ_SAFE_SLOTS (default 4) per device; when every context is busy it waits for one.
+// Contexts are shared with salz_encode_blocks / salz_encode_stream (same slots, same mutexes).
+static std::condition_variable g_pool_cv;
+
+static int safe_slots_per_device()
+{
+    static const int v = [] {
+        const char *e = getenv("SALZ_SAFE_SLOTS");
+        const int k = e ? atoi(e) : 4;
+        return k < 1 ? 1 : k > kMaxSlots ? kMaxSlots : k;
+    }();
+    return v;
+}
+
+// An idle context, locked (ctx->mu held on return), or nullptr when all are busy and no new
+// one may be created. Creates at most one context per call; *create_failed reports a failed
+// creation (device memory exhausted) and *have_any whether any context exists to wait for.
+static salz_gpu_ctx *pool_try_acquire(int cur, size_t need, bool *create_failed, bool *have_any)
+{
+    *create_failed = false;
+    *have_any = false;
+    const int ndev = salz_gpu_device_count();
+    if (ndev <= 0)
+        return nullptr;
+    const int per = safe_slots_per_device();
+    std::vector<salz_gpu_ctx *> snap;
+    {
+        std::lock_guard<std::mutex> lk(g_default_mu);
+        if (g_default.empty())
+            g_default.assign((size_t)ndev * kMaxSlots, nullptr);
+        snap = g_default;
+    }
+    for (int k = 0; k < ndev; k++) {  // existing idle contexts, current device first
+        const int d = (cur + k) % ndev;
+        for (int s = 0; s < kMaxSlots; s++) {
+            salz_gpu_ctx *c = snap[(size_t)d * kMaxSlots + s];
+            *have_any = *have_any || c != nullptr;
+            if (c && c->mu.try_lock())
+                return c;
+        }
+    }
+    // all busy: a new context on the device with the fewest (the caller's own on a tie)
+    int best = -1, best_n = per;
+    for (int k = 0; k < ndev; k++) {
+        const int d = (cur + k) % ndev;
+        int cnt = 0;
+        for (int s = 0; s < per; s++)
+            cnt += snap[(size_t)d * kMaxSlots + s] != nullptr;
+        if (cnt < best_n) {
+            best = d;
+            best_n = cnt;
+        }
+    }
+    if (best < 0)
+        return nullptr;
+    for (int s = 0; s < per; s++) {
+        std::lock_guard<std::mutex> lk(g_default_mu);
+        salz_gpu_ctx *&c = g_default[(size_t)best * kMaxSlots + s];
+        if (c)
+            continue;
+        c = salz_gpu_ctx_create(best, need);
+        if (!c) {
+            *create_failed = true;
+            return nullptr;
+        }
+        c->mu.lock();  // new and not yet visible to anyone but the pool lock holder
+        return c;
+    }
+    return nullptr;
+}
+
 // Called by salz_encode_safe (salz.c) after argument checks.
 int salz_gpu_encode_default(const uint8_t *src, size_t src_len, uint8_t *dst, size_t *dst_len)
 {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess)
-        dev = 0;
-    salz_gpu_ctx *c = default_ctx(dev, src_len);
-    if (!c)
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess)
+        cur = 0;
+    if (salz_gpu_device_count() <= 0 || cur < 0 || cur >= salz_gpu_device_count()) {
+        set_error("no usable HIP device (gfx950) for salz_encode_safe");
         return -1;
-    std::lock_guard<std::mutex> lk(c->mu);
-    return encode_host_locked(c, src, src_len, dst, dst_len, nullptr);
+    }
+    salz_gpu_ctx *c = nullptr;
+    for (;;) {
+        bool create_failed, have_any;
+        c = pool_try_acquire(cur, src_len < 9 ? 9 : src_len, &create_failed, &have_any);
+        if (c)
+            break;
+        if (create_failed && !have_any)
+            return -1;  // not even one context fits the device: report the allocation error
+        std::unique_lock<std::mutex> lk(g_default_mu);
+        g_pool_cv.wait_for(lk, std::chrono::milliseconds(2));
+    }
+    int rc = encode_host_locked(c, src, src_len, dst, dst_len, nullptr);
+    c->mu.unlock();
+    g_pool_cv.notify_one();
+    return rc;
 }
 
 // ---- multi-block / multi-GPU container encode ---------------------------------------------
@@ -1162,14 +1252,8 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
             if (r.out) (void)hipHostFree(r.out);
         }
     };
-    for (RingSlot &r : ring) {
-        if (hipHostMalloc(reinterpret_cast<void **>(&r.in), span) != hipSuccess ||
-            hipHostMalloc(reinterpret_cast<void **>(&r.out), cap) != hipSuccess) {
-            free_ring();
-            set_error("pinned host buffers for the batch ring (%zu x %zu bytes)", R, span + cap);
-            return -1;
-        }
-    }
+    // ring buffers are pinned lazily, when the reader first fills a slot: a small input touches
+    // one slot, a large one all R
     std::mutex mu;
     std::condition_variable cv;
     std::deque<size_t> todo;       // ring indices waiting for an encoder, in batch order
@@ -1195,6 +1279,12 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
                 k = t % R;
             }
             RingSlot &r = ring[k];
+            if (!r.in && (hipHostMalloc(reinterpret_cast<void **>(&r.in), span) != hipSuccess ||
+                          hipHostMalloc(reinterpret_cast<void **>(&r.out), cap) != hipSuccess)) {
+                std::lock_guard<std::mutex> lk(mu);
+                fail("pinned host buffers for the batch ring (" + std::to_string(span + cap) + " bytes)");
+                break;
+            }
             size_t got = 0;
             bool eof = false, bad = false;
             while (got < span) {  // fill the batch like fread (short only at EOF)
@@ -1224,12 +1314,7 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
         cv.notify_all();
     };
     auto worker = [&](int dev, int slot) {
-        salz_gpu_ctx *c = default_ctx(dev, span < 9 ? 9 : span, slot);
-        if (!c) {
-            std::lock_guard<std::mutex> lk(mu);
-            fail(g_err);
-            return;
-        }
+        salz_gpu_ctx *c = nullptr;  // created at the first batch this worker takes
         for (;;) {
             size_t k;
             {
@@ -1241,6 +1326,17 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
                 todo.pop_front();
             }
             RingSlot &r = ring[k];
+            if (!c) {
+                // workspace sized to this batch (a small input gets a small one; it grows on
+                // demand if a later batch is larger)
+                c = default_ctx(dev, r.in_len < 9 ? 9 : r.in_len, slot);
+                if (!c) {
+                    std::lock_guard<std::mutex> lk(mu);
+                    r.state = 3;
+                    fail(g_err);
+                    break;
+                }
+            }
             size_t out = cap;
             int rc;
             if (r.last && r.in_len % block_size == 0) {

@@ -1193,15 +1193,26 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                                ws.rank);
             SALZ_LAUNCH_CHECK();
         }
-        if (read_scalars(ws, 0, 256, "sa.m") != 0)
-            return -1;
-        if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
-            set_error("suffix sort: device index check failed (code 0x%x, round %d)", e,
-                      ws.stats.sa_rounds);
-            return -1;
+        // A split block's ranks leave together: a local failure is folded into the round's
+        // allreduce (bit 48 and up count failed ranks) instead of leaving the others blocked.
+        bool failed = read_scalars(ws, 0, 256, "sa.m") != 0;
+        if (!failed) {
+            if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
+                set_error("suffix sort: device index check failed (code 0x%x, round %d)", e,
+                          ws.stats.sa_rounds);
+                failed = true;
+            }
         }
-        const uint64_t tot = ws.hscal[8], ltot = ws.hscal[9];
+        if (failed && !dist)
+            return -1;
+        const uint64_t tot = failed ? 0 : ws.hscal[8], ltot = failed ? 0 : ws.hscal[9];
         const uint32_t Gnew = (uint32_t)tot, mnew = (uint32_t)(tot >> 32);
+        if (!failed && mnew && (h >= n || Gnew == 0)) {
+            set_error("suffix sort did not converge (h=%u n=%u m=%u)", h, n, mnew);
+            if (!dist)
+                return -1;
+            failed = true;
+        }
         if (verbose) {  // the round's wall time (this round synchronised with the host twice)
             const auto now = std::chrono::steady_clock::now();
             fprintf(stderr, "sa round %d (%s) h=%u m=%u (large %u in %u groups) groups=%u -> "
@@ -1210,9 +1221,17 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             t_round = now;
         }
         if (dist) {  // a split block ends when every rank's bucket is sorted
-            uint64_t g = mnew;
+            constexpr uint64_t kFailedRank = 1ull << 48;
+            uint64_t g = failed ? kFailedRank : mnew;
             if (dist->ops->allreduce_sum(dist->ops->user, &g) != 0) {
                 set_error("split suffix sort: allreduce failed");
+                return -1;
+            }
+            if (failed)
+                return -1;
+            if (g >= kFailedRank) {
+                set_error("split suffix sort: %llu other rank(s) failed in round %d",
+                          (unsigned long long)(g >> 48), ws.stats.sa_rounds);
                 return -1;
             }
             if (g == 0)
@@ -1227,10 +1246,6 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         }
         if (dc3_auto && h >= 32 && (uint64_t)mnew * 4 > (uint64_t)n * 3)
             return stage_suffix_array_dc3(ws, bl, codes, codes_raw);
-        if (h >= n || Gnew == 0) {
-            set_error("suffix sort did not converge (h=%u n=%u m=%u)", h, n, mnew);
-            return -1;
-        }
         if (dist) {  // rank[i + h] lives with the rank that owns suffix i + h
             if (dist_keys(ws, *dist, Vx, ngid, mnew, h, kb, Kx) != 0)
                 return -1;

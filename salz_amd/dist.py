@@ -83,14 +83,29 @@ def pack_frames(streams, lengths: Sequence[int], out):
 def gather_container(packed, nbytes: int, block_size: int, rank: int = 0, world: int = 1,
                      group=None, out=None):
     """The exchange step. `packed` holds this rank's `nbytes` of frames. Returns the container
-    tensor on rank 0 (on packed's device; `out` may supply its storage), None elsewhere."""
+    tensor on rank 0 (on packed's device; `out` may supply its storage), None elsewhere.
+
+    Whenever a process group is initialised (world 1 included, so a one-rank launch runs the
+    same collectives), the counts are all-gathered and the runs travel point to point. With
+    nccl (RCCL) the HBM tensors go straight through; with gloo, device tensors are staged
+    through host memory (several ranks may then share one GPU)."""
     import torch
 
     dev = packed.device
-    if world > 1:
-        import torch.distributed as dist
+    dist = None
+    try:
+        import torch.distributed as _d
 
-        cnt = torch.tensor([nbytes], dtype=torch.int64, device=dev)
+        if _d.is_available() and _d.is_initialized():
+            dist = _d
+    except ImportError:
+        pass
+    if dist is None and world > 1:
+        raise RuntimeError("gather_container: world > 1 needs an initialised process group")
+    host = dist is not None and dist.get_backend(group) == "gloo" and packed.is_cuda
+    cdev = torch.device("cpu") if host else dev
+    if dist is not None:
+        cnt = torch.tensor([nbytes], dtype=torch.int64, device=cdev)
         allc = [torch.zeros_like(cnt) for _ in range(world)]
         dist.all_gather(allc, cnt, group=group)
         counts = [int(c.item()) for c in allc]
@@ -98,27 +113,30 @@ def gather_container(packed, nbytes: int, block_size: int, rank: int = 0, world:
         counts = [nbytes]
     total = 8 + sum(counts)
     if rank != 0:
-        import torch.distributed as dist
-
         if nbytes:
-            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, packed[:nbytes], 0, group=group)]):
+            src = packed[:nbytes].cpu() if host else packed[:nbytes]
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, src, 0, group=group)]):
                 req.wait()
         return None
     if out is None or out.numel() < total:
         out = torch.empty(total, dtype=torch.uint8, device=dev)
     out[:8].copy_(torch.tensor(list(header(block_size)), dtype=torch.uint8).to(dev))
     out[8:8 + counts[0]].copy_(packed[:counts[0]])
-    if world > 1:
-        import torch.distributed as dist
-
-        ops, off = [], 8 + counts[0]
+    if dist is not None:
+        ops, bufs, off = [], [], 8 + counts[0]
         for r in range(1, world):
             if counts[r]:
-                ops.append(dist.P2POp(dist.irecv, out[off:off + counts[r]], r, group=group))
+                dstv = out[off:off + counts[r]]
+                buf = torch.empty(counts[r], dtype=torch.uint8) if host else dstv
+                bufs.append((dstv, buf))
+                ops.append(dist.P2POp(dist.irecv, buf, r, group=group))
             off += counts[r]
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
+        if host:
+            for dstv, buf in bufs:
+                dstv.copy_(buf)
     return out[:total]
 
 

@@ -2,7 +2,10 @@
 tests/test_dist_split.py: every rank encodes the same blocks over gloo on one GPU; rank 0 writes
 the streams.
 
-  python tests/split_worker.py RANK WORLD PORT IN.npz OUT.npz
+  python tests/split_worker.py RANK WORLD PORT IN.npz OUT.npz [perblock]
+
+perblock: every block gets a context of its own, sized to that block (encode_block_split
+without ctx), instead of one context sized to the largest block.
 """
 import os
 import sys
@@ -23,13 +26,15 @@ def main():
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     data = np.load(src_path)
     names = sorted(data.files)
-    ctx = salz_amd.Context(0, max(len(data[k]) for k in names))
+    perblock = len(sys.argv) > 6 and sys.argv[6] == "perblock"
+    ctx = None if perblock else salz_amd.Context(0, max(len(data[k]) for k in names))
     out = {}
     for k in names:
         s = encode_block_split(data[k], 0, ctx=ctx)
         if rank == 0:
             out[k] = np.frombuffer(s, np.uint8)
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
     if rank == 0:
         np.savez(out_path, **out)
     dist.barrier()

@@ -35,16 +35,14 @@ def _inputs():
     }
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-def test_split_suffix_array_matches_oracle(tmp_path, world):
-    inputs = _inputs()
+def _run_split(tmp_path, world, inputs, *extra):
     src = tmp_path / "in.npz"
     out = tmp_path / "out.npz"
     np.savez(src, **inputs)
     port = _port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "split_worker.py"), str(r), str(world),
-                               str(port), str(src), str(out)], env=env, stdout=subprocess.PIPE,
+                               str(port), str(src), str(out), *extra], env=env, stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT)
              for r in range(world)]
     logs = []
@@ -62,3 +60,16 @@ def test_split_suffix_array_matches_oracle(tmp_path, world):
         rc, ref = oracle_encode(s)
         assert rc == 0
         assert got[k].tobytes() == ref, k
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_split_suffix_array_matches_oracle(tmp_path, world):
+    _run_split(tmp_path, world, _inputs())
+
+
+def test_split_small_blocks_own_context(tmp_path):
+    """Blocks under 32 KiB, each with a context sized to it: the 65536-class histogram must not
+    live in a per-slot array (it overran ws.u0 for such contexts)."""
+    inputs = {"t20k": gen("text", 20_000, 7), "t32775": gen("text", 32_775, 8), "m1k": gen("mixed", 1_000, 9),
+              "fib5k": gen("fib", 5_000)}
+    _run_split(tmp_path, 2, inputs, "perblock")

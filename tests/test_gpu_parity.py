@@ -504,3 +504,26 @@ def test_cli_streams_gigabyte_file_with_bounded_memory(salz, tmp_path):
     assert rc == 0 and rss_d - rss0_d < 384, f"decode peak RSS {rss_d:.0f} MiB vs {rss0_d:.0f} MiB"
     back = np.fromfile(f, np.uint8)
     assert back.size == N and np.array_equal(back, src)
+
+
+def test_cli_multi_batch_ring_and_exact_multiple(salz, tmp_path):
+    """The streaming CLI at level 5 (1 MiB blocks, 8 blocks per ring batch): 2 * 8 MiB + 100
+    bytes spans three batches and must equal salz_encode_blocks' container; an input of exactly
+    16 MiB ends in an empty trailing block, which fails like the reference CLI
+    (programs/salzcli.c:143-179, lib/salz.c:197) and leaves no output file (:350-353)."""
+    import subprocess
+
+    cli = os.path.join(ROOT, "salz_amd", "salz")
+    src = gen("text", 2 * (8 << 20) + 100, 31)
+    f = tmp_path / "three.txt"
+    src.tofile(f)
+    subprocess.run([cli, "-5", "-k", "-q", str(f)], check=True, timeout=300)
+    packed = (tmp_path / "three.txt.salz").read_bytes()
+    assert packed == salz.encode_blocks(src, 1 << 20)
+    rc, ref = oracle_encode(src[(16 << 20):])  # the 100-byte trailing block
+    assert rc == 0 and packed.endswith(len(ref).to_bytes(4, "little") + ref)
+    g = tmp_path / "exact.txt"
+    src[: 16 << 20].tofile(g)
+    r = subprocess.run([cli, "-5", "-k", "-q", str(g)], timeout=300)
+    assert r.returncode != 0
+    assert not (tmp_path / "exact.txt.salz").exists()

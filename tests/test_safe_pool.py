@@ -1,0 +1,92 @@
+"""salz_encode_safe from several threads (VERDICT r02 missing #2).
+
+The reference encoder keeps no globals and allocates per call (lib/salz.c:175-256, :777-823),
+so T threads calling salz_encode_safe have T blocks in flight. Here the calls go through the C
+ABI (ctypes into libsalz.so: salz_encode_safe, plain pointers and sizes; ctypes releases the
+GIL) and the library's context pool hands each call an idle context (own HIP stream and
+workspace), preferring the caller's current device (pipeline.hip, salz_gpu_encode_default).
+Every output must equal the CPU port's stream; four threads must beat one thread's aggregate
+MB/s on 1 MiB and 16 MiB blocks.
+"""
+import ctypes
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from tests.helpers import enc_max, gen, oracle_encode
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import salz_amd
+
+    if salz_amd.device_count() == 0:
+        pytest.fail("no HIP device visible: GPU tests need an MI355X")
+    return salz_amd.lib
+
+
+def _encode_safe(lib, blk: np.ndarray) -> bytes:
+    cap = enc_max(len(blk))
+    out = np.empty(cap, np.uint8)
+    n = ctypes.c_size_t(cap)
+    rc = lib.salz_encode_safe(blk.ctypes.data, len(blk), out.ctypes.data, ctypes.byref(n))
+    assert rc == 0
+    return out[: n.value].tobytes()
+
+
+def _run(lib, blocks, threads):
+    """Encode every block once, `threads` callers pulling block indices; returns (outputs, s)."""
+    outs = [None] * len(blocks)
+    nxt = [0]
+    mu = threading.Lock()
+
+    def work():
+        while True:
+            with mu:
+                i = nxt[0]
+                nxt[0] += 1
+            if i >= len(blocks):
+                return
+            outs[i] = _encode_safe(lib, blocks[i])
+
+    ths = [threading.Thread(target=work) for _ in range(threads)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return outs, time.perf_counter() - t0
+
+
+def _blocks(kind, size, count):
+    src = gen(kind, size * count + 1, 11)
+    return [np.ascontiguousarray(src[i * size:(i + 1) * size]) for i in range(count)]
+
+
+def test_safe_four_threads_match_oracle(lib):
+    blocks = (_blocks("text", 1 << 20, 6) + _blocks("mixed", 700_001, 4) + [gen("fib", 500_000)]
+              + [gen("smx", 400_000, 2, 4)] + _blocks("text", 9_000, 8))
+    refs = [oracle_encode(b)[1] for b in blocks]
+    for rep in range(2):
+        outs, _ = _run(lib, blocks, 4)
+        bad = [i for i, (o, r) in enumerate(zip(outs, refs)) if o != r]
+        assert bad == [], f"pass {rep}: blocks {bad} differ from the oracle"
+
+
+@pytest.mark.parametrize("size,count", [(1 << 20, 48), (16 << 20, 8)])
+def test_safe_four_threads_scale(lib, size, count):
+    blocks = _blocks("text", size, count)
+    _run(lib, blocks[:4], 4)  # warm every pool context up to this block size
+    one = min(_run(lib, blocks, 1)[1] for _ in range(2))
+    outs, four = min((_run(lib, blocks, 4) for _ in range(2)), key=lambda r: r[1])
+    mbs1 = size * count / one / 1e6
+    mbs4 = size * count / four / 1e6
+    print(f"salz_encode_safe {size} B blocks: 1 thread {mbs1:.0f} MB/s, 4 threads {mbs4:.0f} MB/s "
+          f"({mbs4 / mbs1:.2f}x)")
+    rc, ref = oracle_encode(blocks[0])
+    assert outs[0] == ref
+    assert mbs4 >= 1.5 * mbs1, f"4 threads {mbs4:.0f} MB/s vs 1 thread {mbs1:.0f} MB/s"
