@@ -112,3 +112,20 @@ def sha256(b) -> str:
 def golden(name: str):
     with open(os.path.join(GOLDEN_DIR, name)) as f:
         return json.load(f)
+
+
+def wrap_input(name: str, n: int) -> np.ndarray:
+    """Inputs of the int32 cost-wrap regime (tools/make_wrap_golden.py): "smx256" = splitmix64
+    bytes (seed 5); "wrap400" = the same bytes with the last 4 MiB of every 16 MiB replaced by a
+    copy of an earlier 4 MiB run at a seeded offset."""
+    src = gen("smx", n, 5, 256).copy()
+    if name == "smx256":
+        return src
+    assert name == "wrap400"
+    rng = np.random.default_rng(5)
+    seg, rep = 16 << 20, 4 << 20
+    for b in range(seg, n + 1, seg):
+        lo = b - rep
+        s = int(rng.integers(0, lo - rep))
+        src[lo:b] = src[s:s + rep]
+    return src

@@ -101,3 +101,29 @@ def test_mixed_40mib_default_chunk_length(salz, monkeypatch):
     c.close()
     rc, ref = oracle_encode(src)
     assert rc == 0 and out == ref
+
+
+@pytest.mark.parametrize("name,n", [("smx256", 1 << 28), ("wrap400", 400_000_000)])
+def test_int32_cost_wrap_regime(salz, name, n):
+    """Blocks whose parse runs on wrapped int32 costs (9 n > 2^31 - 1; lib/salz.c:621-661 keeps
+    the costs in int32 and its factor sums are truncated to int32, SURVEY §7 hard part 5):
+    smx256 (256 MiB of splitmix bytes) comes out PLAIN; wrap400 (400 MB, a quarter repeated)
+    comes out as a SALZ stream whose cost from position 0 is ~2.7e9 bits, so the first fifth of
+    its parse decides on wrapped costs. Both must equal the oracle's bytes, pinned as golden
+    hashes by tools/make_wrap_golden.py (the oracle takes 2-4 minutes per input), and decode
+    back through the frame-length rule."""
+    import hashlib
+    import json
+    import os
+
+    from tests.helpers import GOLDEN_DIR, wrap_input
+
+    vec = {v["name"]: v for v in json.load(open(os.path.join(GOLDEN_DIR, "cost_wrap.json")))["vectors"]}[name]
+    src = wrap_input(name, n)
+    assert hashlib.sha256(src.tobytes()).hexdigest() == vec["in_sha256"]
+    out = salz.encode_safe(src)
+    assert len(out) == vec["out_len"]
+    h = int.from_bytes(out[:4], "little")
+    assert (h >> 24, h & 0xFFFFFF) == (vec["out_type"], vec["out_hdr_len"])
+    assert hashlib.sha256(out).hexdigest() == vec["out_sha256"]
+    assert salz.decode_safe(out, n, frame=True) == src.tobytes()

@@ -1,6 +1,8 @@
 """CPU tests: the oracle (test infrastructure) against the reference's golden vectors, plus
 structural properties of each stage. No GPU needed."""
 import ctypes
+import json
+import os
 
 import numpy as np
 import pytest
@@ -121,3 +123,29 @@ def test_vnibble_restatement_small_exhaustive():
         for j in range(1, k):
             assert not (low >> (4 * j)) & 0x8
         prev_k = k
+
+
+@pytest.mark.slow
+@pytest.mark.skipif(not os.environ.get("SALZ_SLOW"), reason="2-4 min of oracle each: set SALZ_SLOW=1")
+@pytest.mark.parametrize("name,n", [("smx256", 1 << 28), ("wrap400", 400_000_000)])
+def test_oracle_cost_wrap_golden(name, n):
+    """The cost-wrap golden vectors (tools/make_wrap_golden.py) against a fresh oracle run:
+    2-4 minutes each (SALZ_SLOW=1); the GPU side checks the same hashes every round."""
+    import hashlib
+
+    from tests.helpers import GOLDEN_DIR, wrap_input
+
+    vec = {v["name"]: v for v in json.load(open(os.path.join(GOLDEN_DIR, "cost_wrap.json")))["vectors"]}[name]
+    src = wrap_input(name, n)
+    assert hashlib.sha256(src.tobytes()).hexdigest() == vec["in_sha256"]
+    rc, out = oracle_encode(src)
+    assert rc == 0 and hashlib.sha256(out).hexdigest() == vec["out_sha256"]
+
+
+def test_cost_wrap_inputs_are_in_the_wrap_regime():
+    """wrap400's stream (342 MB) means a parse cost from position 0 above 2^31 - 1 bits."""
+    from tests.helpers import GOLDEN_DIR
+
+    vec = {v["name"]: v for v in json.load(open(os.path.join(GOLDEN_DIR, "cost_wrap.json")))["vectors"]}
+    assert vec["wrap400"]["out_type"] == 1 and 8 * (vec["wrap400"]["out_len"] - 4) > 2**31
+    assert 9 * (vec["smx256"]["n"] - 8) > 2**31 and vec["smx256"]["out_type"] == 0
