@@ -467,14 +467,16 @@ def _run_rss(cmd, timeout=600):
 def test_cli_streams_gigabyte_file_with_bounded_memory(salz, tmp_path):
     """The CLI streams (salz_encode_stream / salz_decode_stream, programs/salzcli.c:102-270):
     an enwik9-sized file (10^9 + 7 bytes, level 9 = 16 MiB blocks, 60 blocks) compresses with
-    the same peak host RSS as a one-block file (the HIP runtime alone holds ~1.4 GB of RSS on
-    the box; the block ring adds ~0.2 GB at level 9 whatever the input size) to exactly the
+    the same peak host RSS as a 9-block file that already fills every encoder slot and the
+    block ring (contexts and ring buffers are created as the input needs them) to exactly the
     container salz_encode_blocks makes in memory, whose first and last frames equal the
     oracle's streams, and decompresses back with bounded RSS too."""
     cli = os.path.join(ROOT, "salz_amd", "salz")
     N, block = 1_000_000_007, 16 << 20
+    # the reference point: a file just long enough to fill every encoder slot and the whole
+    # block ring (contexts and ring buffers are created lazily, so a one-block file uses less)
     small = tmp_path / "small.txt"
-    gen("text", 1_000_003, 21).tofile(small)
+    gen("text", 8 * block + 3, 21).tofile(small)
     rc, rss0 = _run_rss([cli, "-9", "-k", "-q", str(small)])
     assert rc == 0
     rc, rss0_d = _run_rss([cli, "-d", "-q", "-f", str(tmp_path / "small.txt.salz")])
@@ -484,7 +486,7 @@ def test_cli_streams_gigabyte_file_with_bounded_memory(salz, tmp_path):
     src.tofile(f)
     rc, rss = _run_rss([cli, "-9", "-k", "-q", str(f)])
     assert rc == 0
-    assert rss - rss0 < 256, f"peak RSS {rss:.0f} MiB vs {rss0:.0f} MiB for one block"
+    assert rss - rss0 < 256, f"peak RSS {rss:.0f} MiB vs {rss0:.0f} MiB for 9 blocks"
     packed = (tmp_path / "big.txt.salz").read_bytes()
     want = salz.encode_blocks(src, block)
     assert packed == want
