@@ -21,13 +21,7 @@
 // the 256 MB Infinity Cache). Instead each workgroup appends its answers to per-text-range
 // staging runs (ranges of 2^rlog positions, one global atomic per range and workgroup), and
 // k_cand_scatter moves the staged answers range by range: its concurrent writes then all fall
-// in one cache-resident window of the candidate array. The workgroup keeps its answers (hit
-// leaf, LCP minimum) in registers and then LDS, and writes each staging run with consecutive
-// lanes on consecutive slots (whole lines but for a run's two ends).
-//
-// Only the block-local tree nodes that cover >= kScan leaves are published to the global heap
-// (63 of 2047 per block): a query that leaves its block (k_ansv_global) descends through them
-// and finishes with a linear scan of kScan leaves of the suffix array / LCP arrays.
+// in one cache-resident window of the candidate array.
 #include "internal.hpp"
 
 #include <cstdio>
@@ -43,13 +37,8 @@ constexpr uint32_t kNear = 16;  // linear neighbour scan before the tree walk
 constexpr uint32_t kWQ = 1408;  // LDS walk-queue entries per block
 constexpr uint32_t kShards = 16;      // global-queue shards (blockIdx mod kShards)
 constexpr size_t kQCountWord = 800;   // u32 index into Workspace::dscal: 2 * kShards counters
-constexpr uint32_t kMaxRanges = 512;  // staging text ranges per block (rlog is raised to fit)
-constexpr uint32_t kPubLocal = 64;    // block-local heap nodes k < kPubLocal are published
-constexpr uint32_t kScan = 2 * kB / kPubLocal;  // leaves under a lowest published node (64)
-constexpr uint32_t kLeaves = kB / kT;           // leaves per thread (8)
-constexpr uint32_t kMissHit = 0xffffu;          // hit code: answer outside the block (global queue)
-constexpr uint32_t kQueued = 0xfffeu;           // hit code: queued for the block walk (phase 2)
-static_assert(kMaxRanges % kT == 0, "ranges per thread");
+constexpr uint32_t kMaxRanges = 256;  // staging text ranges per block (rlog is raised to fit)
+static_assert(kMaxRanges <= kT, "one thread per range");
 
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
@@ -89,12 +78,12 @@ __device__ __forceinline__ uint32_t shard_base(uint32_t s, uint32_t used_blocks,
     return base;
 }
 
-// One query of the block (e = leaf << 1 | nsv) walks the block's LDS min-tree. Returns the hit
-// leaf (kMissHit when the answer lies outside the block: the query then goes to the global
-// queue, wave-aggregated) and the LCP minimum in lm.
-__device__ __forceinline__ uint32_t block_walk(uint32_t e, const uint32_t *vsa, const uint32_t *vlc, uint32_t b0,
-                                               uint32_t *qp, uint32_t *qp_len, uint32_t *qn, uint32_t *qn_len,
-                                               uint32_t *qcount, uint32_t qbase, uint32_t &lm_out)
+// One queued query of the block (e = leaf << 1 | nsv) walks the block's LDS min-tree; a
+// query whose answer lies outside the block goes to the global queue (wave-aggregated).
+__device__ __forceinline__ void block_walk(uint32_t e, uint32_t slot, const uint32_t *vsa,
+                                           const uint32_t *vlc, uint32_t b0, uint2 *sh, uint32_t *qp, uint32_t *qp_len,
+                                           uint32_t *qn, uint32_t *qn_len, uint32_t *qcount,
+                                           uint32_t qbase, const Blocks &bl)
 {
     const uint32_t l = e >> 1, r = b0 + l;
     const uint32_t v = vsa[kB + l];
@@ -123,6 +112,8 @@ __device__ __forceinline__ uint32_t block_walk(uint32_t e, const uint32_t *vsa, 
             }
             node >>= 1;
         }
+        if (hit != kInf)
+            sh[2 * slot] = half(v, vsa[kB + hit], lm, bl);
     } else {
         // NSV: nearest smaller to the right; LCP minimum over (r, r'].
         lm = kInf;
@@ -147,6 +138,8 @@ __device__ __forceinline__ uint32_t block_walk(uint32_t e, const uint32_t *vsa, 
             }
             node >>= 1;
         }
+        if (hit != kInf)
+            sh[2 * slot + 1] = half(v, vsa[kB + hit], lm, bl);
     }
     // global queue: one atomic per wave and side on this block's shard counter
     const bool miss = hit == kInf;
@@ -168,8 +161,6 @@ __device__ __forceinline__ uint32_t block_walk(uint32_t e, const uint32_t *vsa, 
             (side ? qn_len : qp_len)[q] = lm;
         }
     }
-    lm_out = lm;
-    return miss ? kMissHit : hit;
 }
 
 __global__ __launch_bounds__(kT) void k_ansv_local(
@@ -183,34 +174,28 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     __shared__ uint32_t vsa[2 * kB + kNear];  // heap: [1, kB) tree, [kB, 2kB) leaves, + pad
     __shared__ uint32_t vlc[2 * kB + kNear];
     __shared__ uint16_t loc[kB];             // leaf's index within its text range's run
-    __shared__ uint16_t inv[kB];             // staging order (range-major) -> leaf
     __shared__ uint32_t rbase[kMaxRanges];   // per text range: count, then the run's first slot
-    __shared__ uint32_t lstart[kMaxRanges];  // per text range: first staging-order index
-    __shared__ uint32_t wsum[kT / 64];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    for (uint32_t r = tid; r < kMaxRanges; r += kT)
-        rbase[r] = 0;
+    uint2 *const sh = reinterpret_cast<uint2 *>(stage);  // halves: 2 slot (PSV), 2 slot + 1 (NSV)
+    const uint32_t tid = threadIdx.x;
+    if (tid < kMaxRanges)
+        rbase[tid] = 0;
     const uint32_t b0 = blockIdx.x * kB;
-    const uint32_t nvalid = n - b0 < kB ? n - b0 : kB;
     // SALZ_PROF_ANSV (diagnostics): per-phase cycle totals of thread 0
     const unsigned long long t0 = prof ? clock64() : 0ull;
 
     // Build the block's min-tree (heap: node k has children 2k, 2k + 1; leaves at kB + l) and
-    // publish its top internal nodes (k < kPubLocal) into the global heap. Thread t owns leaves
-    // 8t .. 8t + 7: the three levels above them are formed in registers, the next six by
-    // butterflies within the wave, the top two by one thread: two barriers instead of one per
-    // level.
+    // publish its internal nodes into the global heap. Thread t owns leaves 8t .. 8t + 7: the
+    // three levels above them are formed in registers, the next six by butterflies within the
+    // wave, the top two by one thread: two barriers instead of one per level.
     static_assert(kB == 8 * kT, "8 leaves per thread");
     const uint32_t root = np2 / kB + blockIdx.x;
     auto put = [&](uint32_t k, uint32_t a, uint32_t c) {
         vsa[k] = a;
         vlc[k] = c;
-        if (k < kPubLocal) {
-            const uint32_t lev = 31u - __builtin_clz(k);
-            const uint32_t g = (root << lev) + (k - (1u << lev));
-            tsa[g] = a;
-            tlcp[g] = c;
-        }
+        const uint32_t lev = 31u - __builtin_clz(k);
+        const uint32_t g = (root << lev) + (k - (1u << lev));
+        tsa[g] = a;
+        tlcp[g] = c;
     };
     uint32_t a[8], c[8];
     {
@@ -269,44 +254,14 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
         put(3, umin(vsa[6], vsa[7]), umin(vlc[6], vlc[7]));
         put(1, umin(vsa[2], vsa[3]), umin(vlc[2], vlc[3]));
     }
-    // Staging: leaf l's answers go to slot rbase[p >> rlog] + loc[l] (one run per text range in
-    // this workgroup; the run is reserved with one global atomic per range). lstart: the
-    // range-major order of the block's leaves, in which the runs are written out.
-    for (uint32_t l = tid; l < nvalid; l += kT)
+    // Staging slots: leaf l's answers go to slot rbase[p >> rlog] + loc[l] (one run per text
+    // range in this workgroup; the run is reserved with one global atomic per range).
+    for (uint32_t l = tid; l < kB && b0 + l < n; l += kT)
         loc[l] = (uint16_t)atomicAdd(&rbase[vsa[kB + l] >> rlog], 1u);
     __syncthreads();
-    {
-        constexpr uint32_t kPer = kMaxRanges / kT;  // consecutive ranges per thread
-        uint32_t cnt[kPer], sum = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < kPer; j++) {
-            cnt[j] = rbase[tid * kPer + j];
-            sum += cnt[j];
-        }
-        uint32_t incl = sum;
-#pragma unroll
-        for (unsigned d = 1; d < 64; d <<= 1) {
-            const uint32_t t = shfl_up_u32(incl, d);
-            if (lane >= d)
-                incl += t;
-        }
-        if (lane == 63)
-            wsum[wave] = incl;
-        __syncthreads();
-        uint32_t pre = incl - sum;
-        for (uint32_t w = 0; w < wave; w++)
-            pre += wsum[w];
-#pragma unroll
-        for (uint32_t j = 0; j < kPer; j++) {
-            const uint32_t r = tid * kPer + j;
-            lstart[r] = pre;
-            pre += cnt[j];
-            rbase[r] = cnt[j] ? (r << rlog) + atomicAdd(&rfill[r], cnt[j]) : 0u;
-        }
-    }
+    if (tid < kMaxRanges && rbase[tid])
+        rbase[tid] = (tid << rlog) + atomicAdd(&rfill[tid], rbase[tid]);
     __syncthreads();
-    for (uint32_t l = tid; l < nvalid; l += kT)
-        inv[lstart[vsa[kB + l] >> rlog] + loc[l]] = (uint16_t)l;
 
     unsigned long long t1 = 0;
     if (prof) {
@@ -316,22 +271,26 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     // Phase 1: most nearest smaller values are a few ranks away. Scan up to kNear neighbours
     // on each side (lanes read consecutive LDS words: no bank conflicts); queue the rest.
     // The walk queue holds kWQ entries (12% of 2 kB queries miss on text); a full queue walks
-    // in place. The answers stay in registers (hit leaf pair + two minima per leaf) until the
-    // tree's LDS is free again.
+    // in place. Kept small so 4 workgroups fit a CU's LDS.
     __shared__ uint16_t wq[kWQ];
     __shared__ uint32_t wq_n;
     const uint32_t qbase = shard_base(blockIdx.x % kShards, gridDim.x, n);
+    auto slot_of = [&](uint32_t l) { return rbase[vsa[kB + l] >> rlog] + loc[l]; };
+    auto enqueue = [&](uint32_t e) {
+        const uint32_t slot = atomicAdd(&wq_n, 1u);
+        if (slot < kWQ)
+            wq[slot] = (uint16_t)e;
+        else
+            block_walk(e, slot_of(e >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len, qcount,
+                       qbase, bl);
+    };
     if (tid == 0)
         wq_n = 0;
     __syncthreads();
-    uint32_t rhit[kLeaves], rlmP[kLeaves], rlmN[kLeaves];  // hitP | hitN << 16
-#pragma unroll
-    for (uint32_t k = 0; k < kLeaves; k++) {
-        const uint32_t l = tid + k * kT;
-        rhit[k] = kQueued | (kQueued << 16);
-        rlmP[k] = rlmN[k] = 0;
-        if (l >= nvalid)
-            continue;
+    for (uint32_t l = tid; l < kB; l += kT) {
+        const uint32_t r = b0 + l;
+        if (r >= n)
+            break;
         const uint32_t v = vsa[kB + l];
         // Fully unrolled: all 4 * kNear LDS reads are independent and issue back to back
         // (paired into ds_read2_b32 with constant offsets); the first hit is then selected
@@ -345,18 +304,19 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
             sR[d - 1] = vsa[kB + l + d];
             cR[d - 1] = vlc[kB + l + d];
         }
-        uint32_t lmP = vlc[kB + l], lm = lmP, hitP = kInf;
+        uint32_t lmP = vlc[kB + l], lm = lmP, hitP = kInf, pvP = 0;
 #pragma unroll
         for (uint32_t d = 1; d <= kNear; d++) {
             const bool live = hitP == kInf && d <= l;
             if (live && sL[d - 1] < v) {
                 hitP = l - d;
+                pvP = sL[d - 1];
                 lmP = lm;
             }
             if (live)
                 lm = umin(lm, cL[d - 1]);
         }
-        uint32_t lmN = kInf, hitN = kInf;
+        uint32_t lmN = kInf, hitN = kInf, pvN = 0;
         lm = kInf;
 #pragma unroll
         for (uint32_t d = 1; d <= kNear; d++) {
@@ -365,33 +325,26 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
                 lm = umin(lm, cR[d - 1]);
                 if (sR[d - 1] < v) {
                     hitN = l + d;
+                    pvN = sR[d - 1];
                     lmN = lm;
                 }
             }
         }
-        // a miss is queued for the block walk (its walker fills that side in), or walked here
-        // when the queue is full
-        if (hitP == kInf) {
-            const uint32_t slot = atomicAdd(&wq_n, 1u);
-            if (slot < kWQ) {
-                wq[slot] = (uint16_t)(l << 1);
-                hitP = kQueued;
-            } else {
-                hitP = block_walk(l << 1, vsa, vlc, b0, qp, qp_len, qn, qn_len, qcount, qbase, lmP);
-            }
+        const uint32_t slot = slot_of(l);
+        sp[slot] = v;
+        if (hitP != kInf && hitN != kInf) {
+            const uint2 hp = half(v, pvP, lmP, bl), hn = half(v, pvN, lmN, bl);
+            stage[slot] = make_uint4(hp.x, hp.y, hn.x, hn.y);
+        } else {
+            if (hitP != kInf)
+                sh[2 * slot] = half(v, pvP, lmP, bl);
+            else
+                enqueue(l << 1);
+            if (hitN != kInf)
+                sh[2 * slot + 1] = half(v, pvN, lmN, bl);
+            else
+                enqueue(l << 1 | 1u);
         }
-        if (hitN == kInf) {
-            const uint32_t slot = atomicAdd(&wq_n, 1u);
-            if (slot < kWQ) {
-                wq[slot] = (uint16_t)(l << 1 | 1u);
-                hitN = kQueued;
-            } else {
-                hitN = block_walk(l << 1 | 1u, vsa, vlc, b0, qp, qp_len, qn, qn_len, qcount, qbase, lmN);
-            }
-        }
-        rhit[k] = hitP | (hitN << 16);
-        rlmP[k] = lmP;
-        rlmN[k] = lmN;
     }
     __syncthreads();
     unsigned long long t2 = 0;
@@ -400,73 +353,18 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
 
     // Phase 2: the queued queries walk the block's min-tree; answers outside the block go to
     // the global queues (k_ansv_global continues from the block root).
-    constexpr uint32_t kWalks = (kWQ + kT - 1) / kT;
     const uint32_t nw = wq_n < kWQ ? wq_n : kWQ;
-    uint32_t whit[kWalks], wlm[kWalks];
-#pragma unroll
-    for (uint32_t k = 0; k < kWalks; k++) {
-        const uint32_t w = tid + k * kT;
-        whit[k] = kMissHit;
-        wlm[k] = 0;
-        if (w < nw)
-            whit[k] = block_walk(wq[w], vsa, vlc, b0, qp, qp_len, qn, qn_len, qcount, qbase, wlm[k]);
-    }
-    __syncthreads();  // the tree is no longer read: its LDS now holds the answers
-    uint16_t *ahit = reinterpret_cast<uint16_t *>(vsa);  // [2 l + side], in vsa[0, kB)
-    uint32_t *alm = vlc;                                 // [2 l + side]
-#pragma unroll
-    for (uint32_t k = 0; k < kLeaves; k++) {
-        const uint32_t l = tid + k * kT;
-        if (l >= nvalid)
-            continue;
-        const uint32_t hp = rhit[k] & 0xffffu, hn = rhit[k] >> 16;
-        if (hp != kQueued) {
-            ahit[2 * l] = (uint16_t)hp;
-            alm[2 * l] = rlmP[k];
-        }
-        if (hn != kQueued) {
-            ahit[2 * l + 1] = (uint16_t)hn;
-            alm[2 * l + 1] = rlmN[k];
-        }
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kWalks; k++) {
-        const uint32_t w = tid + k * kT;
-        if (w < nw) {
-            const uint32_t e = wq[w];
-            ahit[e] = (uint16_t)whit[k];
-            alm[e] = wlm[k];
-        }
-    }
-    __syncthreads();
-    unsigned long long t3 = 0;
-    if (prof)
-        t3 = clock64();
-    // Write-out in staging order: consecutive lanes take consecutive slots of a range's run.
-    // Halves answered outside the block are left as garbage; k_ansv_global overwrites them.
-#pragma unroll
-    for (uint32_t k = 0; k < kLeaves; k++) {
-        const uint32_t q = tid + k * kT;
-        if (q >= nvalid)
-            break;
-        const uint32_t l = inv[q];
-        const uint32_t v = vsa[kB + l], rg = v >> rlog;
-        const uint32_t slot = rbase[rg] + (q - lstart[rg]);
-        const uint32_t hp = ahit[2 * l], hn = ahit[2 * l + 1];
-        const uint2 h0 = half(v, hp == kMissHit ? kInf : vsa[kB + hp], alm[2 * l], bl);
-        const uint2 h1 = half(v, hn == kMissHit ? kInf : vsa[kB + hn], alm[2 * l + 1], bl);
-        sp[slot] = v;
-        stage[slot] = make_uint4(h0.x, h0.y, h1.x, h1.y);
-    }
+    for (uint32_t w = tid; w < nw; w += kT)
+        block_walk(wq[w], slot_of(wq[w] >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len,
+                   qcount, qbase, bl);
     if (prof) {
         __syncthreads();
         if (tid == 0) {
-            const unsigned long long t4 = clock64();
+            const unsigned long long t3 = clock64();
             atomicAdd(&prof[0], t1 - t0);
             atomicAdd(&prof[1], t2 - t1);
             atomicAdd(&prof[2], t3 - t2);
-            atomicAdd(&prof[3], t4 - t3);
-            atomicAdd(&prof[4], (unsigned long long)nw);
+            atomicAdd(&prof[3], (unsigned long long)nw);
         }
     }
 }
@@ -534,9 +432,7 @@ struct Tree {
 };
 
 // Queries that left their block: continue the climb from the block root. blockIdx.y is the
-// queue shard. A descent into another block's subtree goes through its published nodes down to
-// the lowest published level (kScan leaves per node) and then scans those leaves of the suffix
-// array and LCP arrays in order from the query's side.
+// queue shard.
 __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
                               const uint32_t *__restrict__ qlen,
                               const uint32_t *__restrict__ qcount, uint32_t used_blocks, int nsv,
@@ -549,14 +445,13 @@ __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
     const uint32_t r = q[e];
     uint32_t lm = qlen[e];
     const uint32_t v = t.sa[r];
-    const uint32_t grp = t.np2 / kScan;  // first node of the lowest published level
     uint32_t node = t.np2 / kB + r / kB, hit = kInf;
     while (node > 1) {
         bool side = nsv ? !(node & 1u) : (node & 1u);
         if (side) {
             uint32_t s = nsv ? node + 1 : node - 1;
             if (t.vmin(s) < v) {
-                while (s < grp) {
+                while (s < t.np2) {
                     uint32_t near = nsv ? 2 * s : 2 * s + 1;  // child adjacent to the query
                     if (t.vmin(near) < v) {
                         s = near;
@@ -565,28 +460,9 @@ __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
                         s = nsv ? 2 * s + 1 : 2 * s;
                     }
                 }
-                // s covers leaves [g0, g0 + kScan): scan them from the query's side
-                const uint32_t g0 = (s - grp) * kScan;
-                if (nsv) {
-                    for (uint32_t k = 0; k < kScan; k++) {
-                        const uint32_t rr = g0 + k;
-                        lm = umin(lm, t.lcp[rr]);
-                        if (t.sa[rr] < v) {
-                            hit = rr;
-                            break;
-                        }
-                    }
-                } else {
-                    for (uint32_t k = kScan; k-- > 0;) {
-                        const uint32_t rr = g0 + k;
-                        if (rr < t.n && t.sa[rr] < v) {
-                            hit = rr;
-                            break;
-                        }
-                        if (rr < t.n)
-                            lm = umin(lm, t.lcp[rr]);
-                    }
-                }
+                if (nsv)
+                    lm = umin(lm, t.lmin(s));
+                hit = s - t.np2;
                 break;
             }
             lm = umin(lm, t.lmin(s));
@@ -641,7 +517,7 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
     static const bool prof_on = getenv("SALZ_PROF_ANSV") != nullptr;
     unsigned long long *prof = prof_on ? reinterpret_cast<unsigned long long *>(ws.dscal) + 200 : nullptr;
     if (prof)
-        SALZ_HIP(hipMemsetAsync(prof, 0, 40, st));
+        SALZ_HIP(hipMemsetAsync(prof, 0, 32, st));
     // Staging: text ranges of 2^rlog positions (cand windows of 16 << rlog bytes; 16 MB by
     // default: 2^19 and 2^21 measured slower), at most kMaxRanges of them. Slots sp / stage
     // alias scratch that is free here.
@@ -677,10 +553,10 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
         uint32_t gq[2] = {0, 0};
         for (uint32_t s = 0; s < 2 * kShards; s++)
             gq[s & 1] += reinterpret_cast<uint32_t *>(ws.hscal)[kQCountWord + s];
-        fprintf(stderr, "ansv_local: %u blocks, cycles/block build %.0f near %.0f tree %.0f write %.0f; "
+        fprintf(stderr, "ansv_local: %u blocks, cycles/block build %.0f near %.0f tree %.0f; "
                 "queued %.3f per leaf; global %u + %u\n", used_blocks, (double)h[0] / used_blocks,
-                (double)h[1] / used_blocks, (double)h[2] / used_blocks, (double)h[3] / used_blocks,
-                (double)h[4] / n, gq[0], gq[1]);
+                (double)h[1] / used_blocks, (double)h[2] / used_blocks, (double)h[3] / n, gq[0],
+                gq[1]);
     }
     for (uint32_t lo = nblocks / 2; lo >= 1; lo >>= 1) {
         hipLaunchKernelGGL(k_tree_level, dim3(grid_for(lo, kT)), dim3(kT), 0, st, tsa, tlcp, lo,

@@ -97,7 +97,20 @@ struct Workspace {
     // begin/end event pairs around every radix scatter launch, resolved after the call
     std::vector<hipEvent_t> rx_pool;
     size_t rx_used = 0;
+    // Pinned staging of pageable host buffers (copy_h2d / copy_d2h), two chunks ping-ponged,
+    // allocated on first use: each context copies through its own, so concurrent encodes
+    // from host memory do not queue on the runtime's shared staging path.
+    uint8_t *hstage[2] = {nullptr, nullptr};
+    hipEvent_t hstage_ev[2] = {};
 };
+
+constexpr size_t kStageChunk = 4 << 20;  // bytes per pinned staging chunk
+// Host <-> device copies on ws.stream: pinned (or device) host memory goes straight to the DMA
+// engine; pageable memory through the context's pinned chunks (the CPU copy of one chunk
+// overlaps the DMA of the other). copy_h2d returns once the source may be reused, before the
+// last DMA finishes; copy_d2h returns with the data in dst.
+int copy_h2d(Workspace &ws, uint8_t *dst, const uint8_t *src, size_t bytes);
+int copy_d2h(Workspace &ws, uint8_t *dst, const uint8_t *src, size_t bytes);
 
 constexpr size_t kHostScal = 64 << 10;  // mapped host buffer: scalars below, read_device above
 

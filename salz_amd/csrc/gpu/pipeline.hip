@@ -105,7 +105,94 @@ void workspace_free(Workspace &ws)
         (void)hipEventDestroy(e);
     if (ws.own_stream && ws.stream)
         (void)hipStreamDestroy(ws.stream);
+    for (int b = 0; b < 2; b++) {
+        if (ws.hstage[b])
+            (void)hipHostFree(ws.hstage[b]);
+        if (ws.hstage_ev[b])
+            (void)hipEventDestroy(ws.hstage_ev[b]);
+    }
     ws = Workspace{};
+}
+
+// Whether a host buffer is pinned (registered or hipHostMalloc'ed) or device memory, so a
+// copy can skip the staging.
+static bool dma_ready(const void *p)
+{
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+static int stage_ready(Workspace &ws)
+{
+    for (int b = 0; b < 2; b++) {
+        if (!ws.hstage[b]) {
+            void *h = nullptr;
+            SALZ_HIP(hipHostMalloc(&h, kStageChunk, hipHostMallocDefault));
+            ws.hstage[b] = static_cast<uint8_t *>(h);
+        }
+        if (!ws.hstage_ev[b])
+            SALZ_HIP(hipEventCreateWithFlags(&ws.hstage_ev[b], hipEventDisableTiming));
+    }
+    return 0;
+}
+
+int copy_h2d(Workspace &ws, uint8_t *dst, const uint8_t *src, size_t bytes)
+{
+    if (bytes == 0)
+        return 0;
+    if (bytes <= (64u << 10) || dma_ready(src)) {
+        SALZ_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ws.stream));
+        return 0;
+    }
+    if (stage_ready(ws) != 0)
+        return -1;
+    for (size_t o = 0, k = 0; o < bytes; o += kStageChunk, k++) {
+        const size_t len = bytes - o < kStageChunk ? bytes - o : kStageChunk;
+        const int b = (int)(k & 1);
+        if (k >= 2)  // the DMA that last read this chunk
+            SALZ_HIP(hipEventSynchronize(ws.hstage_ev[b]));
+        memcpy(ws.hstage[b], src + o, len);
+        SALZ_HIP(hipMemcpyAsync(dst + o, ws.hstage[b], len, hipMemcpyHostToDevice, ws.stream));
+        SALZ_HIP(hipEventRecord(ws.hstage_ev[b], ws.stream));
+    }
+    // (a later copy_h2d on this context waits on these events before reusing a chunk; every
+    // caller synchronises the stream before returning anyway)
+    return 0;
+}
+
+int copy_d2h(Workspace &ws, uint8_t *dst, const uint8_t *src, size_t bytes)
+{
+    if (bytes == 0)
+        return 0;
+    if (bytes <= (64u << 10) || dma_ready(dst)) {
+        SALZ_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ws.stream));
+        SALZ_HIP(hipStreamSynchronize(ws.stream));
+        return 0;
+    }
+    if (stage_ready(ws) != 0)
+        return -1;
+    const size_t nch = (bytes + kStageChunk - 1) / kStageChunk;
+    auto len_of = [&](size_t k) { return bytes - k * kStageChunk < kStageChunk ? bytes - k * kStageChunk : kStageChunk; };
+    auto issue = [&](size_t k) -> int {
+        SALZ_HIP(hipMemcpyAsync(ws.hstage[k & 1], src + k * kStageChunk, len_of(k), hipMemcpyDeviceToHost,
+                                ws.stream));
+        SALZ_HIP(hipEventRecord(ws.hstage_ev[k & 1], ws.stream));
+        return 0;
+    };
+    for (size_t k = 0; k < nch && k < 2; k++)
+        if (issue(k) != 0)
+            return -1;
+    for (size_t k = 0; k < nch; k++) {
+        SALZ_HIP(hipEventSynchronize(ws.hstage_ev[k & 1]));
+        memcpy(dst + k * kStageChunk, ws.hstage[k & 1], len_of(k));
+        if (k + 2 < nch && issue(k + 2) != 0)
+            return -1;
+    }
+    return 0;
 }
 
 // Room for one stream (or a batch's streams at batch_stride apart) with margin: a SALZ stream
@@ -438,8 +525,10 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P
     }
 
     if (mark(ws, EV_START)) return -1;
-    SALZ_HIP(hipMemcpyAsync(ws.text, src, P, src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                            st));
+    if (src_dev)
+        SALZ_HIP(hipMemcpyAsync(ws.text, src, P, hipMemcpyDeviceToDevice, st));
+    else if (copy_h2d(ws, ws.text, src, P) != 0)
+        return -1;
     SALZ_HIP(hipMemsetAsync(ws.text + P, 0, 128, st));
     // (a batch's chunk length follows its block size: the per-block trade-off of pass count
     // against pass length, parse.hip)
@@ -606,8 +695,8 @@ static int encode_batch_locked(Workspace &ws, const uint8_t *src, size_t P, size
         set_error("batch frames (%zu bytes) exceed the destination capacity (%zu)", total, *dst_len);
         return -1;
     }
-    SALZ_HIP(hipMemcpyAsync(dst, packed, total, hipMemcpyDeviceToHost, ws.stream));
-    SALZ_HIP(hipStreamSynchronize(ws.stream));
+    if (copy_d2h(ws, dst, packed, total) != 0)
+        return -1;
     *dst_len = total;
     return 0;
 }
@@ -780,7 +869,7 @@ static int encode_host_locked(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_
     size_t len = 0;
     if (encode_one(ws, src, false, src_len, ws.out, cap, &len, dump) != 0)
         return -1;
-    if (hipMemcpy(dst, ws.out, len, hipMemcpyDeviceToHost) != hipSuccess) {
+    if (copy_d2h(ws, dst, ws.out, len) != 0) {
         set_error("D2H copy of the encoded stream failed");
         return -1;
     }

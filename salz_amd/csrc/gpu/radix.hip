@@ -208,14 +208,11 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     const uint32_t *__restrict__ offs, uint32_t ntiles, const uint32_t *__restrict__ totals,
     TextSrc txt, uint8_t *__restrict__ dout, int nshift)
 {
-    // Keys and values are staged one after the other in the same 32 KB, and the per-wave digit
-    // counts of the ranking live in its first 4 KB until the staging starts; the digit of each
-    // staged slot is kept (4 KB) so the value pass recomputes its destination instead of
-    // holding it in registers: 38 KB of LDS and <= 128 VGPRs, 4 workgroups per CU.
+    // Keys and values are staged one after the other in the same 32 KB (4 workgroups per CU
+    // instead of 2 with a 48 KB key + value stage).
     __shared__ uint64_t skey[kTile];
     uint32_t *sval = reinterpret_cast<uint32_t *>(skey);
-    uint32_t (*cnt)[256] = reinterpret_cast<uint32_t (*)[256]>(skey);
-    __shared__ uint8_t sdig[kTile];
+    __shared__ uint32_t cnt[4][256];
     __shared__ uint32_t dstart[256];
     __shared__ uint32_t gbase[256];
     __shared__ uint32_t wsum[4];
@@ -234,17 +231,14 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     for (int j = 0; j < kItems; j++) {
         size_t i = base + (size_t)j * 64 + lane;
         bool ok = i < m;
-        // The values are loaded (or, text-built, recomputed) only when they are staged, after
-        // the ranking, so they are not live across it; the block passes (kMode 2) need them
-        // for their digits.
         if (kMode == 1) {  // unconditional text loads (clamped entry)
             const uint32_t sfx = init_suffix(ok ? i : 0, txt.g);
             const uint64_t kk = init_key(txt, sfx, nullptr);
             k[j] = ok ? kk : 0ull;
+            v[j] = sfx;
         } else {
             k[j] = ok ? kin[i] : 0ull;
-            if (kMode == 2)
-                v[j] = ok ? vin[i] : 0u;
+            v[j] = ok ? vin[i] : 0u;
         }
     }
 
@@ -333,35 +327,30 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
         }
         return;
     }
-    // tile-local sorted position of each item (in place of its wave-local rank)
-#pragma unroll
-    for (int j = 0; j < kItems; j++) {
-        const unsigned d = (unsigned)(k[j] >> shift) & 255u;
-        lrank[j] += dstart[d] + cnt[wave][d];
-    }
-    __syncthreads();  // the counts are read: their LDS now stages the keys
+    uint32_t pos[kItems];  // tile-local sorted position of each item
 #pragma unroll
     for (int j = 0; j < kItems; j++) {
         size_t i = base + (size_t)j * 64 + lane;
-        if (i < m) {
-            skey[lrank[j]] = k[j];
-            sdig[lrank[j]] = (uint8_t)(k[j] >> shift);
-        }
+        unsigned d = (unsigned)(k[j] >> shift) & 255u;
+        pos[j] = dstart[d] + cnt[wave][d] + lrank[j];
+        if (i < m)
+            skey[pos[j]] = k[j];
     }
     __syncthreads();
 
     size_t tbase = (size_t)blockIdx.x * kTile;
     uint32_t tcount = (uint32_t)((m - tbase) < (size_t)kTile ? (m - tbase) : (size_t)kTile);
+    uint32_t gdst[kItems];  // global destination of staged slot tid + j * kThreads
 #pragma unroll
     for (int j = 0; j < kItems; j++) {
         const uint32_t s = tid + (uint32_t)j * kThreads;
         if (s < tcount) {
             uint64_t key = skey[s];
             unsigned d = (unsigned)(key >> shift) & 255u;
-            const uint32_t g = gbase[d] + (s - dstart[d]);
-            kout[g] = key;
+            gdst[j] = gbase[d] + (s - dstart[d]);
+            kout[gdst[j]] = key;
             if (dout)  // the next pass's digit, for its histogram
-                dout[g] = (uint8_t)(key >> nshift);
+                dout[gdst[j]] = (uint8_t)(key >> nshift);
         }
     }
     __syncthreads();  // keys out of LDS; the same bytes now stage the values
@@ -369,16 +358,14 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     for (int j = 0; j < kItems; j++) {
         size_t i = base + (size_t)j * 64 + lane;
         if (i < m)
-            sval[lrank[j]] = kMode == 1 ? init_suffix(i, txt.g) : vin[i];
+            sval[pos[j]] = v[j];
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kItems; j++) {
         const uint32_t s = tid + (uint32_t)j * kThreads;
-        if (s < tcount) {
-            const unsigned d = sdig[s];
-            vout[gbase[d] + (s - dstart[d])] = sval[s];
-        }
+        if (s < tcount)
+            vout[gdst[j]] = sval[s];
     }
 }
 

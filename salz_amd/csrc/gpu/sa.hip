@@ -255,8 +255,10 @@ __global__ void k_headpos(HeadBits hb, uint32_t m, uint32_t *__restrict__ headpo
 
 // Survivor masks of wave word w of the list (entries 64w .. 64w + 63): entry c is in a
 // singleton group iff it is a head and so is c + 1 (or c is the last entry). se: entries of
-// groups of size >= 2; sh: heads of those groups. Both loads unconditional (clamped word).
-__device__ __forceinline__ void surv_masks(const HeadBits &hb, size_t w, uint32_t m, uint64_t &se, uint64_t &sh)
+// groups of size >= 2; sh: heads of those groups. Groups of two that k_pairs finished (their
+// head's bit in pf) leave the list like singletons. All loads unconditional (clamped word).
+__device__ __forceinline__ void surv_masks(const HeadBits &hb, const uint64_t *pf, size_t w, uint32_t m,
+                                           uint64_t &se, uint64_t &sh)
 {
     const size_t nw = ((size_t)m + 63) / 64;
     const bool more = w + 1 < nw;
@@ -268,17 +270,115 @@ __device__ __forceinline__ void surv_masks(const HeadBits &hb, size_t w, uint32_
         nh |= 1ull << (left - 1);  // the last entry's successor is past the list
     se = valid & ~(h & nh);
     sh = valid & h & ~nh;
+    if (pf) {
+        const uint64_t fh = pf[w], fp = pf[w ? w - 1 : 0];
+        const uint64_t fs = (fh << 1) | (w ? fp >> 63 : 0ull);  // the pairs' second entries
+        se &= ~(fh | fs);
+        sh &= ~fh;
+    }
 }
 
 // Per wave word: (survivor entries << 32 | survivor heads); k_commit reads their exclusive scan.
-__global__ __launch_bounds__(kT) void k_surv(HeadBits hb, uint32_t m, uint64_t *__restrict__ P)
+__global__ __launch_bounds__(kT) void k_surv(HeadBits hb, const uint64_t *__restrict__ pf, uint32_t m,
+                                             uint64_t *__restrict__ P)
 {
     const size_t w = (size_t)blockIdx.x * kT + threadIdx.x;
     if (w >= ((size_t)m + 63) / 64)
         return;
     uint64_t se, sh;
-    surv_masks(hb, w, m, se, sh);
+    surv_masks(hb, pf, w, m, se, sh);
     P[w] = ((uint64_t)__popcll(se) << 32) | (uint64_t)__popcll(sh);
+}
+
+// Groups of exactly two members at depth h (a head c whose successor is no head and whose
+// successor's successor is a head or past the list) are decided here by comparing their two
+// suffixes directly past the shared h bytes, eight lanes per pair and 128 bytes per step (the
+// long-compare shape of k_heads_lcp), for at most kPairMax bytes. A decided pair's head gets
+// its bit in pf and its record in pr (mismatch offset L | the second entry sorts first << 31);
+// k_commit then places both suffixes for good (SA, final ranks, and the LCP h + L of the second)
+// instead of keeping them for the next doubling round. Past the end of their block the shorter
+// suffix sorts first, as everywhere in this sort. On text, about a third of the survivors of
+// each round are such pairs, and they are what the late rounds consist of.
+// Final ranks are finer than a depth-h group rank: a later round may then split two suffixes
+// whose h + hk bytes still agree, so k_heads_lcp compares past hk without a bound.
+constexpr uint32_t kPairMax = 1024;
+__global__ __launch_bounds__(kT) void k_pairs(const uint32_t *__restrict__ V, HeadBits hb, uint32_t m, Blocks bl,
+                                              uint32_t h, const uint8_t *__restrict__ T, uint64_t *__restrict__ pf,
+                                              uint32_t *__restrict__ pr, uint32_t *__restrict__ npairs)
+{
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    const size_t w = c >> 6;
+    if (w * 64 >= m)
+        return;  // whole wave past the end
+    const size_t nw = ((size_t)m + 63) / 64;
+    const bool more = w + 1 < nw;
+    const uint64_t H = hb.hmask[w], Hn = hb.hmask[more ? w + 1 : w];
+    const uint64_t left = (uint64_t)m - (uint64_t)w * 64;  // >= 1
+    const uint64_t valid = left >= 64 ? ~0ull : (1ull << left) - 1ull;
+    const uint64_t past1 = left >= 65 ? 0ull : ~0ull << (left - 1);  // c + 1 >= m
+    const uint64_t past2 = left >= 66 ? 0ull : ~0ull << (left >= 2 ? left - 2 : 0);  // c + 2 >= m
+    const uint64_t nh = (H >> 1) | (more ? Hn << 63 : 0ull) | past1;
+    const uint64_t nnh = (H >> 2) | (more ? Hn << 62 : 0ull) | past2;
+    const uint64_t ph = valid & H & ~nh & nnh;  // heads of groups of two
+    uint64_t pend = ph, done = 0;
+    const uint32_t lane = lane_id(), sub = lane >> 3, sl8 = lane & 7u;
+    while (pend) {
+        uint64_t pk = pend;  // group `sub` takes the sub-th pending pair in lane order
+        for (uint32_t u = 0; u < sub; u++)
+            pk &= pk - 1;
+        const bool have = pk != 0;
+        const uint32_t src = have ? (uint32_t)__ffsll((unsigned long long)pk) - 1u : 0u;
+        uint64_t batch = pend;  // the (up to) eight pairs of this step, for the result bits
+        for (uint32_t u = 0; u < 8; u++)
+            pend &= pend - 1;
+        batch &= ~pend;
+        const size_t ch = w * 64 + src;
+        const uint32_t i = V[have ? ch : w * 64], j = V[have ? ch + 1 : w * 64];  // (clamped: c + 1 < m)
+        const uint32_t e = bl.end(i), mx = i > j ? i : j;
+        const uint32_t lim = e - mx > h ? e - mx - h : 0u;  // bytes both suffixes have past h
+        const uint32_t sl = have ? (lim < kPairMax ? lim : kPairMax) : 0u;
+        // (a lane without a pair reads the text's first bytes: a list entry may be shorter than h)
+        const size_t si = have ? (size_t)i + h : 0, sj = have ? (size_t)j + h : 0;
+        uint32_t mis = 0xffffffffu;
+        for (uint32_t base = 0;; base += 8 * 16) {
+            const uint32_t off = base + sl8 * 16, offc = off < sl ? off : 0u;
+            const uint64_t x0 = load_u64_any(T, si + offc) ^ load_u64_any(T, sj + offc);
+            const uint64_t x1 = load_u64_any(T, si + offc + 8) ^ load_u64_any(T, sj + offc + 8);
+            uint32_t mm = 0xffffffffu;
+            if (off < sl && (x0 | x1))
+                mm = x0 ? off + ((uint32_t)__builtin_ctzll(x0) >> 3) : off + 8u + ((uint32_t)__builtin_ctzll(x1) >> 3);
+            mm = umin_(mm, shfl_xor_u32(mm, 1));
+            mm = umin_(mm, shfl_xor_u32(mm, 2));
+            mm = umin_(mm, shfl_xor_u32(mm, 4));
+            if (mis == 0xffffffffu)
+                mis = mm;
+            const bool fin = mis != 0xffffffffu || base + 8 * 16 >= sl;
+            if (!wave_ballot(!fin))
+                break;
+        }
+        // decided: a mismatch inside both suffixes, or one of them ends within kPairMax bytes
+        const bool hit = mis < sl;
+        const bool decided = have && (hit || lim <= kPairMax);
+        if (decided && sl8 == 0) {
+            const uint32_t L = hit ? mis : lim;
+            // the second entry sorts first when its byte at the mismatch is smaller, or when
+            // the first entry's suffix is the longer one and the shorter ran out
+            const bool swap = hit ? T[sj + L] < T[si + L] : j > i;
+            pr[ch] = L | (swap ? 0x80000000u : 0u);
+        }
+        const uint64_t dl = wave_ballot(decided && sl8 == 0);  // bit 8 * sub
+        for (uint32_t u = 0; u < 8 && batch; u++) {
+            const uint64_t b = batch & (~batch + 1ull);  // u-th pair of the step, in lane order
+            batch &= batch - 1;
+            if ((dl >> (8 * u)) & 1ull)
+                done |= b;
+        }
+    }
+    if (lane == 0) {
+        pf[w] = done;
+        if (npairs && done)
+            atomicAdd(npairs, (uint32_t)__popcll(done));
+    }
 }
 
 // Next round's group table (ginfo: size << 32 | compact start) is written by each surviving
@@ -296,7 +396,9 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
                          uint32_t *__restrict__ nval, uint32_t *__restrict__ ngid,
                          uint32_t *__restrict__ rank, uint32_t *__restrict__ sa, GroupTab tab,
                          uint32_t m, uint32_t n, uint32_t nsa, int kb_old, int round0, uint32_t *err,
-                         uint32_t ihi, uint32_t *__restrict__ later, uint32_t gbase)
+                         uint32_t ihi, uint32_t *__restrict__ later, uint32_t gbase,
+                         const uint64_t *__restrict__ pf, const uint32_t *__restrict__ pr,
+                         uint32_t *__restrict__ lcps, uint32_t hdepth)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
@@ -312,21 +414,33 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     // The first subgroup of an old group keeps the old group's head, so its members' ranks
     // are unchanged; every other rank (and all of round 0) is written.
     const bool same = !round0 && (hp == 0 || (key[hp - 1] >> kb_old) != (key[hp] >> kb_old));
+    // A group of two that k_pairs decided: both members take their final places now (the
+    // second of them also its LCP with the first); ranks are final positions + 1.
+    const bool pair = size == 2 && pf && ((pf[hp >> 6] >> (hp & 63u)) & 1ull);
+    uint32_t slot = c + o, rpos = hp + o;  // SA slot (singletons, pairs); rank = group head's + 1
+    if (pair) {
+        const uint32_t rec = pr[hp];
+        slot = rpos = hp + o + (((uint32_t)c - hp) ^ (rec >> 31));
+        if (lcps && slot == hp + o + 1u)
+            lcps[slot] = hdepth + (rec & 0x7fffffffu);
+    }
     // rank[i] is a random 4-byte scatter (a read-modify-write of a whole HBM burst). Large
     // rounds write only the ranks of i < ihi here and leave every update in list order in
-    // `later` for the split passes (k_rank_upper) or the staged scatter (k_rank_stage /
-    // k_rank_apply); small ones write rank directly (ihi = ~0, no `later`).
-    const uint32_t rv = same ? 0xffffffffu : gbase + hp + o + 1u;  // (gbase: a split block's bucket)
-    if (!same && i < ihi)
+    // `later` for the split passes (k_rank_upper) or the staged scatter (k_rank_apply); small
+    // ones write rank directly (ihi = ~0, no `later`). The entry that keeps its old head's
+    // place keeps its rank.
+    const bool keep = same && rpos == hp + o;
+    const uint32_t rv = keep ? 0xffffffffu : gbase + rpos + 1u;  // (gbase: a split block's bucket)
+    if (!keep && i < ihi)
         rank[i] = rv;
     if (later)
         later[c] = rv;
-    if (size == 1) {
-        sa[c + o] = i;
+    if (size == 1 || pair) {
+        sa[slot] = i;
     } else {
         // compact index = survivor entries before c, new group id = survivor heads up to c - 1
         uint64_t se, sh;
-        surv_masks(hb, c >> 6, m, se, sh);
+        surv_masks(hb, pf, c >> 6, m, se, sh);
         const uint64_t pw = P[c >> 6], below = (1ull << (c & 63u)) - 1ull;
         const uint32_t idx = (uint32_t)(pw >> 32) + (uint32_t)__popcll(se & below);
         const uint32_t ng = (uint32_t)pw + (uint32_t)__popcll(sh & (below | (below + 1ull))) - 1u;
@@ -393,7 +507,10 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
             pos = (uint32_t)c + o;
             // (same group, so the same block: e1 bounds both suffixes)
             if (!bad_index(i >= e1 || j >= e1 || pos >= bl.nsa() || e1 - mx < hk, err, kErrCommit)) {
-                lim = umin_(hk, e1 - mx - hk);
+                // Up to the end of the text: the keys differ, so normally within hk bytes, but
+                // a pair finished early (k_pairs) carries final ranks, which can split two
+                // suffixes whose next hk bytes still agree.
+                lim = e1 - mx - hk;
                 if (hk <= kLcpLane) {
                     uint32_t l = lim;
                     for (uint32_t off = 0; off < lim; off += 8) {
@@ -1034,6 +1151,13 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // (SALZ_SEG_TINY=0: LSD passes everywhere)
     // (64: 32, 96 and 128 measured within 0.2 ms of it, 32 up to 0.2 ms slower on mixed data)
     const uint32_t seg_tiny = getenv("SALZ_SEG_TINY") ? (uint32_t)atoi(getenv("SALZ_SEG_TINY")) : 64u;
+    // Groups of two finished by a direct compare each round (k_pairs, SALZ_SA_PAIRS=1), from the
+    // round whose groups share SALZ_SA_PAIRS_H bytes on. Off by default: on the text surrogate
+    // it measured even at every threshold (C2 SA 22.2 ms at 64 and 256 bytes, 22.9 from 16,
+    // against 22.2 without; profiles/r03e_pairs_ab.txt): what the smaller late rounds save,
+    // k_pairs and the longer head compares it causes (k_heads_lcp) spend again.
+    const bool pairs_on = getenv("SALZ_SA_PAIRS") && atoi(getenv("SALZ_SA_PAIRS")) != 0;
+    const uint32_t pairs_h = getenv("SALZ_SA_PAIRS_H") ? (uint32_t)atoi(getenv("SALZ_SA_PAIRS_H")) : 64u;
     auto t_round = std::chrono::steady_clock::now();
     for (;;) {
         ws.stats.sa_rounds++;
@@ -1123,6 +1247,19 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         hipLaunchKernelGGL(k_headpos, dim3(grid_for(((size_t)m + 64 * kHpWords - 1) / (64 * kHpWords) * 64, kT)),
                            dim3(kT), 0, st, hb, m, headpos);
         SALZ_LAUNCH_CHECK();
+        // Groups of two decided by a direct compare (k_pairs): pf / pr in scratch that is free
+        // between this round's sort and the next one's (lsc; Kx past k_commit's `later`).
+        uint64_t *pf = nullptr;
+        uint32_t *pr = nullptr;
+        if (pairs_on && h >= pairs_h) {
+            pf = reinterpret_cast<uint64_t *>(ws.lsc);
+            pr = reinterpret_cast<uint32_t *>(Kx) + m;
+            if (verbose)  // (the count is a same-address atomic per wave: diagnostics only)
+                SALZ_HIP(hipMemsetAsync(d32 + 24, 0, sizeof(uint32_t), st));
+            hipLaunchKernelGGL(k_pairs, dim3(grid_for(m, kT)), dim3(kT), 0, st, V, hb, m, bl, h, ws.text, pf, pr,
+                               verbose ? d32 + 24 : nullptr);
+            SALZ_LAUNCH_CHECK();
+        }
         // The host needs G only for the debug checks; no round waits for it.
         const bool need_G = dbg_rounds || verbose;
         uint32_t G = 0;
@@ -1142,7 +1279,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         uint64_t *P = reinterpret_cast<uint64_t *>(ws.u1);
         {
             const size_t nw = ((size_t)m + 63) / 64;
-            hipLaunchKernelGGL(k_surv, dim3(grid_for(nw, kT)), dim3(kT), 0, st, hb, m, P);
+            hipLaunchKernelGGL(k_surv, dim3(grid_for(nw, kT)), dim3(kT), 0, st, hb, pf, m, P);
             SALZ_LAUNCH_CHECK();
             if (scan_sum_u64(P, P, nw, false, d64, ws, st) != 0)
                 return -1;
@@ -1170,7 +1307,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, headpos,
                            P, reinterpret_cast<unsigned long long *>(d64 + 1), offo, offn, Vx, ngid, ws.rank,
                            ws.sa, tab, m, n, nsa, kb_old,
-                           round0, derr, ihi, mode ? later : nullptr, dist ? dist->gbase : 0u);
+                           round0, derr, ihi, mode ? later : nullptr, dist ? dist->gbase : 0u, pf, pr,
+                           ws.lcps_ok ? ws.lcps : nullptr, h);
         SALZ_LAUNCH_CHECK();
         for (uint32_t q = 1; q < parts; q++) {
             hipLaunchKernelGGL(k_rank_upper, dim3(grid_for(m, kT)), dim3(kT), 0, st, V, later, m,
@@ -1215,9 +1353,10 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         }
         if (verbose) {  // the round's wall time (this round synchronised with the host twice)
             const auto now = std::chrono::steady_clock::now();
-            fprintf(stderr, "sa round %d (%s) h=%u m=%u (large %u in %u groups) groups=%u -> "
+            fprintf(stderr, "sa round %d (%s) h=%u m=%u (large %u in %u groups) groups=%u pairs=%u -> "
                     "survivors %u in %u groups  %.3f ms\n", ws.stats.sa_rounds, how, h, m, mL, GL, G,
-                    mnew, Gnew, std::chrono::duration<double, std::milli>(now - t_round).count());
+                    pairs_on ? reinterpret_cast<uint32_t *>(ws.hscal)[24] : 0u, mnew, Gnew,
+                    std::chrono::duration<double, std::milli>(now - t_round).count());
             t_round = now;
         }
         if (dist) {  // a split block ends when every rank's bucket is sorted

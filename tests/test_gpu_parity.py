@@ -233,7 +233,7 @@ def test_encode_blocks_container(salz, block, size):
     assert salz.decode_blocks(got, size) == src.tobytes()
 
 
-@pytest.mark.parametrize("keys", ["1", "0", "1d0", "1t0", "1s0", "1s2048"])
+@pytest.mark.parametrize("keys", ["1", "0", "1d0", "1t0", "1s0", "1s2048", "1p1", "0p1", "1p8"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
                                                ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
@@ -246,8 +246,12 @@ def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
     unique suffix array; the radix histograms from the digit bytes (the default) or from the
     keys ("1d0", SALZ_RADIX_DIGITS=0); round 0's first pass from the text (the default) or from
     the materialised list ("1t0", SALZ_TEXT_FIRST=0); LDS windows placed by counting up to the
-    default group size, never ("1s0") or always ("1s2048", SALZ_SEG_TINY)."""
+    default group size, never ("1s0") or always ("1s2048", SALZ_SEG_TINY); groups of two kept in
+    the doubling (the default) or finished by a direct compare (k_pairs, SALZ_SA_PAIRS=1) from
+    depth 64 ("1p1", "0p1") or from round 0 ("1p8", SALZ_SA_PAIRS_H=8)."""
     monkeypatch.setenv("SALZ_SA_MODE", mode)
+    monkeypatch.setenv("SALZ_SA_PAIRS", "1" if "p" in keys else "0")
+    monkeypatch.setenv("SALZ_SA_PAIRS_H", "8" if keys.endswith("p8") else "64")
     monkeypatch.setenv("SALZ_ALPHA", keys[0])
     monkeypatch.setenv("SALZ_RADIX_DIGITS", "0" if keys == "1d0" else "1")
     monkeypatch.setenv("SALZ_TEXT_FIRST", "0" if keys == "1t0" else "1")
@@ -476,7 +480,7 @@ def test_cli_streams_gigabyte_file_with_bounded_memory(salz, tmp_path):
     # the reference point: a file just long enough to fill every encoder slot and the whole
     # block ring (contexts and ring buffers are created lazily, so a one-block file uses less)
     small = tmp_path / "small.txt"
-    gen("text", 8 * block + 3, 21).tofile(small)
+    gen("text", 8 * block + 1003, 21).tofile(small)  # (a trailing block of <= 8 bytes fails)
     rc, rss0 = _run_rss([cli, "-9", "-k", "-q", str(small)])
     assert rc == 0
     rc, rss0_d = _run_rss([cli, "-d", "-q", "-f", str(tmp_path / "small.txt.salz")])
