@@ -295,7 +295,7 @@ __device__ __forceinline__ uint64_t round0_key_mapped(const uint8_t *Tm, uint32_
 {
     const uint32_t left = e - i;
     uint64_t key = 0;
-    if (a.k == 8) {  // the usual text case: straight-line, so the loads of a thread's items batch
+    if (a.k == 8 || a.k == 9) {  // the usual text cases: straight-line, so the loads of a thread's items batch
         uint64_t w = load_u64_any(Tm, i);
         if (left < 8)
             w &= (1ull << (8u * left)) - 1ull;
@@ -305,7 +305,12 @@ __device__ __forceinline__ uint64_t round0_key_mapped(const uint8_t *Tm, uint32_
         uint64_t x = __builtin_bswap64(w);
         x = (x & 0x00FF00FF00FF00FFull) | (((x >> 8) & 0x00FF00FF00FF00FFull) << b);
         x = (x & 0x0000FFFF0000FFFFull) | (((x >> 16) & 0x0000FFFF0000FFFFull) << (2 * b));
-        return (x & 0xFFFFFFFFull) | ((x >> 32) << (4 * b));
+        x = (x & 0xFFFFFFFFull) | ((x >> 32) << (4 * b));
+        if (a.k == 9) {  // a ninth symbol (7-bit alphabets: 63 bits), zero past the end
+            const uint32_t s9 = Tm[(size_t)i + 8];  // (unconditional: the buffer is padded)
+            x = (x << b) | (left > 8 ? s9 : 0u);
+        }
+        return x;
     }
     for (uint32_t j0 = 0; j0 < a.k; j0 += 8) {
         uint64_t w = load_u64_any(Tm, (size_t)i + j0);

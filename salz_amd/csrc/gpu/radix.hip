@@ -76,19 +76,19 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
             if (i < left)
                 atomicAdd(&mine[digit_of(2, 0, vals[base + i], shift, txt.g)], 1u);
         }
-    } else if (kMode == 1 && shift == 0 && (txt.a.bits == 0 || txt.a.k == 8)) {
-        // Round 0's first digit is its key's low byte: the 8th byte (raw keys), or the 8th
-        // symbol with the low bits of the 7th (8 symbols of >= 5 bits): two byte loads per
-        // suffix instead of the whole key. Loads unconditional (the text is padded), past the
-        // suffix's end masked to 0 like the key's bytes.
-        const uint32_t b = txt.a.bits;
+    } else if (kMode == 1 && shift == 0 && (txt.a.bits == 0 || ((txt.a.k == 8 || txt.a.k == 9) && txt.a.bits >= 4))) {
+        // Round 0's first digit is its key's low byte: the 8th byte (raw keys), or the last
+        // symbol with the low bits of the one before (8 or 9 symbols of >= 4 bits): two byte
+        // loads per suffix instead of the whole key. Loads unconditional (the text is padded),
+        // past the suffix's end masked to 0 like the key's bytes.
+        const uint32_t b = txt.a.bits, kl = txt.a.bits ? txt.a.k - 1u : 7u;
         uint32_t d[kItems];
 #pragma unroll
         for (int j = 0; j < kItems; j++) {
             const size_t idx = (size_t)j * kThreads + tid;
             const uint32_t i = init_suffix(idx < left ? base + idx : 0, txt.g), e = txt.g.end(i);
-            const uint32_t t7 = txt.T[(size_t)i + 7], t6 = txt.T[(size_t)i + 6];
-            const uint32_t s7 = i + 7u < e ? t7 : 0u, s6 = b && i + 6u < e ? t6 : 0u;
+            const uint32_t t7 = txt.T[(size_t)i + kl], t6 = txt.T[(size_t)i + kl - 1u];
+            const uint32_t s7 = i + kl < e ? t7 : 0u, s6 = b && i + kl - 1u < e ? t6 : 0u;
             d[j] = (s7 | (s6 << b)) & 255u;
         }
 #pragma unroll
