@@ -304,32 +304,28 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
             sR[d - 1] = vsa[kB + l + d];
             cR[d - 1] = vlc[kB + l + d];
         }
-        uint32_t lmP = vlc[kB + l], lm = lmP, hitP = kInf, pvP = 0;
+        // The first hit per side as the lowest bit of a 16-bit mask of "smaller" tests (bounded
+        // to the block), then the LCP minimum up to it: two compare-and-select sweeps per side
+        // instead of one sequential chain of live / hit / minimum selects per neighbour.
+        uint32_t mP = 0, mN = 0;
 #pragma unroll
-        for (uint32_t d = 1; d <= kNear; d++) {
-            const bool live = hitP == kInf && d <= l;
-            if (live && sL[d - 1] < v) {
-                hitP = l - d;
-                pvP = sL[d - 1];
-                lmP = lm;
-            }
-            if (live)
-                lm = umin(lm, cL[d - 1]);
+        for (uint32_t d = 0; d < kNear; d++) {
+            mP |= (sL[d] < v ? 1u : 0u) << d;
+            mN |= (sR[d] < v ? 1u : 0u) << d;
         }
-        uint32_t lmN = kInf, hitN = kInf, pvN = 0;
-        lm = kInf;
+        mP &= l >= kNear ? 0xffffu : (1u << l) - 1u;                          // d <= l
+        mN &= kB - 1u - l >= kNear ? 0xffffu : (1u << (kB - 1u - l)) - 1u;  // l + d < kB
+        const uint32_t dP = mP ? (uint32_t)__builtin_ctz(mP) : kNear, dN = mN ? (uint32_t)__builtin_ctz(mN) : kNear;
+        // PSV: LCP minimum over (r', r] = LCP[r] and the neighbours passed over; NSV: over
+        // (r, r'] = the neighbours up to and including the hit
+        uint32_t lmP = vlc[kB + l], lmN = kInf;
 #pragma unroll
-        for (uint32_t d = 1; d <= kNear; d++) {
-            const bool live = hitN == kInf && l + d < kB;
-            if (live) {
-                lm = umin(lm, cR[d - 1]);
-                if (sR[d - 1] < v) {
-                    hitN = l + d;
-                    pvN = sR[d - 1];
-                    lmN = lm;
-                }
-            }
+        for (uint32_t d = 0; d < kNear; d++) {
+            lmP = d < dP ? umin(lmP, cL[d]) : lmP;
+            lmN = d <= dN ? umin(lmN, cR[d]) : lmN;
         }
+        const uint32_t hitP = mP ? l - dP - 1u : kInf, hitN = mN ? l + dN + 1u : kInf;
+        const uint32_t pvP = mP ? vsa[kB + hitP] : 0u, pvN = mN ? vsa[kB + hitN] : 0u;
         const uint32_t slot = slot_of(l);
         sp[slot] = v;
         if (hitP != kInf && hitN != kInf) {
