@@ -304,7 +304,7 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
             sR[d - 1] = vsa[kB + l + d];
             cR[d - 1] = vlc[kB + l + d];
         }
-        // The first hit per side as the lowest bit of a 16-bit mask of "smaller" tests (bounded
+        // The first hit per side as the lowest bit of a kNear-bit mask of "smaller" tests (bounded
         // to the block), then the LCP minimum up to it: two compare-and-select sweeps per side
         // instead of one sequential chain of live / hit / minimum selects per neighbour.
         uint32_t mP = 0, mN = 0;
@@ -313,8 +313,9 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
             mP |= (sL[d] < v ? 1u : 0u) << d;
             mN |= (sR[d] < v ? 1u : 0u) << d;
         }
-        mP &= l >= kNear ? 0xffffu : (1u << l) - 1u;                          // d <= l
-        mN &= kB - 1u - l >= kNear ? 0xffffu : (1u << (kB - 1u - l)) - 1u;  // l + d < kB
+        constexpr uint32_t kAll = kNear >= 32 ? 0xffffffffu : (1u << kNear) - 1u;
+        mP &= l >= kNear ? kAll : (1u << l) - 1u;                          // d <= l
+        mN &= kB - 1u - l >= kNear ? kAll : (1u << (kB - 1u - l)) - 1u;  // l + d < kB
         const uint32_t dP = mP ? (uint32_t)__builtin_ctz(mP) : kNear, dN = mN ? (uint32_t)__builtin_ctz(mN) : kNear;
         // PSV: LCP minimum over (r', r] = LCP[r] and the neighbours passed over; NSV: over
         // (r, r'] = the neighbours up to and including the hit
