@@ -95,3 +95,31 @@ def test_shards_cover_every_block_once():
         for nb in (1, 7, 15, 16):
             seen = sorted(b for r in range(world) for b in my_blocks(nb, r, world))
             assert seen == list(range(nb))
+
+
+def _world1_worker(port, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    from salz_amd.dist import gather_container, header
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        packed = torch.arange(40, dtype=torch.uint8)
+        out = gather_container(packed, 37, 1 << 20, 0, 1)
+        q.put(bytes(out.numpy().tobytes()) == header(1 << 20) + bytes(range(37)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_container_world1_process_group():
+    """With a process group initialised at world 1 (bench.py --launch), the exchange step runs
+    its collectives (all-gather of the run length) and still yields header + the rank's run."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_world1_worker, args=(_free_port(), q))
+    p.start()
+    ok = q.get(timeout=120)
+    p.join(timeout=60)
+    assert ok and p.exitcode == 0
