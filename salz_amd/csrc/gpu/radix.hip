@@ -201,34 +201,37 @@ __global__ __launch_bounds__(kRowThreads) void k_radix_rowscan(uint32_t *__restr
         totals[blockIdx.x] = carry;
 }
 
-template <int kMode>
-__global__ __launch_bounds__(kThreads) void k_radix_scatter(
+// TH threads per 4096-element tile (256: 16 items per thread; 512: 8 items, half the registers
+// per thread and twice the waves per CU for the same LDS).
+template <int kMode, int TH>
+__global__ __launch_bounds__(TH) void k_radix_scatter(
     const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
     uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t m, int shift,
     const uint32_t *__restrict__ offs, uint32_t ntiles, const uint32_t *__restrict__ totals,
     TextSrc txt, uint8_t *__restrict__ dout, int nshift)
 {
+    constexpr int IT = kTile / TH, NW = TH / 64;
     // Keys and values are staged one after the other in the same 32 KB (4 workgroups per CU
     // instead of 2 with a 48 KB key + value stage).
     __shared__ uint64_t skey[kTile];
     uint32_t *sval = reinterpret_cast<uint32_t *>(skey);
-    __shared__ uint32_t cnt[4][256];
+    __shared__ uint32_t cnt[NW][256];
     __shared__ uint32_t dstart[256];
     __shared__ uint32_t gbase[256];
-    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t wsum[2][4];
 
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    for (int i = tid; i < 4 * 256; i += kThreads)
+    for (int i = tid; i < NW * 256; i += TH)
         (&cnt[0][0])[i] = 0;
     __syncthreads();
 
-    // Warp-striped: wave w owns tile elements [w*1024, (w+1)*1024), item j covers 64 of them.
-    const size_t base = (size_t)blockIdx.x * kTile + (size_t)wave * (kItems * 64);
-    uint64_t k[kItems];
-    uint32_t v[kItems];
-    uint32_t lrank[kItems];
+    // Warp-striped: wave w owns tile elements [w*IT*64, (w+1)*IT*64), item j covers 64 of them.
+    const size_t base = (size_t)blockIdx.x * kTile + (size_t)wave * (IT * 64);
+    uint64_t k[IT];
+    uint32_t v[IT];
+    uint32_t lrank[IT];
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < IT; j++) {
         size_t i = base + (size_t)j * 64 + lane;
         bool ok = i < m;
         if (kMode == 1) {  // unconditional text loads (clamped entry)
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     }
 
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < IT; j++) {
         size_t i = base + (size_t)j * 64 + lane;
         bool ok = i < m;
         unsigned d = digit_of(kMode, k[j], v[j], shift, txt.g);
@@ -269,54 +272,54 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     }
     __syncthreads();
 
-    // Digit bases: exclusive scan of the 256 digit totals (thread = digit).
-    {
-        const uint32_t t = totals[tid];
-        uint32_t x = t;
+    // Digit bases (exclusive scan of the 256 digit totals) and the tile-local digit starts
+    // (exclusive scan of the per-digit tile counts), thread = digit; the per-wave counts become
+    // per-wave starts.
+    const bool dg = tid < 256;
+    uint32_t xt = 0, xc = 0, tt = 0, tot = 0;
+    if (dg) {
+        tt = totals[tid];
+#pragma unroll
+        for (int w = 0; w < NW; w++)
+            tot += cnt[w][tid];
+        xt = tt;
+        xc = tot;
 #pragma unroll
         for (unsigned dd = 1; dd < 64; dd <<= 1) {
-            uint32_t y = shfl_up_u32(x, dd);
-            if (lane >= dd)
-                x += y;
+            const uint32_t yt = shfl_up_u32(xt, dd), yc = shfl_up_u32(xc, dd);
+            if (lane >= dd) {
+                xt += yt;
+                xc += yc;
+            }
         }
-        if (lane == 63)
-            wsum[wave] = x;
-        __syncthreads();
-        uint32_t pre = 0;
-        for (unsigned w = 0; w < wave; w++)
-            pre += wsum[w];
-        gbase[tid] = pre + x - t + offs[(size_t)tid * ntiles + blockIdx.x];
-        __syncthreads();
+        if (lane == 63) {
+            wsum[0][wave] = xt;
+            wsum[1][wave] = xc;
+        }
     }
-    // Per digit (thread = digit): wave prefixes and tile-local digit starts.
-    {
-        uint32_t c0 = cnt[0][tid], c1 = cnt[1][tid], c2 = cnt[2][tid], c3 = cnt[3][tid];
-        uint32_t tot = c0 + c1 + c2 + c3;
-        // block exclusive scan of tot over 256 digits
-        uint32_t x = tot;
-#pragma unroll
-        for (unsigned dd = 1; dd < 64; dd <<= 1) {
-            uint32_t y = shfl_up_u32(x, dd);
-            if (lane >= dd)
-                x += y;
+    __syncthreads();
+    if (dg) {
+        uint32_t pt = 0, pc = 0;
+        for (unsigned w = 0; w < wave; w++) {
+            pt += wsum[0][w];
+            pc += wsum[1][w];
         }
-        if (lane == 63)
-            wsum[wave] = x;
-        __syncthreads();
-        uint32_t pre = 0;
-        for (unsigned w = 0; w < wave; w++)
-            pre += wsum[w];
-        dstart[tid] = pre + x - tot;
-        cnt[0][tid] = 0;
-        cnt[1][tid] = c0;
-        cnt[2][tid] = c0 + c1;
-        cnt[3][tid] = c0 + c1 + c2;
+        gbase[tid] = pt + xt - tt + offs[(size_t)tid * ntiles + blockIdx.x];
+        const uint32_t ds = pc + xc - tot;
+        dstart[tid] = ds;
+        uint32_t run = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            const uint32_t c = cnt[w][tid];
+            cnt[w][tid] = run;
+            run += c;
+        }
     }
     __syncthreads();
 
     if (kMode == 2) {  // block passes (a batch's round 0 only): scatter from registers
 #pragma unroll
-        for (int j = 0; j < kItems; j++) {
+        for (int j = 0; j < IT; j++) {
             const size_t i = base + (size_t)j * 64 + lane;
             const unsigned d = digit_of(2, 0, v[j], shift, txt.g);
             if (i < m) {
@@ -327,9 +330,9 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
         }
         return;
     }
-    uint32_t pos[kItems];  // tile-local sorted position of each item
+    uint32_t pos[IT];  // tile-local sorted position of each item
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < IT; j++) {
         size_t i = base + (size_t)j * 64 + lane;
         unsigned d = (unsigned)(k[j] >> shift) & 255u;
         pos[j] = dstart[d] + cnt[wave][d] + lrank[j];
@@ -340,10 +343,10 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
 
     size_t tbase = (size_t)blockIdx.x * kTile;
     uint32_t tcount = (uint32_t)((m - tbase) < (size_t)kTile ? (m - tbase) : (size_t)kTile);
-    uint32_t gdst[kItems];  // global destination of staged slot tid + j * kThreads
+    uint32_t gdst[IT];  // global destination of staged slot tid + j * TH
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
-        const uint32_t s = tid + (uint32_t)j * kThreads;
+    for (int j = 0; j < IT; j++) {
+        const uint32_t s = tid + (uint32_t)j * TH;
         if (s < tcount) {
             uint64_t key = skey[s];
             unsigned d = (unsigned)(key >> shift) & 255u;
@@ -355,15 +358,15 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     }
     __syncthreads();  // keys out of LDS; the same bytes now stage the values
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < IT; j++) {
         size_t i = base + (size_t)j * 64 + lane;
         if (i < m)
             sval[pos[j]] = v[j];
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
-        const uint32_t s = tid + (uint32_t)j * kThreads;
+    for (int j = 0; j < IT; j++) {
+        const uint32_t s = tid + (uint32_t)j * TH;
         if (s < tcount)
             vout[gdst[j]] = sval[s];
     }
@@ -391,6 +394,9 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     // (stable), so the list is ordered by (block, key).
     const int blk_bits = blocks && g.nb > 1 ? bit_width(g.nb - 1u) : 0;
     const int passes_key = (bit_hi - bit_lo + 7) / 8, passes = passes_key + (blk_bits + 7) / 8;
+    // key passes with 512-thread workgroups (8 items per thread; SALZ_RADIX_WG512=0: 256 threads,
+    // 16 items, ~0.5% slower on C2, profiles/r03h_tm_radix_ab.txt)
+    static const bool wg512 = !getenv("SALZ_RADIX_WG512") || atoi(getenv("SALZ_RADIX_WG512")) != 0;
     for (int pass = 0; pass < passes; pass++) {
         const int mode = pass >= passes_key ? 2 : (text && pass == 0) ? 1 : 0;
         const int shift = mode == 2 ? 8 * (pass - passes_key) : bit_lo + 8 * pass;
@@ -421,13 +427,16 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
         if (timed)
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used], st));
         if (mode == 1)
-            hipLaunchKernelGGL(k_radix_scatter<1>, dim3(ntiles), dim3(kThreads), 0, st, kin,
+            hipLaunchKernelGGL((k_radix_scatter<1, kThreads>), dim3(ntiles), dim3(kThreads), 0, st, kin,
                                vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
         else if (mode == 2)
-            hipLaunchKernelGGL(k_radix_scatter<2>, dim3(ntiles), dim3(kThreads), 0, st, kin,
+            hipLaunchKernelGGL((k_radix_scatter<2, kThreads>), dim3(ntiles), dim3(kThreads), 0, st, kin,
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
+        else if (wg512)
+            hipLaunchKernelGGL((k_radix_scatter<0, 512>), dim3(ntiles), dim3(512), 0, st, kin,
                                vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
         else
-            hipLaunchKernelGGL(k_radix_scatter<0>, dim3(ntiles), dim3(kThreads), 0, st, kin,
+            hipLaunchKernelGGL((k_radix_scatter<0, kThreads>), dim3(ntiles), dim3(kThreads), 0, st, kin,
                                vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
         SALZ_LAUNCH_CHECK();
         if (timed) {
