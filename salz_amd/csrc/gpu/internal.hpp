@@ -52,6 +52,10 @@ struct ParseState {
     uint32_t levels;        // pointer-jumping levels
     bool snaps;             // all levels stored at jt0 + k*n_exit (else emission recomputes
                             // them from level 0 in two ping-pong buffers)
+    // lazy costs at the end of the parse (cost is then null until parse_materialize_cost):
+    // cost = lzC + lzL[chunk], written into lzD
+    uint32_t *lzC = nullptr, *lzL = nullptr, *lzD = nullptr;
+    uint32_t lzn = 0;
 };
 
 struct Workspace {
@@ -177,6 +181,7 @@ int stage_suffix_array_dc3(Workspace &ws, const Blocks &bl, const Alpha &codes, 
 int stage_lcp(Workspace &ws, const Blocks &bl, uint32_t *lcp_out); // lcp.hip  -> lcp[r]
 int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp);  // ansv.hip -> ws.cand
 int stage_parse(Workspace &ws, const Blocks &bl);                  // parse.hip
+int parse_materialize_cost(Workspace &ws);                         // parse.hip: lazy costs -> parse.cost
 uint32_t parse_chunk_log(size_t N);                                // parse.hip: klog for N bytes
 // emit.hip: block b's stream at dst + b * stride (at most cap bytes); lens[b] its length
 int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, size_t stride,

@@ -24,6 +24,7 @@
 #include "internal.hpp"
 
 #include <cstdlib>
+#include <vector>
 
 namespace salz {
 namespace {
@@ -97,26 +98,40 @@ constexpr uint32_t kCDepth = 7;
 // lane reads its chunk's first state instead and `same` tells the step to reuse p + 1's value.
 __device__ __forceinline__ uint64_t far_load(const uint64_t *pst, const uint32_t *cin, size_t base,
                                              uint32_t a, uint32_t b, uint32_t klog, uint32_t p,
-                                             uint32_t len, uint32_t n, uint32_t &lq, uint32_t &same)
+                                             uint32_t len, uint32_t n, uint32_t &lq, uint32_t &same,
+                                             uint32_t &li)
 {
     const bool far = len > kWin && p < n && len <= n - p;  // (inert steps past n: never far)
     same = far && p + len == lq ? 1u : 0u;
     lq = far ? p + len : 0xffffffffu;
     const uint32_t q = far && !same ? p + len : a;
+    li = q >> klog;  // lazy costs: the chunk whose offset applies to a target past the chunk
     const uint64_t *addr = q < b ? pst + base + ((size_t)(q - a) << 6)
                                  : reinterpret_cast<const uint64_t *>(cin) + (sidx(q, klog) >> 1);
     return *addr;
 }
 
 // (cost << 32 | exit) of target q = p + len from its raw load; sidx(q) is odd iff its chunk
-// q >> klog is (the lane bit of the interleaved layout).
-__device__ __forceinline__ uint64_t far_decode(uint64_t raw, uint32_t q, uint32_t b, uint32_t klog)
+// q >> klog is (the lane bit of the interleaved layout). lv: the lazy offset of q's chunk (0
+// outside the lazy passes).
+__device__ __forceinline__ uint64_t far_decode(uint64_t raw, uint32_t q, uint32_t b, uint32_t klog, uint32_t lv)
 {
     if (q < b)
         return raw;
-    const uint32_t v = ((q >> klog) & 1u) ? (uint32_t)(raw >> 32) : (uint32_t)raw;
+    const uint32_t v = (((q >> klog) & 1u) ? (uint32_t)(raw >> 32) : (uint32_t)raw) + lv;
     return ((uint64_t)v << 32) | q;
 }
+
+// Lazy costs (the late passes, DESIGN.md "Parse"): the exact cost of position q is
+// C[sidx(q)] + L[q >> klog]. A chunk whose decisions did not change and whose exits all moved by
+// one delta only adds the delta to its L word instead of rewriting its K costs.
+struct Lazy {
+    const uint32_t *L;    // per chunk offset (null outside the lazy passes)
+    uint32_t *summ;       // per chunk: its first kSumm distinct exits and an overflow flag
+    uint8_t *chg;         // per chunk: a decision changed in this pass's walk
+};
+constexpr uint32_t kSumm = 8;
+constexpr uint32_t kSummW = kSumm + 1;  // words per chunk
 
 // wdirty (from the third pass on): one flag per wave of 64 chunks; a clean wave's chunks
 // would repeat their decisions (k_parse_mark), so they only carry their choices over, and
@@ -127,12 +142,14 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
     uint64_t *__restrict__ pst,
     const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, Blocks bl, uint32_t klog,
     uint32_t *__restrict__ changed, uint32_t *err, uint8_t *__restrict__ eflag,
-    const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum, uint32_t *__restrict__ reach)
+    const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum, uint32_t *__restrict__ reach,
+    uint32_t *__restrict__ rlo, Lazy lz)
 {
     const uint32_t c = blockIdx.x * kT + threadIdx.x;  // chunk
     const uint64_t a64 = (uint64_t)c << klog;
     uint32_t diff = 0, errw = 0;
     uint32_t far_end = 0;  // farthest candidate target (first pass: k_parse_mark's range test)
+    uint32_t reach_lo = 0;  // first position with a factor target at or past the chunk end
     if (c == 0)
         eflag[sidx(n, klog)] = 1u;  // the root of the exit forest
     if (a64 < n) {
@@ -148,6 +165,8 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         if (wdirty && !wdirty[c >> 6]) {  // wave-uniform: a clean wave
             for (uint32_t j = 0; j < b - a; j++)
                 chnew[slot(j)] = chold[slot(j)];
+            if (lz.chg)
+                lz.chg[c] = 0;
             return;
         }
         if (dsum)
@@ -160,6 +179,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         typename C::T cr[kCDepth + 1];
         uint8_t orr[kDepth];
         uint64_t fP[kDepth], fN[kDepth];
+        uint32_t lP[kDepth], lN[kDepth];  // lazy offsets of the far targets' chunks
         uint64_t win[kWin];  // win[k] = state of p + 1 + k
         const uint32_t pK = a + K - 1;
         // ring bit k: the far target of position p - k equals p - k + 1's (value reused)
@@ -171,20 +191,27 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
 #pragma unroll
         for (uint32_t k = 0; k < kDepth; k++) {
             orr[k] = chold[slot(K - 1 - k)];
-            uint32_t sp, sn;
-            fP[k] = far_load(pst, cin, base, a, b, klog, pK - k, C::lp(cr[k]), n, lqP, sp);
-            fN[k] = far_load(pst, cin, base, a, b, klog, pK - k, C::ln(cr[k]), n, lqN, sn);
+            uint32_t sp, sn, ip, in;
+            fP[k] = far_load(pst, cin, base, a, b, klog, pK - k, C::lp(cr[k]), n, lqP, sp, ip);
+            fN[k] = far_load(pst, cin, base, a, b, klog, pK - k, C::ln(cr[k]), n, lqN, sn, in);
+            lP[k] = lz.L ? lz.L[ip] : 0u;
+            lN[k] = lz.L ? lz.L[in] : 0u;
             sameP |= sp << k;
             sameN |= sn << k;
         }
 #pragma unroll
         for (uint32_t k = 0; k < kWin; k++) {  // states a + K .. a + K + kWin - 1 (past n: unused)
-            const uint32_t q = a + K + k;
-            const uint32_t v = cin[sidx(q <= n ? q : n, klog)];
+            const uint32_t q = a + K + k, qq = q <= n ? q : n;
+            const uint32_t v = cin[sidx(qq, klog)] + (lz.L ? lz.L[qq >> klog] : 0u);
             win[k] = q <= n ? (((uint64_t)v << 32) | q) : 0;
         }
         uint32_t last_ex = 0xffffffffu;
+        uint32_t exs[kSumm], nex = 0, tex = 0xffffffffu;  // distinct exits (lz.summ)
+#pragma unroll
+        for (uint32_t k = 0; k < kSumm; k++)
+            exs[k] = 0xffffffffu;
         far_end = b;
+        reach_lo = b;
 #pragma unroll 8
         for (uint32_t j = K; j-- > 0;) {
             const uint32_t p = a + j;
@@ -197,6 +224,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
                 const uint32_t tp = live && lenP >= 3u ? p + lenP : 0u, tn = live && lenN >= 3u ? p + lenN : 0u;
                 far_end = tp > far_end ? tp : far_end;
                 far_end = tn > far_end ? tn : far_end;
+                reach_lo = tp >= b || tn >= b ? p : reach_lo;
             }
             uint32_t best = 9u + (uint32_t)(win[0] >> 32), ex = (uint32_t)win[0];
             uint8_t ch = 0;
@@ -210,7 +238,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
                         for (uint32_t k = 2; k < kWin; k++)
                             t = lenP == k + 1 ? win[k] : t;
                     } else {
-                        t = (sameP & 1u) ? prevP : far_decode(fP[0], p + lenP, b, klog);
+                        t = (sameP & 1u) ? prevP : far_decode(fP[0], p + lenP, b, klog, lP[0]);
                         prevP = t;
                     }
                     const uint32_t alt = C::bp(c0) + (uint32_t)(t >> 32);
@@ -229,7 +257,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
                         for (uint32_t k = 2; k < kWin; k++)
                             t = lenN == k + 1 ? win[k] : t;
                     } else {
-                        t = (sameN & 1u) ? prevN : far_decode(fN[0], p + lenN, b, klog);
+                        t = (sameN & 1u) ? prevN : far_decode(fN[0], p + lenN, b, klog, lN[0]);
                         prevN = t;
                     }
                     const uint32_t alt = C::bn(c0) + (uint32_t)(t >> 32);
@@ -255,6 +283,19 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             // share one line instead of each touching its own.
             eflag[sidx(ex != last_ex ? ex : n, klog)] = 1u;
             last_ex = ex;
+            if (lz.summ && live && ex != tex) {  // (consecutive positions mostly share their exit)
+                tex = ex;
+                bool seen = false;
+#pragma unroll
+                for (uint32_t k = 0; k < kSumm; k++)
+                    seen |= exs[k] == ex;
+                if (!seen) {
+#pragma unroll
+                    for (uint32_t k = 0; k < kSumm; k++)
+                        exs[k] = k == nex ? ex : exs[k];
+                    nex++;
+                }
+            }
             // shift the window and the rings one position down
 #pragma unroll
             for (uint32_t k = kWin - 1; k > 0; k--)
@@ -268,6 +309,8 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
                 orr[k] = orr[k + 1];
                 fP[k] = fP[k + 1];
                 fN[k] = fN[k + 1];
+                lP[k] = lP[k + 1];
+                lN[k] = lN[k + 1];
             }
             // new loads (unconditional, clamped): position p - kDepth's old choice and far
             // targets (its candidate, cr[kDepth - 1], was loaded four steps ago), and position
@@ -275,16 +318,28 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             const uint32_t jd = j >= kDepth ? j - kDepth : 0u;
             const typename C::T cd = cr[kDepth - 1];
             orr[kDepth - 1] = chold[slot(jd)];
-            uint32_t sp, sn;
-            fP[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, C::lp(cd), n, lqP, sp);
-            fN[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, C::ln(cd), n, lqN, sn);
+            uint32_t sp, sn, ip, in;
+            fP[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, C::lp(cd), n, lqP, sp, ip);
+            fN[kDepth - 1] = far_load(pst, cin, base, a, b, klog, a + jd, C::ln(cd), n, lqN, sn, in);
+            lP[kDepth - 1] = lz.L ? lz.L[ip] : 0u;
+            lN[kDepth - 1] = lz.L ? lz.L[in] : 0u;
             sameP = (sameP >> 1) | (sp << (kDepth - 1));
             sameN = (sameN >> 1) | (sn << (kDepth - 1));
             cr[kCDepth] = cand[slot(j >= kCDepth + 1 ? j - kCDepth - 1 : 0u)];
         }
+        if (lz.summ) {  // (unused entries repeat the first exit)
+#pragma unroll
+            for (uint32_t k = 0; k < kSumm; k++)
+                lz.summ[kSummW * (size_t)c + k] = exs[k] != 0xffffffffu ? exs[k] : exs[0];
+            lz.summ[kSummW * (size_t)c + kSumm] = nex > kSumm ? 1u : 0u;
+        }
+        if (lz.chg)
+            lz.chg[c] = diff != 0 ? 1u : 0u;
     }
-    if (reach && a64 < n)
+    if (reach && a64 < n) {
         reach[c] = far_end;
+        rlo[c] = reach_lo;
+    }
     if (errw)
         atomicOr(err, errw);  // a candidate past the end (reported once per lane)
     // one atomic per wave
@@ -336,6 +391,39 @@ __global__ __launch_bounds__(kT) void k_shift_breaks(const uint32_t *__restrict_
 // dirty waves; none left means the fixed point.
 // A chunk whose targets [b, reach] hold no break of the shift (prefix counts pbrk over chunks)
 // passes without looking at its candidates; only the others run the per-candidate test.
+// Lazy passes: the shift of target q since the last test is dl[k] of its chunk k when that chunk
+// was uniform (uni[k]), else D[sidx(q)].
+struct LazyTest {
+    const uint32_t *L;  // null: shifts from the cost arrays cnew - cold
+    const uint8_t *uni;
+    const uint32_t *dl, *D;
+};
+
+// (new cost, shift) of target q <= n; every load unconditional
+__device__ __forceinline__ uint32_t shift_of(const LazyTest &lt, const uint32_t *cnew, const uint32_t *cold,
+                                             uint32_t klog, uint32_t q, uint32_t &v)
+{
+    const size_t sq = sidx(q, klog);
+    if (lt.L) {
+        const uint32_t k = q >> klog;
+        v = cnew[sq] + lt.L[k];
+        const uint32_t dd = lt.D[sq], dk = lt.dl[k];
+        return lt.uni[k] ? dk : dd;
+    }
+    v = cnew[sq];
+    return v - cold[sq];
+}
+
+// Split test (a wave per chunk for the per-candidate part): k_parse_mark decides the chunks its
+// range test passes and lists the others, k_mark_rows tests a listed chunk's candidates with a
+// whole wave (K / 64 rows per lane, one memory latency), k_mark_final sets the wave flags. A wave
+// whose one chunk needs the per-candidate test no longer walks K rows with 64 lanes.
+struct MarkSplit {
+    uint32_t *list, *count;  // chunks left to the per-candidate test
+    uint8_t *cbad;           // per chunk: dirty
+    uint32_t *d0s;           // per chunk: the shift at its end
+};
+
 template <class C>
 __global__ __launch_bounds__(kT) void k_parse_mark(const typename C::T *__restrict__ cand,
                                                    const uint32_t *__restrict__ cnew,
@@ -345,7 +433,9 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const typename C::T *__restri
                                                    uint32_t *__restrict__ dsum,
                                                    uint32_t *__restrict__ ndirty,
                                                    const uint32_t *__restrict__ reach,
-                                                   const uint32_t *__restrict__ pbrk)
+                                                   const uint32_t *__restrict__ pbrk,
+                                                   const uint32_t *__restrict__ rlo, LazyTest lt,
+                                                   MarkSplit ms)
 {
     const uint32_t c = blockIdx.x * kT + threadIdx.x;
     const uint64_t a64 = (uint64_t)c << klog;
@@ -359,9 +449,8 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const typename C::T *__restri
         const uint32_t e = bl.end(a), b0 = bl.start(a);
         const uint32_t b = (e - a) < K ? e : a + K;
         const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
-        const size_t sb = sidx(b, klog);
-        const uint32_t nb = cnew[sb];
-        d0 = nb - cold[sb];
+        uint32_t nb;
+        d0 = shift_of(lt, cnew, cold, klog, b, nb);
         bad = nb >= (1u << 30);
         bool range_ok = false;
         if (reach) {  // breaks in (b, r] lie in chunks c + 1 .. (r - 1) >> klog
@@ -369,8 +458,34 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const typename C::T *__restri
             const uint32_t hi = r > b ? ((r - 1) >> klog) + 1 : c + 1;
             range_ok = pbrk[hi] == pbrk[c + 1];
         }
+        if (ms.list) {  // split test: list the chunk for k_mark_rows, decide in k_mark_final
+            const bool need = !range_ok && !bad;
+            const uint64_t mk = wave_ballot(need);
+            if (mk) {
+                const int leader = (int)__ffsll((unsigned long long)mk) - 1;
+                uint32_t at = 0;
+                if ((int)lane_id() == leader)
+                    at = atomicAdd(ms.count, (uint32_t)__popcll(mk));
+                at = shfl_u32(at, leader);
+                if (need)
+                    ms.list[at + count_below(mk)] = c;
+            }
+            ms.cbad[c] = bad ? 1u : 0u;
+            ms.d0s[c] = d0;
+            return;
+        }
         const uint32_t jn = range_ok ? 0u : b - a;
-        // rows tested: K when some chunk of the wave needs the full test, else none (uniform)
+        // Only rows from the chunk's first factor reaching past b (rlo, from the first pass) have
+        // targets to test; the wave starts at its lowest such row.
+        const uint32_t jl = rlo ? rlo[c] - a : 0u;
+        uint32_t wm = jn ? jl : K;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            const uint32_t o = shfl_xor_u32(wm, m);
+            wm = o < wm ? o : wm;
+        }
+        const uint32_t jstart = wm & ~15u;
+        // rows tested: up to K when some chunk of the wave needs the full test, else none (uniform)
         const uint32_t rows = wave_ballot(jn != 0) != 0 ? K : 0u;
         // K rows for every lane (rows past jn test b itself, which always passes), in batches
         // of 8: a batch's candidates are loaded while the previous batch's costs are checked
@@ -391,22 +506,23 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const typename C::T *__restri
 #pragma unroll
             for (uint32_t u = 0; u < 8; u++) {
                 const uint32_t p = a + j0 + u;
-                const bool on = j0 + u < jn && p != b0;
+                const bool on = j0 + u >= jl && j0 + u < jn && p != b0;
                 const uint32_t lp = C::lp(cd[u]), ln = C::ln(cd[u]);
                 const uint32_t qp = p + lp, qn = p + ln;
                 const bool xp = on && lp >= 3u && qp >= b && qp != lqp;
                 const bool xn = on && ln >= 3u && qn >= b && qn != lqn;
                 lqp = on && lp >= 3u ? qp : 0xffffffffu;
                 lqn = on && ln >= 3u ? qn : 0xffffffffu;
-                const size_t sp = sidx(xp ? qp : b, klog), sn = sidx(xn ? qn : b, klog);
-                const uint32_t vp = cnew[sp], vn = cnew[sn];
-                bad |= vp - cold[sp] != d0 || vp >= (1u << 30);
-                bad |= vn - cold[sn] != d0 || vn >= (1u << 30);
+                uint32_t vp, vn;
+                const uint32_t dp = shift_of(lt, cnew, cold, klog, xp ? qp : b, vp);
+                const uint32_t dn = shift_of(lt, cnew, cold, klog, xn ? qn : b, vn);
+                bad |= dp != d0 || vp >= (1u << 30);
+                bad |= dn != d0 || vn >= (1u << 30);
             }
         };
         CT A[8], B[8];
-        load(A, 0);
-        for (uint32_t j0 = 0; j0 < rows; j0 += 16) {
+        load(A, jstart);
+        for (uint32_t j0 = jstart; j0 < rows; j0 += 16) {
             load(B, j0 + 8);
             check(A, j0);
             load(A, j0 + 16);
@@ -421,6 +537,74 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const typename C::T *__restri
     }
     if (!m && a64 < n)
         dsum[c] += d0;
+}
+
+// A listed chunk's per-candidate test, one wave per chunk (grid-stride over the list): lane l takes
+// rows rlo + l, rlo + l + 64, ... of the chunk, all loads issued before any is used.
+template <class C>
+__global__ __launch_bounds__(kT) void k_mark_rows(const typename C::T *__restrict__ cand,
+                                                  const uint32_t *__restrict__ cnew,
+                                                  const uint32_t *__restrict__ cold, uint32_t n, Blocks bl,
+                                                  uint32_t klog, const uint32_t *__restrict__ rlo, LazyTest lt,
+                                                  MarkSplit ms)
+{
+    const uint32_t lane = lane_id(), nwaves = gridDim.x * (kT / 64);
+    const uint32_t cnt = *ms.count;
+    for (uint32_t w = (blockIdx.x * kT + threadIdx.x) >> 6; w < cnt; w += nwaves) {
+        const uint32_t c = ms.list[w];
+        const uint32_t a = c << klog, K = 1u << klog;
+        const uint32_t e = bl.end(a), b0 = bl.start(a);
+        const uint32_t b = (e - a) < K ? e : a + K;
+        const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
+        const uint32_t d0 = ms.d0s[c];
+        const uint32_t jl = rlo ? rlo[c] - a : 0u, jn = b - a;
+        const uint32_t steps = (jn - jl + 63u) / 64u;  // (wave-uniform)
+        bool bad = false;
+        for (uint32_t i0 = 0; i0 < steps; i0 += 8) {
+            typename C::T cd[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) {
+                const uint32_t j = jl + (i0 + u) * 64u + lane;
+                cd[u] = cand[base + ((size_t)(j < jn ? j : jl) << 6)];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) {
+                const uint32_t j = jl + (i0 + u) * 64u + lane, p = a + j;
+                const bool on = j < jn && p != b0;
+                const uint32_t lp = C::lp(cd[u]), ln = C::ln(cd[u]);
+                const uint32_t qp = p + lp, qn = p + ln;
+                const bool xp = on && lp >= 3u && qp >= b, xn = on && ln >= 3u && qn >= b;
+                uint32_t vp, vn;
+                const uint32_t dp = shift_of(lt, cnew, cold, klog, xp ? qp : b, vp);
+                const uint32_t dn = shift_of(lt, cnew, cold, klog, xn ? qn : b, vn);
+                bad |= dp != d0 || vp >= (1u << 30);
+                bad |= dn != d0 || vn >= (1u << 30);
+            }
+        }
+        if (wave_ballot(bad) && lane == 0)
+            ms.cbad[c] = 1u;
+    }
+}
+
+// Wave flags of the split test: a wave of chunks is clean when none of them is dirty.
+__global__ __launch_bounds__(kT) void k_mark_final(uint32_t n, uint32_t klog, const uint8_t *__restrict__ cbad,
+                                                   const uint32_t *__restrict__ d0s, uint8_t *__restrict__ wdirty,
+                                                   uint32_t *__restrict__ dsum, uint32_t *__restrict__ ndirty)
+{
+    const uint32_t c = blockIdx.x * kT + threadIdx.x;
+    const uint64_t a64 = (uint64_t)c << klog;
+    if ((a64 & ~(((uint64_t)64 << klog) - 1)) >= n)
+        return;  // whole wave past the end
+    const bool in = a64 < n;
+    const bool bad = in && cbad[in ? c : 0];
+    const uint64_t m = wave_ballot(bad);
+    if (lane_id() == 0) {
+        wdirty[c >> 6] = m ? 1u : 0u;
+        if (m)
+            atomicAdd(ndirty, 1u);
+    }
+    if (!m && in)
+        dsum[c] += d0s[c];
 }
 
 // Exit flags (bytes marked by the chunk pass, storage-slot order) -> ExitBits: the set as one
@@ -452,8 +636,10 @@ __global__ __launch_bounds__(kT) void k_compact_exits(ExitBits eb, const uint64_
                                                       const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog,
                                                       size_t S8, uint32_t *__restrict__ elist,
                                                       uint32_t *__restrict__ jt0, uint32_t *__restrict__ js,
-                                                      const uint32_t *__restrict__ dsum)
+                                                      const uint32_t *__restrict__ dsum,
+                                                      const uint32_t *__restrict__ Lz, uint32_t *__restrict__ ce)
 {
+    // (lazy passes: a cost is cin + the chunk's offset Lz; ce = every node's cost before this pass)
     const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
     if (x >= S8)
         return;
@@ -470,7 +656,10 @@ __global__ __launch_bounds__(kT) void k_compact_exits(ExitBits eb, const uint64_
         const uint32_t ev = q == n ? n : (uint32_t)v;
         const size_t se = sidx(ev, klog);
         const uint32_t parent = bits_index(eb.mask, eb.wpre, se);
-        const uint32_t w = (uint32_t)(v >> 32) + dsum[(q < n ? q : 0u) >> klog] - cin[se];
+        const uint32_t lq = Lz ? Lz[q >> klog] : 0u, le = Lz ? Lz[ev >> klog] : 0u;
+        const uint32_t w = (uint32_t)(v >> 32) + dsum[(q < n ? q : 0u) >> klog] - (cin[se] + le);
+        if (ce)
+            ce[xi] = q == n ? 0u : cin[s] + lq;
         elist[xi] = q;
         jt0[xi] = q == n ? xi : parent;
         js[xi] = q == n ? 0u : w;
@@ -546,7 +735,123 @@ __global__ __launch_bounds__(kT) void k_cost_rest(ExitBits eb, const uint32_t *_
     }
 }
 
+// Lazy passes, after the exact costs of the exit set: per chunk, whether its costs all moved by
+// one delta (no decision changed in this pass's walk, at most two distinct exits, both moving by
+// the same delta, both costs under 2^29 so that no cost of the chunk reaches 2^30: a path inside
+// one chunk adds far less) -> Lnew = Lcur + delta; otherwise the chunk is rewritten
+// (k_lazy_rewrite) with offset 0.
+__global__ __launch_bounds__(kT) void k_lazy_chunks(uint32_t nchunks, const uint32_t *__restrict__ summ,
+                                                    const uint8_t *__restrict__ chg, ExitBits eb,
+                                                    const uint32_t *__restrict__ js, const uint32_t *__restrict__ ce,
+                                                    const uint32_t *__restrict__ Lcur, uint32_t *__restrict__ Lnew,
+                                                    uint32_t *__restrict__ dl, uint8_t *__restrict__ uni, uint32_t klog,
+                                                    uint32_t n)
+{
+    const uint32_t c = blockIdx.x * kT + threadIdx.x;
+    if (c >= nchunks)
+        return;
+    const uint32_t *sm = summ + kSummW * (size_t)c;
+    bool u = !chg[c] && !sm[kSumm];
+    uint32_t d0 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kSumm; k++) {
+        const uint32_t e = sm[k] < n ? sm[k] : n;  // (every walked chunk has an exit)
+        const uint32_t x = bits_index(eb.mask, eb.wpre, sidx(e, klog));
+        const uint32_t v = js[x], d = v - ce[x];
+        d0 = k == 0 ? d : d0;
+        u &= d == d0 && v < (1u << 29);
+    }
+    uni[c] = u ? 1u : 0u;
+    dl[c] = d0;
+    Lnew[c] = u ? Lcur[c] + d0 : 0u;
+}
+
+// The rewritten chunks of a lazy pass (k_cost_rest's shape and formula): C = the new exact cost
+// (offset 0), D = new - old (the shift the next test reads).
+__global__ __launch_bounds__(kT) void k_lazy_rewrite(ExitBits eb, const uint32_t *__restrict__ js,
+                                                     const uint64_t *__restrict__ pst,
+                                                     const uint32_t *__restrict__ ce, uint32_t n,
+                                                     uint32_t klog, size_t S, uint32_t *__restrict__ C,
+                                                     uint32_t *__restrict__ D, const uint32_t *__restrict__ Lcur,
+                                                     const uint8_t *__restrict__ uni,
+                                                     const uint32_t *__restrict__ dsum, uint32_t nchunks)
+{
+    const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
+    const uint32_t lane = (uint32_t)(x & 63u);
+    const size_t rest = x >> 6;
+    const uint32_t groups = (1u << klog) / kRows;
+    const size_t t = rest / groups;
+    const uint32_t g = (uint32_t)(rest % groups);
+    if ((t << (klog + 6)) >= S)
+        return;
+    const uint32_t c = (uint32_t)(t * 64 + lane);  // chunk
+    if (c >= nchunks || uni[c])
+        return;
+    const uint32_t shift = dsum[c], lc = Lcur[c];
+    uint32_t last_se = 0xffffffffu, base_cost = 0;
+    for (uint32_t r = 0; r < kRows; r++) {
+        const size_t s = (t << (klog + 6)) | ((size_t)(g * kRows + r) << 6) | lane;
+        const uint64_t p = spos(s, klog);
+        if (p > n)
+            break;
+        const uint32_t old = C[s] + lc;
+        uint32_t cost;
+        if ((eb.mask[s >> 6] >> lane) & 1u) {
+            cost = js[bits_index(eb.mask, eb.wpre, s)];
+        } else {
+            const uint64_t v = pst[s];
+            const uint32_t se = (uint32_t)sidx((uint32_t)v, klog);
+            if (se != last_se) {
+                const uint32_t xe = bits_index(eb.mask, eb.wpre, se);
+                base_cost = js[xe] - ce[xe];
+                last_se = se;
+            }
+            cost = (uint32_t)(v >> 32) + shift + base_cost;
+        }
+        D[s] = cost - old;
+        C[s] = cost;
+    }
+}
+
+// Lazy breaks for the range test: brk[k] = 1 when the shift may change inside (kK, (k + 1)K]: chunk
+// k or k + 1 rewritten, or their deltas differ (entries past the last chunk are uniform, delta 0).
+__global__ __launch_bounds__(kT) void k_lazy_breaks(const uint8_t *__restrict__ uni, const uint32_t *__restrict__ dl,
+                                                    uint32_t nchunks, uint32_t *__restrict__ brk)
+{
+    const uint32_t k = blockIdx.x * kT + threadIdx.x;
+    if (k >= nchunks)
+        return;
+    brk[k] = !uni[k] || !uni[k + 1] || dl[k] != dl[k + 1] ? 1u : 0u;
+}
+
+// Exact costs of a lazy parse (C + L) into out (the debug dump's cost array).
+__global__ __launch_bounds__(kT) void k_lazy_materialize(const uint32_t *__restrict__ C, const uint32_t *__restrict__ L,
+                                                         uint32_t n, uint32_t klog, size_t S, uint32_t *__restrict__ out)
+{
+    const size_t s = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (s >= S)
+        return;
+    const uint64_t p = spos(s, klog);
+    out[s] = p <= n ? C[s] + L[p >> klog] : 0u;
+}
+
 }  // namespace
+
+int parse_materialize_cost(Workspace &ws)
+{
+    ParseState &ps = ws.parse;
+    if (!ps.lzC)
+        return 0;
+    const size_t tile = (size_t)kTileChunks << ws.klog;
+    const uint32_t n = ps.lzn;
+    const size_t S = ((size_t)n + 1 + tile - 1) / tile * tile;
+    hipLaunchKernelGGL(k_lazy_materialize, dim3(grid_for(S, kT)), dim3(kT), 0, ws.stream, ps.lzC, ps.lzL, n, ws.klog, S,
+                       ps.lzD);
+    SALZ_LAUNCH_CHECK();
+    ps.cost = ps.lzD;
+    ps.lzC = nullptr;
+    return 0;
+}
 
 // Chunk length from the block length N (bytes; n = N - 8 positions): the largest K <= 512
 // that leaves MORE than 2^17 chunks (two waves per SIMD) for blocks up to 32 MiB, and more
@@ -618,6 +923,30 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     // the full ones every pass)
     const bool pack = n < kPackLen && (!getenv("SALZ_PARSE_PACK") || atoi(getenv("SALZ_PARSE_PACK")) != 0);
     uint2 *cand8 = pack ? reinterpret_cast<uint2 *>(ws.g64) : nullptr;
+    // Lazy costs from the first skipping pass on (SALZ_PARSE_LAZY=0: every pass rewrites every
+    // cost): per-chunk offsets (two generations), deltas, uniform / changed flags, exit summaries,
+    // and the pre-pass cost of every exit node.
+    const bool lazy_on = skip_on && (!getenv("SALZ_PARSE_LAZY") || atoi(getenv("SALZ_PARSE_LAZY")) != 0);
+    const size_t nc64 = (size_t)ps.nchunks + 64;
+    uint32_t *Lv[2] = {pbrk + nc64, pbrk + 2 * nc64};
+    uint32_t *dl = pbrk + 3 * nc64;
+    uint8_t *uni = reinterpret_cast<uint8_t *>(pbrk + 4 * nc64), *chg = uni + nc64;
+    uint32_t *summ = pbrk + 5 * nc64;
+    uint32_t *rlo = pbrk + (5 + kSummW) * nc64;  // per chunk: first row reaching past its end
+    // split test (k_mark_rows; SALZ_PARSE_SPLIT=0: the per-candidate test inside k_parse_mark)
+    const bool split_on = range_on && (!getenv("SALZ_PARSE_SPLIT") || atoi(getenv("SALZ_PARSE_SPLIT")) != 0);
+    uint32_t *ms_count = reinterpret_cast<uint32_t *>(ws.dscal) + 51;
+    const MarkSplit ms{split_on ? pbrk + (6 + kSummW) * nc64 : nullptr, ms_count,
+                       reinterpret_cast<uint8_t *>(pbrk + (8 + kSummW) * nc64), pbrk + (7 + kSummW) * nc64};
+    uint32_t *ce = pbrk + (9 + kSummW) * nc64;
+    if ((size_t)(ce - reinterpret_cast<uint32_t *>(ws.lsc)) + ws.cap_n + 2 > 4 * (ws.cap_s > ws.cap_n + 2 ? ws.cap_s : ws.cap_n + 2)) {
+        set_error("parse: lazy-cost scratch does not fit");
+        return -1;
+    }
+    bool lazy = false;
+    int lc = 0;
+    uint32_t *lzC = nullptr, *lzD = nullptr;
+    ps.lzC = nullptr;
 
     hipLaunchKernelGGL(k_cost_seed, dim3(grid_for(S, kT)), dim3(kT), 0, st, cost[0], bl, klog, S);
     SALZ_LAUNCH_CHECK();
@@ -630,7 +959,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     uint32_t prev_changed = 0xffffffffu;
     for (;; it++) {
         const int cur = it & 1;
-        uint32_t *cin = cost[cur], *cout = cost[cur ^ 1];
+        uint32_t *cin = lazy ? lzC : cost[cur], *cout = lazy ? lzD : cost[cur ^ 1];
         uint8_t *chold = choice[cur], *chnew = choice[cur ^ 1];
         // From the third pass on, waves of chunks whose decisions would repeat skip the pass,
         // and a pass with no dirty wave left is not run at all: the previous decisions are the
@@ -642,10 +971,22 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         // save throughput, run it before every pass from the third.
         const bool late = (uint64_t)prev_changed * 64 < n &&
                           (it == 2 || (uint64_t)prev_changed * 4096 < n);
-        const bool skipping = it >= 2 && (n < (1u << 25) || late || early);
+        // (with lazy costs the test is cheap after its first pass: large blocks skip from the third
+        // pass too)
+        const bool skipping = it >= 2 && (n < (1u << 25) || late || early || lazy_on);
+        // the first skipping pass enters the lazy costs (its test still reads the cost arrays)
+        const bool entering = lazy_on && skipping && !lazy;
         if (skipping) {
             SALZ_HIP(hipMemsetAsync(ndirty, 0, 4, st));
-            if (range_on) {
+            LazyTest lt{lazy ? Lv[lc] : nullptr, uni, dl, lzD};
+            if (lazy && range_on) {
+                hipLaunchKernelGGL(k_lazy_breaks, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, uni, dl, ps.nchunks,
+                                   brk);
+                SALZ_LAUNCH_CHECK();
+                SALZ_HIP(hipMemsetAsync(brk + ps.nchunks, 0, sizeof(uint32_t), st));
+                if (scan_sum_u32(brk, pbrk, (size_t)ps.nchunks + 1, false, nullptr, ws, st) != 0)
+                    return -1;
+            } else if (range_on) {
                 SALZ_HIP(hipMemsetAsync(brk, 0, sizeof(uint32_t) * ((size_t)ps.nchunks + 1), st));
                 const size_t bthreads = (size_t)((ps.nchunks + 63) / 64) * 64 * (ps.chunk / kRowsBrk);
                 hipLaunchKernelGGL(k_shift_breaks, dim3(grid_for(bthreads, kT)), dim3(kT), 0, st, cin, cout, n, klog,
@@ -654,15 +995,30 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                 if (scan_sum_u32(brk, pbrk, (size_t)ps.nchunks + 1, false, nullptr, ws, st) != 0)
                     return -1;
             }
+            if (split_on)
+                SALZ_HIP(hipMemsetAsync(ms_count, 0, 4, st));
             if (pack)
                 hipLaunchKernelGGL(k_parse_mark<CandPacked>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st,
                                    cand8, cin, cout, n, bl, klog, wdirty, dsum, ndirty, range_on ? reach : nullptr,
-                                   pbrk);
+                                   pbrk, range_on ? rlo : nullptr, lt, ms);
             else
                 hipLaunchKernelGGL(k_parse_mark<CandFull>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st,
                                    ws.cand, cin, cout, n, bl, klog, wdirty, dsum, ndirty,
-                                   range_on ? reach : nullptr, pbrk);
+                                   range_on ? reach : nullptr, pbrk, range_on ? rlo : nullptr, lt, ms);
             SALZ_LAUNCH_CHECK();
+            if (split_on) {  // listed chunks: a wave each (2048 waves, grid-stride), then the wave flags
+                const uint32_t rgrid = 2048 / (kT / 64);
+                if (pack)
+                    hipLaunchKernelGGL(k_mark_rows<CandPacked>, dim3(rgrid), dim3(kT), 0, st, cand8, cin, cout, n, bl,
+                                       klog, rlo, lt, ms);
+                else
+                    hipLaunchKernelGGL(k_mark_rows<CandFull>, dim3(rgrid), dim3(kT), 0, st, ws.cand, cin, cout, n, bl,
+                                       klog, rlo, lt, ms);
+                SALZ_LAUNCH_CHECK();
+                hipLaunchKernelGGL(k_mark_final, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, n, klog, ms.cbad, ms.d0s,
+                                   wdirty, dsum, ndirty);
+                SALZ_LAUNCH_CHECK();
+            }
             if (read_scalars(ws, 0, 256, "parse.mark") != 0)
                 return -1;
             const uint32_t nd = reinterpret_cast<uint32_t *>(ws.hscal)[50];
@@ -674,6 +1030,10 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                 break;
             }
         }
+        if (entering) {  // offsets 0 (entries past the last chunk: uniform, delta 0)
+            SALZ_HIP(hipMemsetAsync(Lv[0], 0, sizeof(uint32_t) * 4 * nc64, st));  // Lv[0], Lv[1], dl
+            SALZ_HIP(hipMemsetAsync(uni, 1, nc64, st));
+        }
         SALZ_HIP(hipMemsetAsync(changed, 0, 4, st));
         // Exit flags accumulate once waves skip passes: a skipped chunk's exits stay marked
         // from the pass that chose them (stale exits only add nodes to the forest).
@@ -682,13 +1042,15 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
         uint8_t *wd = skipping && skip_on ? wdirty : nullptr;
         uint32_t *rch = it == 0 && range_on ? reach : nullptr;
+        const Lazy lzw{lazy ? Lv[lc] : nullptr, lazy_on ? summ : nullptr, lazy_on ? chg : nullptr};
         if (pack && it > 0)
             hipLaunchKernelGGL(k_parse_chunk<CandPacked>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, cand8,
-                               nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr, eflag, wd, dsum, rch);
+                               nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr, eflag, wd, dsum, rch,
+                               rlo, lzw);
         else
             hipLaunchKernelGGL(k_parse_chunk<CandFull>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
                                it == 0 ? cand8 : nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr,
-                               eflag, wd, dsum, rch);
+                               eflag, wd, dsum, rch, rlo, lzw);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 256, "parse.changed") != 0)
             return -1;
@@ -704,6 +1066,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             ps.cost = cin;
             break;
         }
+        const bool lz_pass = lazy || entering;  // this pass updates the costs lazily
         prev_changed = nchanged;
         // After t passes the last t chunks hold exact decisions (the last one sees only exact
         // costs, then induction), so nchunks + 1 passes always suffice.
@@ -730,7 +1093,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             return -1;
         }
         hipLaunchKernelGGL(k_compact_exits, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st, eb, ws.pst, cin, n, klog,
-                           S / 8, elist, snap, js[0], dsum);
+                           S / 8, elist, snap, js[0], dsum, lz_pass ? Lv[lc] : nullptr, lz_pass ? ce : nullptr);
         SALZ_LAUNCH_CHECK();
         int jc = 0;
         if (snaps) {
@@ -753,14 +1116,52 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                 jc ^= 1;
             }
         }
-        hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(S / kRows, kT)), dim3(kT), 0, st, eb, js[jc], ws.pst, cin,
-                           n, klog, S, cout, dsum);
-        SALZ_LAUNCH_CHECK();
+        if (lz_pass) {
+            if (entering) {  // C = the exact costs this pass read; the other array holds the shifts
+                lazy = true;
+                lzC = cin;
+                lzD = cout;
+            }
+            hipLaunchKernelGGL(k_lazy_chunks, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ps.nchunks, summ, chg,
+                               eb, js[jc], ce, Lv[lc], Lv[lc ^ 1], dl, uni, klog, n);
+            SALZ_LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_lazy_rewrite, dim3(grid_for(S / kRows, kT)), dim3(kT), 0, st, eb, js[jc], ws.pst, ce,
+                               n, klog, S, lzC, lzD, Lv[lc], uni, dsum, ps.nchunks);
+            SALZ_LAUNCH_CHECK();
+            if (verbose) {  // chunks: uniform, changed by the walk, more than two exits
+                std::vector<uint8_t> hu(ps.nchunks), hc(ps.nchunks);
+                std::vector<uint32_t> hs(kSummW * (size_t)ps.nchunks);
+                SALZ_HIP(hipMemcpyAsync(hu.data(), uni, ps.nchunks, hipMemcpyDeviceToHost, st));
+                SALZ_HIP(hipMemcpyAsync(hc.data(), chg, ps.nchunks, hipMemcpyDeviceToHost, st));
+                SALZ_HIP(hipMemcpyAsync(hs.data(), summ, 4 * hs.size(), hipMemcpyDeviceToHost, st));
+                SALZ_HIP(hipStreamSynchronize(st));
+                size_t nu = 0, nc = 0, no = 0;
+                for (uint32_t c = 0; c < ps.nchunks; c++) {
+                    nu += hu[c];
+                    nc += hc[c];
+                    no += hs[kSummW * (size_t)c + kSumm] != 0;
+                }
+                fprintf(stderr, "parse it=%d lazy: %zu uniform, %zu changed, %zu over %u exits of %u chunks, |E| %u\n", it,
+                        nu, nc, no, kSumm, ps.nchunks, ne);
+            }
+            lc ^= 1;
+        } else {
+            hipLaunchKernelGGL(k_cost_rest, dim3(grid_for(S / kRows, kT)), dim3(kT), 0, st, eb, js[jc], ws.pst, cin,
+                               n, klog, S, cout, dsum);
+            SALZ_LAUNCH_CHECK();
+        }
         ps.n_exit = ne;
         ps.levels = K;
         ps.snaps = snaps;
         ps.elist = elist;
         ps.jt0 = snap;
+    }
+    if (lazy) {  // the exact costs are C + L (parse_materialize_cost writes them out on demand)
+        ps.cost = nullptr;
+        ps.lzC = lzC;
+        ps.lzL = Lv[lc];
+        ps.lzD = lzD;
+        ps.lzn = n;
     }
     ws.stats.parse_iters = it + 1;
     ws.stats.exit_nodes = ps.n_exit;

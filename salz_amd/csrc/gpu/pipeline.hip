@@ -416,6 +416,8 @@ static int dump_after_parse(Workspace &ws, uint32_t n, const salz_gpu_dump *d)
     SALZ_HIP(hipMemcpyAsync(cand.data(), ws.cand, sizeof(uint4) * S, hipMemcpyDeviceToHost,
                             ws.stream));
     SALZ_HIP(hipMemcpyAsync(choice.data(), ws.parse.choice, S, hipMemcpyDeviceToHost, ws.stream));
+    if (parse_materialize_cost(ws) != 0)
+        return -1;
     SALZ_HIP(hipMemcpyAsync(cost.data(), ws.parse.cost, sizeof(uint32_t) * S,
                             hipMemcpyDeviceToHost, ws.stream));
     SALZ_HIP(hipStreamSynchronize(ws.stream));

@@ -379,7 +379,7 @@ def test_lcp_paths(ctx, monkeypatch, lcp_sa, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
-@pytest.mark.parametrize("skip", ["1", "1r0", "0", "1p0"])
+@pytest.mark.parametrize("skip", ["1", "1l0", "1s0", "1r0", "0", "1p0"])
 @pytest.mark.parametrize("kind,n,seed,alpha,klog", [("mixed", 3_000_000, 3, 0, "6"),
                                                     ("mixed", 2_000_001, 7, 0, "9"),
                                                     ("text", 1_500_000, 2, 0, "7"),
@@ -390,8 +390,13 @@ def test_parse_wave_skip(ctx, monkeypatch, skip, kind, n, seed, alpha, klog):
     (parse.hip k_parse_mark, SALZ_PARSE_SKIP=1, the default): decisions, the exact suffix
     costs and the stream match the oracle with and without skipping, with the chunk range test
     (SALZ_PARSE_RANGE=1, the default) and the per-candidate test alone ("1r0"), on the packed
-    candidates (SALZ_PARSE_PACK=1, the default) and the full ones ("1p0")."""
+    candidates (SALZ_PARSE_PACK=1, the default) and the full ones ("1p0"), with the lazy
+    per-chunk cost offsets of the skipping passes (SALZ_PARSE_LAZY=1, the default) and without
+    ("1l0"), and with the per-candidate test as a wave per listed chunk (SALZ_PARSE_SPLIT=1, the
+    default) or inside the test kernel ("1s0")."""
     monkeypatch.setenv("SALZ_PARSE_SKIP", skip[0])
+    monkeypatch.setenv("SALZ_PARSE_LAZY", "0" if skip == "1l0" else "1")
+    monkeypatch.setenv("SALZ_PARSE_SPLIT", "0" if skip == "1s0" else "1")
     monkeypatch.setenv("SALZ_PARSE_RANGE", "0" if skip == "1r0" else "1")
     monkeypatch.setenv("SALZ_PARSE_PACK", "0" if skip == "1p0" else "1")
     monkeypatch.setenv("SALZ_PARSE_KLOG", klog)

@@ -10,7 +10,7 @@ import sys
 
 
 def kname(full):
-    m = re.search(r"(k_\w+(<[^>]*>)?)", full)
+    m = re.search(r"(k_\w+)", full)  # (template arguments dropped)
     return m.group(1) if m else full.split("(")[0][:30]
 
 
