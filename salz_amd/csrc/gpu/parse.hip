@@ -785,29 +785,23 @@ __global__ __launch_bounds__(kT) void k_lazy_rewrite(ExitBits eb, const uint32_t
     if ((t << (klog + 6)) >= S)
         return;
     const uint32_t c = (uint32_t)(t * 64 + lane);  // chunk
-    if (c >= nchunks || uni[c])
+    const uint32_t cc = c < nchunks ? c : 0u;  // (the chunk's words loaded together, unconditionally)
+    const uint32_t shift = dsum[cc], lc = Lcur[cc];
+    if (c >= nchunks || uni[cc])
         return;
-    const uint32_t shift = dsum[c], lc = Lcur[c];
-    uint32_t last_se = 0xffffffffu, base_cost = 0;
     for (uint32_t r = 0; r < kRows; r++) {
         const size_t s = (t << (klog + 6)) | ((size_t)(g * kRows + r) << 6) | lane;
-        const uint64_t p = spos(s, klog);
-        if (p > n)
+        if (spos(s, klog) > n)
             break;
+        // Branch-free, every load of the row unconditional (an exit node's own slot stands in for
+        // its exit, and its in-chunk part is masked off arithmetically).
         const uint32_t old = C[s] + lc;
-        uint32_t cost;
-        if ((eb.mask[s >> 6] >> lane) & 1u) {
-            cost = js[bits_index(eb.mask, eb.wpre, s)];
-        } else {
-            const uint64_t v = pst[s];
-            const uint32_t se = (uint32_t)sidx((uint32_t)v, klog);
-            if (se != last_se) {
-                const uint32_t xe = bits_index(eb.mask, eb.wpre, se);
-                base_cost = js[xe] - ce[xe];
-                last_se = se;
-            }
-            cost = (uint32_t)(v >> 32) + shift + base_cost;
-        }
+        const uint64_t v = pst[s];
+        const uint32_t xm = (uint32_t)(eb.mask[s >> 6] >> lane) & 1u;  // an exit node: its path sum
+        const size_t se = xm ? s : sidx((uint32_t)v, klog);
+        const uint32_t xe = bits_index(eb.mask, eb.wpre, se);
+        const uint32_t jv = js[xe], cv = ce[xe];
+        const uint32_t cost = jv + (((uint32_t)(v >> 32) + shift - cv) & (xm - 1u));
         D[s] = cost - old;
         C[s] = cost;
     }
