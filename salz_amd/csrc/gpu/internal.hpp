@@ -121,7 +121,8 @@ constexpr size_t kHostScal = 64 << 10;  // mapped host buffer: scalars below, re
 int workspace_alloc(Workspace &ws, int device, size_t max_block);
 
 // Copy device scalars dscal[off, off + bytes) to hscal (same offset) and wait for them.
-int read_scalars(Workspace &ws, size_t off, size_t bytes, const char *tag);
+// (zlo, nz: device words dscal[zlo, zlo + nz) zeroed after they are read)
+int read_scalars(Workspace &ws, size_t off, size_t bytes, const char *tag, uint32_t zlo = 0, uint32_t nz = 0);
 // Copy `bytes` of device memory to host memory `dst` through the same mapped buffer.
 int read_device(Workspace &ws, const void *src, size_t bytes, void *dst);
 void workspace_free(Workspace &ws);

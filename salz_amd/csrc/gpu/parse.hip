@@ -939,12 +939,16 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     }
     bool lazy = false;
     int lc = 0;
+    uint32_t prev_listed = 2048;  // chunks the last split test listed (sizes k_mark_rows' grid)
     uint32_t *lzC = nullptr, *lzD = nullptr;
     ps.lzC = nullptr;
 
     hipLaunchKernelGGL(k_cost_seed, dim3(grid_for(S, kT)), dim3(kT), 0, st, cost[0], bl, klog, S);
     SALZ_LAUNCH_CHECK();
     SALZ_HIP(hipMemsetAsync(choice[0], 0xff, S, st));
+    // counters changed (48), ndirty (50), listed chunks (51): zeroed here, then by the scalar reads
+    // that consume them
+    SALZ_HIP(hipMemsetAsync(changed, 0, 16, st));
 
     ps.pst = ws.pst;
     ps.n_exit = 0;
@@ -971,7 +975,6 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         // the first skipping pass enters the lazy costs (its test still reads the cost arrays)
         const bool entering = lazy_on && skipping && !lazy;
         if (skipping) {
-            SALZ_HIP(hipMemsetAsync(ndirty, 0, 4, st));
             LazyTest lt{lazy ? Lv[lc] : nullptr, uni, dl, lzD};
             if (lazy && range_on) {
                 hipLaunchKernelGGL(k_lazy_breaks, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, uni, dl, ps.nchunks,
@@ -989,8 +992,6 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                 if (scan_sum_u32(brk, pbrk, (size_t)ps.nchunks + 1, false, nullptr, ws, st) != 0)
                     return -1;
             }
-            if (split_on)
-                SALZ_HIP(hipMemsetAsync(ms_count, 0, 4, st));
             if (pack)
                 hipLaunchKernelGGL(k_parse_mark<CandPacked>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st,
                                    cand8, cin, cout, n, bl, klog, wdirty, dsum, ndirty, range_on ? reach : nullptr,
@@ -1001,7 +1002,10 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                                    range_on ? reach : nullptr, pbrk, range_on ? rlo : nullptr, lt, ms);
             SALZ_LAUNCH_CHECK();
             if (split_on) {  // listed chunks: a wave each (2048 waves, grid-stride), then the wave flags
-                const uint32_t rgrid = 2048 / (kT / 64);
+                // waves: the previous test's list length (lists shrink from pass to pass; any count is
+                // served by the grid-stride loop), 64 to 2048
+                const uint32_t want = prev_listed < 64 ? 64u : prev_listed > 2048 ? 2048u : prev_listed;
+                const uint32_t rgrid = (want + kT / 64 - 1) / (kT / 64);
                 if (pack)
                     hipLaunchKernelGGL(k_mark_rows<CandPacked>, dim3(rgrid), dim3(kT), 0, st, cand8, cin, cout, n, bl,
                                        klog, rlo, lt, ms);
@@ -1013,9 +1017,10 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                                    wdirty, dsum, ndirty);
                 SALZ_LAUNCH_CHECK();
             }
-            if (read_scalars(ws, 0, 256, "parse.mark") != 0)
+            if (read_scalars(ws, 0, 256, "parse.mark", 50, 2) != 0)  // (ndirty, listed chunks reset)
                 return -1;
             const uint32_t nd = reinterpret_cast<uint32_t *>(ws.hscal)[50];
+            prev_listed = reinterpret_cast<uint32_t *>(ws.hscal)[51];
             if (verbose)
                 fprintf(stderr, "parse it=%d dirty waves %u of %u\n", it, nd, (ps.nchunks + 63) / 64);
             if (nd == 0) {
@@ -1028,7 +1033,6 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             SALZ_HIP(hipMemsetAsync(Lv[0], 0, sizeof(uint32_t) * 4 * nc64, st));  // Lv[0], Lv[1], dl
             SALZ_HIP(hipMemsetAsync(uni, 1, nc64, st));
         }
-        SALZ_HIP(hipMemsetAsync(changed, 0, 4, st));
         // Exit flags accumulate once waves skip passes: a skipped chunk's exits stay marked
         // from the pass that chose them (stale exits only add nodes to the forest).
         if (!skipping)
@@ -1046,7 +1050,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                                it == 0 ? cand8 : nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr,
                                eflag, wd, dsum, rch, rlo, lzw);
         SALZ_LAUNCH_CHECK();
-        if (read_scalars(ws, 0, 256, "parse.changed") != 0)
+        if (read_scalars(ws, 0, 256, "parse.changed", 48, 1) != 0)  // (changed reset)
             return -1;
         const uint32_t nchanged = reinterpret_cast<uint32_t *>(ws.hscal)[48];
         if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {

@@ -263,10 +263,18 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
     return 0;  // rx_pool (radix-scatter timing events) is created on the first timed call
 }
 
-__global__ void k_read_scalars(const uint32_t *__restrict__ d, uint32_t *h, uint32_t words)
+// (reset: after the copy, counters [zlo, zlo + nz) of d are zeroed for their next use, which saves
+// a fill launch per counter)
+__global__ void k_read_scalars(const uint32_t *__restrict__ d, uint32_t *h, uint32_t words, uint32_t *z = nullptr,
+                               uint32_t nz = 0)
 {
     for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
         __hip_atomic_store(&h[i], d[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (nz) {
+        __syncthreads();
+        if (threadIdx.x < nz)
+            z[threadIdx.x] = 0u;
+    }
 }
 
 // Arbitrary device memory through the upper half of the mapped buffer, in pieces.
@@ -286,13 +294,13 @@ int read_device(Workspace &ws, const void *src, size_t bytes, void *dst)
     return 0;
 }
 
-int read_scalars(Workspace &ws, size_t off, size_t bytes, const char *tag)
+int read_scalars(Workspace &ws, size_t off, size_t bytes, const char *tag, uint32_t zlo, uint32_t nz)
 {
     (void)tag;
     const uint32_t *d = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(ws.dscal) + off);
     uint32_t *h = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(ws.hscal_dev) + off);
     hipLaunchKernelGGL(k_read_scalars, dim3(1), dim3(64), 0, ws.stream, d, h,
-                       (uint32_t)((bytes + 3) / 4));
+                       (uint32_t)((bytes + 3) / 4), reinterpret_cast<uint32_t *>(ws.dscal) + zlo, nz);
     SALZ_LAUNCH_CHECK();
     SALZ_HIP(hipStreamSynchronize(ws.stream));
     return 0;
