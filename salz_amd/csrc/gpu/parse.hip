@@ -86,8 +86,6 @@ __global__ __launch_bounds__(kT) void k_cost_seed(uint32_t *cost, Blocks bl, uin
 // previous form (conditional loads, selects on just-loaded values, rings shifted with moves
 // of in-flight registers) drained every outstanding load each step: one HBM latency per step.
 constexpr uint32_t kWin = 8;
-constexpr uint32_t kDepth = 4;
-constexpr uint32_t kCDepth = 7;
 
 // Raw target state of a long factor: one 8-byte load. Inside the chunk it is the target's
 // state in pst; past it, the aligned pair of cin words holding cin[sidx(q)] (far_decode picks
@@ -136,15 +134,19 @@ constexpr uint32_t kSummW = kSumm + 1;  // words per chunk
 // wdirty (from the third pass on): one flag per wave of 64 chunks; a clean wave's chunks
 // would repeat their decisions (k_parse_mark), so they only carry their choices over, and
 // their states stay valid through dsum (the uniform cost shift added since their last pass).
-template <class C>
+// DEP / CDEP: far-target and candidate prefetch distances (8, 15 measured no faster in the late
+// passes either).
+template <class C, uint32_t DEP = 4, uint32_t CDEP = 7>
 __global__ __launch_bounds__(kT) void k_parse_chunk(
     const typename C::T *__restrict__ cand, uint2 *__restrict__ pack_out, const uint32_t *__restrict__ cin,
     uint64_t *__restrict__ pst,
-    const uint8_t *__restrict__ chold, uint8_t *__restrict__ chnew, uint32_t n, Blocks bl, uint32_t klog,
+    const uint8_t *chold, uint8_t *chnew, uint32_t n, Blocks bl, uint32_t klog,
     uint32_t *__restrict__ changed, uint32_t *err, uint8_t *__restrict__ eflag,
     const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum, uint32_t *__restrict__ reach,
     uint32_t *__restrict__ rlo, Lazy lz)
 {
+    constexpr uint32_t kDepth = DEP, kCDepth = CDEP;
+    static_assert(kDepth <= kWin && kCDepth >= kDepth && ((kCDepth + 1) % kDepth) == 0, "ring depths");
     const uint32_t c = blockIdx.x * kT + threadIdx.x;  // chunk
     const uint64_t a64 = (uint64_t)c << klog;
     uint32_t diff = 0, errw = 0;
@@ -162,9 +164,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
         const uint32_t b = (e - a) < K ? e : a + K;
         const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
         auto slot = [&](uint32_t j) { return base + ((size_t)j << 6); };
-        if (wdirty && !wdirty[c >> 6]) {  // wave-uniform: a clean wave
-            for (uint32_t j = 0; j < b - a; j++)
-                chnew[slot(j)] = chold[slot(j)];
+        if (wdirty && !wdirty[c >> 6]) {  // wave-uniform: a clean wave keeps its choices (in place)
             if (lz.chg)
                 lz.chg[c] = 0;
             return;
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             exs[k] = 0xffffffffu;
         far_end = b;
         reach_lo = b;
-#pragma unroll 8
+#pragma unroll CDEP + 1
         for (uint32_t j = K; j-- > 0;) {
             const uint32_t p = a + j;
             const bool live = p < b;
@@ -958,7 +958,11 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     for (;; it++) {
         const int cur = it & 1;
         uint32_t *cin = lazy ? lzC : cost[cur], *cout = lazy ? lzD : cost[cur ^ 1];
-        uint8_t *chold = choice[cur], *chnew = choice[cur ^ 1];
+        // Choices are updated in place (chold == chnew, not restrict): a lane reads a position's
+        // old choice kDepth steps before it writes the new one, and a clean wave keeps its choices
+        // without a copy.
+        (void)cur;
+        uint8_t *chold = choice[0], *chnew = choice[0];
         // From the third pass on, waves of chunks whose decisions would repeat skip the pass,
         // and a pass with no dirty wave left is not run at all: the previous decisions are the
         // fixed point and cin their exact costs (k_parse_mark, DESIGN.md "Parse"). The test
