@@ -65,6 +65,7 @@ struct Workspace {
     size_t np2 = 0;    // power of two >= cap_n (ANSV tree leaves)
     size_t cap_s = 0;  // storage slots of the interleaved per-position arrays (>= cap_n + 1)
     uint32_t klog = 9; // parse chunk = 1 << klog positions for the current block
+    uint32_t sigma = 0; // distinct bytes of the current block, when the suffix sorter counted them
 
     uint8_t *text = nullptr;  // padded copy of the block
     uint32_t *rank = nullptr, *sa = nullptr;

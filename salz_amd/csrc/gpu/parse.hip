@@ -976,7 +976,9 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         // (with lazy costs the test is cheap after its first pass: large blocks skip from the third
         // pass too)
         const bool skipping = it >= 2 && (n < (1u << 25) || late || early || lazy_on);
-        // the first skipping pass enters the lazy costs (its test still reads the cost arrays)
+        // The first skipping pass enters the lazy costs (its test still reads the cost arrays).
+        // (Entering at the second pass, so that the first test reads the shifts per chunk, was
+        // slower on text: C2 parse 4.09 -> 4.23 ms, its second pass changes too many chunks.)
         const bool entering = lazy_on && skipping && !lazy;
         if (skipping) {
             LazyTest lt{lazy ? Lv[lc] : nullptr, uni, dl, lzD};

@@ -1080,6 +1080,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         for (int c = 0; c < 256; c++)
             if (pw[c >> 5] & (1u << (c & 31)))
                 alpha.code[c] = (uint8_t)++sigma;
+        ws.sigma = sigma;  // (the parse's chunk length on large blocks follows it, pipeline.hip)
         const uint32_t bits = (uint32_t)bit_width(sigma);  // codes 1..sigma, 0 = past the end
         if (sigma <= 255) {
             codes = alpha;
