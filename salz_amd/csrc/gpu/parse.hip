@@ -939,7 +939,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     }
     bool lazy = false;
     int lc = 0;
-    uint32_t prev_listed = 2048;  // chunks the last split test listed (sizes k_mark_rows' grid)
+    uint32_t prev_listed = ps.nchunks;  // chunks the last split test listed (sizes k_mark_rows' grid)
     uint32_t *lzC = nullptr, *lzD = nullptr;
     ps.lzC = nullptr;
 
@@ -1009,8 +1009,8 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             SALZ_LAUNCH_CHECK();
             if (split_on) {  // listed chunks: a wave each (2048 waves, grid-stride), then the wave flags
                 // waves: the previous test's list length (lists shrink from pass to pass; any count is
-                // served by the grid-stride loop), 64 to 2048
-                const uint32_t want = prev_listed < 64 ? 64u : prev_listed > 2048 ? 2048u : prev_listed;
+                // served by the grid-stride loop), 64 to 16384; the first test lists up to every chunk
+                const uint32_t want = prev_listed < 64 ? 64u : prev_listed > 16384 ? 16384u : prev_listed;
                 const uint32_t rgrid = (want + kT / 64 - 1) / (kT / 64);
                 if (pack)
                     hipLaunchKernelGGL(k_mark_rows<CandPacked>, dim3(rgrid), dim3(kT), 0, st, cand8, cin, cout, n, bl,
