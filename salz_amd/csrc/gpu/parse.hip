@@ -714,25 +714,40 @@ __global__ __launch_bounds__(kT) void k_cost_rest(ExitBits eb, const uint32_t *_
     if ((t << (klog + 6)) >= S)
         return;
     const uint32_t c = (uint32_t)(t * 64 + lane);  // chunk
+    const size_t s0 = (t << (klog + 6)) | ((size_t)(g * kRows) << 6) | lane;
+    if (spos(s0, klog) > n)
+        return;  // (rows ascend: none of this thread's is a position)
     const uint32_t shift = (uint64_t)c << klog < n ? dsum[c] : 0u;
-    uint32_t last_se = 0xffffffffu, base_cost = 0;
+    // All rows at once, every load unconditional (rows past n repeat row 0, whose store then
+    // repeats too): the state and mask word per row, then each row's exit index and costs. One
+    // chain of three dependent latencies per thread instead of one per row.
+    size_t sr[kRows];
+    uint64_t v[kRows], mw[kRows];
+#pragma unroll
     for (uint32_t r = 0; r < kRows; r++) {
-        const size_t s = (t << (klog + 6)) | ((size_t)(g * kRows + r) << 6) | lane;
-        const uint64_t p = spos(s, klog);
-        if (p > n)
-            break;
-        if ((eb.mask[s >> 6] >> lane) & 1u) {  // (the wave's 64 slots: one word)
-            cost[s] = js[bits_index(eb.mask, eb.wpre, s)];
-            continue;
-        }
-        const uint64_t v = pst[s];
-        const uint32_t se = (uint32_t)sidx((uint32_t)v, klog);
-        if (se != last_se) {
-            base_cost = js[bits_index(eb.mask, eb.wpre, se)] - cin[se];
-            last_se = se;
-        }
-        cost[s] = (uint32_t)(v >> 32) + shift + base_cost;
+        const size_t s = s0 | ((size_t)r << 6);
+        sr[r] = spos(s, klog) <= n ? s : s0;
+        v[r] = pst[sr[r]];
+        mw[r] = eb.mask[sr[r] >> 6];
     }
+    uint32_t xe[kRows], se[kRows];
+    bool isx[kRows];
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; r++) {
+        isx[r] = (mw[r] >> lane) & 1u;  // an exit node: its own path sum
+        se[r] = isx[r] ? (uint32_t)sr[r] : (uint32_t)sidx((uint32_t)v[r], klog);
+        const uint64_t m2 = eb.mask[se[r] >> 6];
+        xe[r] = eb.wpre[se[r] >> 6] + (uint32_t)__popcll(m2 & ((1ull << (se[r] & 63u)) - 1ull));
+    }
+    uint32_t out[kRows];
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; r++) {
+        const uint32_t jv = js[xe[r]], cv = cin[se[r]];
+        out[r] = jv + (((uint32_t)(v[r] >> 32) + shift - cv) & (isx[r] ? 0u : 0xffffffffu));
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; r++)
+        cost[sr[r]] = sr[r] == s0 ? out[0] : out[r];
 }
 
 // Lazy passes, after the exact costs of the exit set: per chunk, whether its costs all moved by
