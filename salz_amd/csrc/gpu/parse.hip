@@ -667,6 +667,52 @@ __global__ __launch_bounds__(kT) void k_compact_exits(ExitBits eb, const uint64_
     }
 }
 
+// The same, one thread per node of E (its word by a binary search over the word prefixes, its slot
+// by selecting the set bit): |E| threads instead of one per 8 slots, where E is sparse.
+__global__ __launch_bounds__(kT) void k_compact_nodes(ExitBits eb, size_t nw, uint32_t steps, uint32_t ne,
+                                                      const uint64_t *__restrict__ pst,
+                                                      const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog,
+                                                      uint32_t *__restrict__ elist, uint32_t *__restrict__ jt0,
+                                                      uint32_t *__restrict__ js, const uint32_t *__restrict__ dsum,
+                                                      const uint32_t *__restrict__ Lz, uint32_t *__restrict__ ce)
+{
+    const uint32_t xi = blockIdx.x * kT + threadIdx.x;
+    if (xi >= ne)
+        return;
+    // the last word whose prefix is <= xi (a fixed number of steps, every load unconditional)
+    size_t lo = 0, hi = nw;
+    for (uint32_t i = 0; i < steps; i++) {
+        const size_t mid = (lo + hi) >> 1;
+        const bool le = eb.wpre[mid] <= xi;
+        lo = le ? mid : lo;
+        hi = le ? hi : mid;
+    }
+    uint64_t m = eb.mask[lo];
+    uint32_t k = xi - eb.wpre[lo], p = 0;
+#pragma unroll
+    for (uint32_t w = 32; w >= 1; w >>= 1) {  // the k-th set bit of m
+        const uint32_t c = (uint32_t)__popcll(m & ((1ull << w) - 1ull));
+        const bool up = k >= c;
+        k = up ? k - c : k;
+        m = up ? m >> w : m;
+        p += up ? w : 0u;
+    }
+    const size_t s = lo * 64 + p;
+    const uint32_t q = (uint32_t)spos(s, klog);
+    const uint64_t v = pst[s];
+    const uint32_t ev = q >= n ? n : (uint32_t)v;
+    const size_t se = sidx(ev, klog);
+    const uint32_t parent = bits_index(eb.mask, eb.wpre, se);
+    const uint32_t qc = q < n ? q : 0u;
+    const uint32_t lq = Lz ? Lz[qc >> klog] : 0u, le = Lz ? Lz[ev >> klog] : 0u;
+    const uint32_t w = (uint32_t)(v >> 32) + dsum[qc >> klog] - (cin[se] + le);
+    if (ce)
+        ce[xi] = q == n ? 0u : cin[s] + lq;
+    elist[xi] = q;
+    jt0[xi] = q == n ? xi : parent;
+    js[xi] = q == n ? 0u : w;
+}
+
 // Pointer jumping over E, two levels per launch (the snapshot of every level is kept for
 // emission's path marking): from level k (jt, js) to k + 1 (jt1, written) and k + 2 (jt2, js2).
 // A thread derives its node's level-(k + 1) successor itself, so no other thread's result of
@@ -954,6 +1000,9 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     }
     bool lazy = false;
     int lc = 0;
+    // exit compaction per node where E is sparse (SALZ_PARSE_NODES=0: per 8 slots always, 2: per
+    // node always)
+    const int node_compact = getenv("SALZ_PARSE_NODES") ? atoi(getenv("SALZ_PARSE_NODES")) : 1;
     uint32_t prev_listed = ps.nchunks;  // chunks the last split test listed (sizes k_mark_rows' grid)
     uint32_t *lzC = nullptr, *lzD = nullptr;
     ps.lzC = nullptr;
@@ -1111,8 +1160,15 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             set_error("parse: exit set larger than the text (|E|=%u)", ne);
             return -1;
         }
-        hipLaunchKernelGGL(k_compact_exits, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st, eb, ws.pst, cin, n, klog,
-                           S / 8, elist, snap, js[0], dsum, lz_pass ? Lv[lc] : nullptr, lz_pass ? ce : nullptr);
+        if (node_compact == 2 || (node_compact == 1 && (uint64_t)ne * 64 < S)) {  // sparse E: a thread per node
+            const size_t nw = S / 64;
+            hipLaunchKernelGGL(k_compact_nodes, dim3(grid_for(ne, kT)), dim3(kT), 0, st, eb, nw,
+                               (uint32_t)bit_width(nw) + 1u, ne, ws.pst, cin, n, klog, elist, snap, js[0], dsum,
+                               lz_pass ? Lv[lc] : nullptr, lz_pass ? ce : nullptr);
+        } else {
+            hipLaunchKernelGGL(k_compact_exits, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st, eb, ws.pst, cin, n, klog,
+                               S / 8, elist, snap, js[0], dsum, lz_pass ? Lv[lc] : nullptr, lz_pass ? ce : nullptr);
+        }
         SALZ_LAUNCH_CHECK();
         int jc = 0;
         if (snaps) {

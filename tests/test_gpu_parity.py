@@ -380,7 +380,7 @@ def test_lcp_paths(ctx, monkeypatch, lcp_sa, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
-@pytest.mark.parametrize("skip", ["1", "1l0", "1s0", "1r0", "0", "1p0"])
+@pytest.mark.parametrize("skip", ["1", "1l0", "1s0", "1n2", "1r0", "0", "1p0"])
 @pytest.mark.parametrize("kind,n,seed,alpha,klog", [("mixed", 3_000_000, 3, 0, "6"),
                                                     ("mixed", 2_000_001, 7, 0, "9"),
                                                     ("text", 1_500_000, 2, 0, "7"),
@@ -394,10 +394,12 @@ def test_parse_wave_skip(ctx, monkeypatch, skip, kind, n, seed, alpha, klog):
     candidates (SALZ_PARSE_PACK=1, the default) and the full ones ("1p0"), with the lazy
     per-chunk cost offsets of the skipping passes (SALZ_PARSE_LAZY=1, the default) and without
     ("1l0"), and with the per-candidate test as a wave per listed chunk (SALZ_PARSE_SPLIT=1, the
-    default) or inside the test kernel ("1s0")."""
+    default) or inside the test kernel ("1s0"), and with the exit set compacted a thread per node
+    ("1n2"; by default only where it is sparse)."""
     monkeypatch.setenv("SALZ_PARSE_SKIP", skip[0])
     monkeypatch.setenv("SALZ_PARSE_LAZY", "0" if skip == "1l0" else "1")
     monkeypatch.setenv("SALZ_PARSE_SPLIT", "0" if skip == "1s0" else "1")
+    monkeypatch.setenv("SALZ_PARSE_NODES", "2" if skip == "1n2" else "1")
     monkeypatch.setenv("SALZ_PARSE_RANGE", "0" if skip == "1r0" else "1")
     monkeypatch.setenv("SALZ_PARSE_PACK", "0" if skip == "1p0" else "1")
     monkeypatch.setenv("SALZ_PARSE_KLOG", klog)
