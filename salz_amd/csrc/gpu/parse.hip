@@ -539,8 +539,9 @@ __global__ __launch_bounds__(kT) void k_parse_mark(const typename C::T *__restri
         dsum[c] += d0;
 }
 
-// A listed chunk's per-candidate test, one wave per chunk (grid-stride over the list): lane l takes
-// rows rlo + l, rlo + l + 64, ... of the chunk, all loads issued before any is used.
+// Listed chunks' per-candidate tests (grid-stride over the list): a wave takes G = 512 / K chunks
+// (one at K = 512, eight at K = 64), LP = 64 / G lanes each; lane l of a chunk takes rows
+// rlo + l, rlo + l + LP, ... (at most 8), all loads issued before any is used.
 template <class C>
 __global__ __launch_bounds__(kT) void k_mark_rows(const typename C::T *__restrict__ cand,
                                                   const uint32_t *__restrict__ cnew,
@@ -549,39 +550,42 @@ __global__ __launch_bounds__(kT) void k_mark_rows(const typename C::T *__restric
                                                   MarkSplit ms)
 {
     const uint32_t lane = lane_id(), nwaves = gridDim.x * (kT / 64);
+    const uint32_t K = 1u << klog, G = K >= 512u ? 1u : 512u / K, LP = 64u / G;
+    const uint32_t sub = lane / LP, lic = lane % LP;
+    const uint64_t gmask = (LP == 64u ? ~0ull : ((1ull << LP) - 1ull)) << (sub * LP);
     const uint32_t cnt = *ms.count;
-    for (uint32_t w = (blockIdx.x * kT + threadIdx.x) >> 6; w < cnt; w += nwaves) {
-        const uint32_t c = ms.list[w];
-        const uint32_t a = c << klog, K = 1u << klog;
+    for (uint32_t w0 = ((blockIdx.x * kT + threadIdx.x) >> 6) * G; w0 < cnt; w0 += nwaves * G) {
+        const uint32_t li = w0 + sub;
+        const bool have = li < cnt;
+        const uint32_t c = ms.list[have ? li : w0];
+        const uint32_t a = c << klog;
         const uint32_t e = bl.end(a), b0 = bl.start(a);
         const uint32_t b = (e - a) < K ? e : a + K;
         const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
         const uint32_t d0 = ms.d0s[c];
         const uint32_t jl = rlo ? rlo[c] - a : 0u, jn = b - a;
-        const uint32_t steps = (jn - jl + 63u) / 64u;  // (wave-uniform)
-        bool bad = false;
-        for (uint32_t i0 = 0; i0 < steps; i0 += 8) {
-            typename C::T cd[8];
+        typename C::T cd[8];
 #pragma unroll
-            for (uint32_t u = 0; u < 8; u++) {
-                const uint32_t j = jl + (i0 + u) * 64u + lane;
-                cd[u] = cand[base + ((size_t)(j < jn ? j : jl) << 6)];
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < 8; u++) {
-                const uint32_t j = jl + (i0 + u) * 64u + lane, p = a + j;
-                const bool on = j < jn && p != b0;
-                const uint32_t lp = C::lp(cd[u]), ln = C::ln(cd[u]);
-                const uint32_t qp = p + lp, qn = p + ln;
-                const bool xp = on && lp >= 3u && qp >= b, xn = on && ln >= 3u && qn >= b;
-                uint32_t vp, vn;
-                const uint32_t dp = shift_of(lt, cnew, cold, klog, xp ? qp : b, vp);
-                const uint32_t dn = shift_of(lt, cnew, cold, klog, xn ? qn : b, vn);
-                bad |= dp != d0 || vp >= (1u << 30);
-                bad |= dn != d0 || vn >= (1u << 30);
-            }
+        for (uint32_t u = 0; u < 8; u++) {
+            const uint32_t j = jl + lic + u * LP;
+            cd[u] = cand[base + ((size_t)(j < jn ? j : jl) << 6)];
         }
-        if (wave_ballot(bad) && lane == 0)
+        bool bad = false;
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) {
+            const uint32_t j = jl + lic + u * LP, p = a + j;
+            const bool on = have && j < jn && p != b0;
+            const uint32_t lp = C::lp(cd[u]), ln = C::ln(cd[u]);
+            const uint32_t qp = p + lp, qn = p + ln;
+            const bool xp = on && lp >= 3u && qp >= b, xn = on && ln >= 3u && qn >= b;
+            uint32_t vp, vn;
+            const uint32_t dp = shift_of(lt, cnew, cold, klog, xp ? qp : b, vp);
+            const uint32_t dn = shift_of(lt, cnew, cold, klog, xn ? qn : b, vn);
+            bad |= dp != d0 || vp >= (1u << 30);
+            bad |= dn != d0 || vn >= (1u << 30);
+        }
+        const uint64_t bm = wave_ballot(bad);
+        if (lic == 0 && have && (bm & gmask))
             ms.cbad[c] = 1u;
     }
 }
@@ -1074,7 +1078,9 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             if (split_on) {  // listed chunks: a wave each (2048 waves, grid-stride), then the wave flags
                 // waves: the previous test's list length (lists shrink from pass to pass; any count is
                 // served by the grid-stride loop), 64 to 16384; the first test lists up to every chunk
-                const uint32_t want = prev_listed < 64 ? 64u : prev_listed > 16384 ? 16384u : prev_listed;
+                const uint32_t per = klog >= 9 ? 1u : 512u >> klog;  // chunks per wave
+                const uint32_t wv = (prev_listed + per - 1) / per;
+                const uint32_t want = wv < 64 ? 64u : wv > 16384 ? 16384u : wv;
                 const uint32_t rgrid = (want + kT / 64 - 1) / (kT / 64);
                 if (pack)
                     hipLaunchKernelGGL(k_mark_rows<CandPacked>, dim3(rgrid), dim3(kT), 0, st, cand8, cin, cout, n, bl,
