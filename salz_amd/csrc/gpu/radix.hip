@@ -83,6 +83,29 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
         // past the suffix's end masked to 0 like the key's bytes.
         const uint32_t b = txt.a.bits, kl = txt.a.bits ? txt.a.k - 1u : 7u;
         uint32_t d[kItems];
+        if (txt.g.nb == 1 && base >= 7 && left >= (size_t)kTile) {  // (tile-uniform)
+            // One block, a whole tile past the short suffixes: entry c is suffix c - 7, so a
+            // thread's 16 consecutive entries need the 17 consecutive bytes from their first
+            // suffix + kl - 1 on: three loads instead of 32 byte loads.
+            const size_t c0 = base + (size_t)tid * kItems;
+            const uint32_t i0 = (uint32_t)(c0 - 7), e = txt.g.npos;
+            const size_t p0 = (size_t)i0 + kl - 1u;
+            const uint64_t w0 = load_u64_any(txt.T, p0), w1 = load_u64_any(txt.T, p0 + 8);
+            const uint32_t w2 = txt.T[p0 + 16];
+            auto byte_at = [&](uint32_t k) -> uint32_t {  // T[p0 + k], k <= 16
+                return k < 8 ? (uint32_t)(w0 >> (8 * k)) & 255u : k < 16 ? (uint32_t)(w1 >> (8 * (k - 8))) & 255u : w2;
+            };
+#pragma unroll
+            for (int j = 0; j < kItems; j++) {
+                const uint32_t i = i0 + (uint32_t)j;
+                const uint32_t s7 = i + kl < e ? byte_at((uint32_t)j + 1u) : 0u;
+                const uint32_t s6 = b && i + kl - 1u < e ? byte_at((uint32_t)j) : 0u;
+                d[j] = (s7 | (s6 << b)) & 255u;
+            }
+#pragma unroll
+            for (int j = 0; j < kItems; j++)
+                atomicAdd(&mine[d[j]], 1u);
+        } else {
 #pragma unroll
         for (int j = 0; j < kItems; j++) {
             const size_t idx = (size_t)j * kThreads + tid;
@@ -95,6 +118,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
         for (int j = 0; j < kItems; j++)
             if ((size_t)j * kThreads + tid < left)
                 atomicAdd(&mine[d[j]], 1u);
+        }
     } else if (kMode == 1) {
         // text loads unconditional (clamped entry), so none is issued under a narrower mask
         uint64_t kk[kItems];
