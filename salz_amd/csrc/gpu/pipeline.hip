@@ -565,11 +565,14 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P
     } else if (stage_suffix_array(ws, bl)) {
         return -1;
     }
-    // A large single block of more than 127 distinct bytes (binary or mixed data, no text alphabet)
-    // parses with 128-position chunks: its pass count barely depends on the chunk length, and the
-    // late passes walk a quarter as far (mixed 100 MB: 43.2 -> 42.0 ms); text keeps K = 512, whose
-    // passes are fewer (3 instead of 6 at K = 128 on 100 MB).
-    if (nbz == 1 && ws.sigma > 127 && ws.klog > 7 && !getenv("SALZ_PARSE_KLOG"))
+    // A large single block (> 32 MiB) of more than 127 distinct bytes (binary or mixed data, no
+    // text alphabet) parses with 128-position chunks: its pass count barely depends on the chunk
+    // length, and the late passes walk a quarter as far (mixed 100 MB: 43.2 -> 42.0 ms); text
+    // keeps K = 512, whose passes are fewer (3 instead of 6 at K = 128 on 100 MB).
+    // Blocks of 8–32 MiB of such data take K = 128 too (16 MiB mixed blocks, 4 slots: C3
+    // 2650 -> 2725 MB/s, though one block alone parses 0.4 ms slower than at K = 64: fewer chunks
+    // and exits cost less GPU time in total while other slots keep the GPU busy).
+    if (nbz == 1 && ws.sigma > 127 && !getenv("SALZ_PARSE_KLOG") && (ws.klog > 7 || (ws.klog < 7 && n > (8u << 20))))
         ws.klog = 7;
     if (guard_check(ws, "sa") || (nbz == 1 && check_stage(ws, n, 2))) return -1;
     if (mark(ws, EV_SA)) return -1;
@@ -646,9 +649,15 @@ __global__ __launch_bounds__(256) void k_pack_frames(const uint8_t *__restrict__
 static int ensure_batch_room(Workspace &ws, size_t P, size_t bs)
 {
     const size_t nb = bs >= P ? 1 : (P + bs - 1) / bs;
-    if (P > ws.cap_N || nb * batch_stride(bs < P ? bs : P) > ws.out_cap)
-        return workspace_alloc(ws, ws.device, P > ws.cap_N ? P : ws.cap_N);
-    return 0;
+    const size_t need = nb * batch_stride(bs < P ? bs : P);  // every block's stream slot
+    if (P <= ws.cap_N && need <= ws.out_cap)
+        return 0;
+    // The output buffer follows the block capacity (out_bound): a batch whose last block is short
+    // needs more stream slots than out_bound(P) covers, so grow until it does.
+    size_t N = P > ws.cap_N ? P : ws.cap_N;
+    while (out_bound(N) < need)
+        N += bs < P ? bs : P;
+    return workspace_alloc(ws, ws.device, N);
 }
 
 static int encode_batch_packed(Workspace &ws, const uint8_t *src, bool src_dev, size_t P, size_t bs,
