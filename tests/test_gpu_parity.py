@@ -234,6 +234,22 @@ def test_encode_blocks_container(salz, block, size):
     assert salz.decode_blocks(got, size) == src.tobytes()
 
 
+@pytest.mark.parametrize("cap,block,size", [(1 << 20, 1 << 20, 5 * (1 << 20) + 12345),
+                                            (1 << 16, 1 << 20, 3 * (1 << 20) + 4097)])
+def test_encode_batch_grows_workspace(salz, cap, block, size):
+    """A fresh context smaller than the batch grows its workspace so every block, a short last
+    one included, gets its own output slot (ensure_batch_room in pipeline.hip); the streams
+    equal the per-block oracle's."""
+    src = gen("mixed", size, 11)
+    c = salz.Context(0, cap)
+    got = c.encode_batch(src, block)
+    c.close()
+    assert len(got) == -(-size // block)
+    for k, off in enumerate(range(0, size, block)):
+        rc, s = oracle_encode(src[off:off + block])
+        assert rc == 0 and got[k] == s, k
+
+
 @pytest.mark.parametrize("keys", ["1", "0", "1d0", "1t0", "1s0", "1s2048", "1p1", "0p1", "1p8"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
