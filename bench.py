@@ -245,6 +245,41 @@ def measure_traffic(args):
     return out, None
 
 
+def link_rates(torch, dev, host_block, d_stream, stream_len) -> dict:
+    """Host link rates of one block and one stream, so the e2e figure can be read against them:
+    H2D of the block and D2H of its stream from pinned host memory (the DMA engines alone) and
+    from pageable memory (what a salz_encode_safe caller hands over), best of 3, CUDA events."""
+    n = len(host_block)
+    pin_in = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    pin_in.numpy()[:] = host_block
+    pin_out = torch.empty(stream_len, dtype=torch.uint8, pin_memory=True)
+    page_in = torch.from_numpy(host_block.copy())
+    page_out = torch.empty(stream_len, dtype=torch.uint8)
+    d_in = torch.empty(n, dtype=torch.uint8, device=dev)
+
+    def best(fn, nbytes):
+        ms = []
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            a.record()
+            fn()
+            b.record()
+            b.synchronize()
+            ms.append(a.elapsed_time(b))
+        return round(nbytes / (min(ms) * 1e-3) / 1e9, 2)
+
+    src_stream = d_stream[:stream_len]
+    return {
+        "h2d_gbs": best(lambda: d_in.copy_(pin_in, non_blocking=True), n),
+        "d2h_gbs": best(lambda: pin_out.copy_(src_stream, non_blocking=True), stream_len),
+        "h2d_pageable_gbs": best(lambda: d_in.copy_(page_in), n),
+        "d2h_pageable_gbs": best(lambda: page_out.copy_(src_stream), stream_len),
+        "link_what": f"one {n:,}-byte block H2D and its {stream_len:,}-byte stream D2H, pinned "
+                     "(h2d_gbs, d2h_gbs) and pageable host memory, best of 3",
+    }
+
+
 def git_head() -> str:
     try:
         import subprocess
@@ -561,7 +596,8 @@ def main():
         e2e = {"value": round(in_bytes * args.steps / dth / 1e6, 3), "unit": "MB/s",
                "ms_per_step": round(dth / args.steps * 1e3, 3),
                "what": "host buffers in and out (pageable numpy memory): H2D of each block, "
-                       "encode, D2H of each stream; same blocks and slots as value, no exchange"}
+                       "encode, D2H of each stream; same blocks and slots as value, no exchange",
+               **link_rates(torch, dev, src[units[0][0]:units[0][1]], d_dst[0], lens[0])}
 
     cpu = None
     parity_full = None

@@ -135,6 +135,19 @@ typedef struct {
                                      + 1 where the next pass's digit byte is written) */
 } salz_gpu_stats;
 
+/*
+ * The context pool behind salz_encode_safe (the reference keeps no state between calls,
+ * lib/salz.c:175-256; here workspaces are cached for the next call). slots_per_device: contexts
+ * per device (1..8; default SALZ_SAFE_SLOTS or 4); cache_bytes: device memory idle cached
+ * workspaces may hold per device before the largest are released after a call (default
+ * SALZ_SAFE_CACHE_BYTES or 32 GiB); any_device: 1 lets a caller borrow contexts of other
+ * devices when its own are busy, 0 keeps every call on the caller's current device (default).
+ * A value <= 0 (< 0 for any_device) leaves that setting unchanged.
+ */
+void salz_gpu_pool_config(int slots_per_device, size_t cache_bytes, int any_device);
+/* Device memory held by the pool's workspaces on `device`. */
+size_t salz_gpu_pool_bytes(int device);
+
 /* Per-stage HIP-event timing of subsequent calls (small overhead when on). */
 void salz_gpu_set_timing(salz_gpu_ctx *ctx, int on);
 int salz_gpu_get_stats(const salz_gpu_ctx *ctx, salz_gpu_stats *out);

@@ -428,12 +428,14 @@ int stage_suffix_array_dc3(Workspace &ws, const Blocks &bl, const Alpha &codes, 
     if (ws.dc3_bytes < need) {
         if (ws.dc3)
             SALZ_HIP(hipFree(ws.dc3));
+        ws.bytes -= ws.dc3_bytes;
         ws.dc3 = nullptr;
         ws.dc3_bytes = 0;
         void *p = nullptr;
         SALZ_HIP(hipMalloc(&p, need));
         ws.dc3 = static_cast<uint8_t *>(p);
         ws.dc3_bytes = need;
+        ws.bytes += need;
     }
     uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
     Dc3 d{ws, st, ws.dc3, ws.dc3 + ws.dc3_bytes, derr};

@@ -84,6 +84,7 @@ struct Workspace {
     uint8_t *dc3 = nullptr;    // DC3 suffix sorter's level arena (dc3.hip), allocated on first use
     uint8_t *dist_owner = nullptr;  // split suffix sort: owning rank per two-byte class (dsa.hip)
     size_t dc3_bytes = 0;
+    size_t bytes = 0;  // device memory held by this workspace (the salz_encode_safe pool's cap)
     uint8_t *out = nullptr;                                              // encoded_len_max
     size_t out_cap = 0;
     uint32_t *radix_counts = nullptr;
@@ -120,6 +121,7 @@ int copy_d2h(Workspace &ws, uint8_t *dst, const uint8_t *src, size_t bytes);
 constexpr size_t kHostScal = 64 << 10;  // mapped host buffer: scalars below, read_device above
 
 int workspace_alloc(Workspace &ws, int device, size_t max_block);
+void workspace_release(Workspace &ws);  // free the buffers, keep the device
 
 // Copy device scalars dscal[off, off + bytes) to hscal (same offset) and wait for them.
 // (zlo, nz: device words dscal[zlo, zlo + nz) zeroed after they are read)

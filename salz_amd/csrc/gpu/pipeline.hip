@@ -47,10 +47,11 @@ struct Guard {
 static thread_local std::vector<Guard> *g_guards = nullptr;
 static bool guard_on() { static const bool on = getenv("SALZ_GUARD") != nullptr; return on; }
 
-template <typename T> static int dalloc_named(T **p, size_t count, const char *name)
+template <typename T> static int dalloc_named(T **p, size_t count, const char *name, size_t *held)
 {
     void *q = nullptr;
     const size_t bytes = count * sizeof(T) + 256;
+    *held += bytes;
     hipError_t e = hipMalloc(&q, bytes + (guard_on() ? kGuardBytes : 0));
     if (e != hipSuccess) {
         set_error("hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
@@ -66,7 +67,7 @@ template <typename T> static int dalloc_named(T **p, size_t count, const char *n
     *p = static_cast<T *>(q);
     return 0;
 }
-#define dalloc(p, count) dalloc_named(p, count, #p)
+#define dalloc(p, count) dalloc_named(p, count, #p, &held)
 
 int guard_check(Workspace &ws, const char *stage)
 {
@@ -112,6 +113,15 @@ void workspace_free(Workspace &ws)
             (void)hipEventDestroy(ws.hstage_ev[b]);
     }
     ws = Workspace{};
+}
+
+// Free every buffer but keep the device: the next encode reallocates (every path that takes a
+// cached context grows its workspace on demand).
+void workspace_release(Workspace &ws)
+{
+    const int dev = ws.device;
+    workspace_free(ws);
+    ws.device = dev;
 }
 
 // Whether a host buffer is pinned (registered or hipHostMalloc'ed) or device memory, so a
@@ -219,6 +229,7 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
     ws.out_cap = out_bound(N);
     size_t scan_elems = scan_temp_elems(ws.radix_counts_elems > n1 ? ws.radix_counts_elems : n1);
     ws.scan_tmp_bytes = scan_elems * sizeof(uint64_t);
+    size_t held = 0;
     if (dalloc(&ws.text, N + 256) || dalloc(&ws.rank, n1) || dalloc(&ws.sa, n1) ||
         dalloc(&ws.keyA, n1) || dalloc(&ws.keyB, n1) || dalloc(&ws.valA, n1) ||
         dalloc(&ws.valB, n1) || dalloc(&ws.u0, n1) || dalloc(&ws.u1, n1) || dalloc(&ws.u2, n1) ||
@@ -233,6 +244,7 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
         set_error("%s", keep.c_str());
         return -1;
     }
+    ws.bytes = held;
     if (const char *pz = getenv("SALZ_POISON")) {
         // tests/diagnostics: fill the workspace with a pattern so reads of never-written
         // memory misbehave deterministically instead of depending on what VRAM held before
@@ -569,10 +581,12 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P
     // text alphabet) parses with 128-position chunks: its pass count barely depends on the chunk
     // length, and the late passes walk a quarter as far (mixed 100 MB: 43.2 -> 42.0 ms); text
     // keeps K = 512, whose passes are fewer (3 instead of 6 at K = 128 on 100 MB).
-    // Blocks of 8–32 MiB of such data take K = 128 too (16 MiB mixed blocks, 4 slots: C3
-    // 2650 -> 2725 MB/s, though one block alone parses 0.4 ms slower than at K = 64: fewer chunks
-    // and exits cost less GPU time in total while other slots keep the GPU busy).
-    if (nbz == 1 && ws.sigma > 127 && !getenv("SALZ_PARSE_KLOG") && (ws.klog > 7 || (ws.klog < 7 && n > (8u << 20))))
+    // Single blocks of 8–16 MiB take K = 128 instead of the size rule's 64 whatever the data:
+    // mixed 16 MiB blocks, 4 slots: C3 2650 -> 2725 MB/s; text 16 MiB blocks in the same layout
+    // 3224 / 3191 -> 3570 / 3567 MB/s (profiles/r03zzz_c3text_klog_ab.txt), though one block alone
+    // parses 0.4 ms slower than at K = 64: fewer chunks and exits cost less GPU time in total
+    // while other slots keep the GPU busy.
+    if (nbz == 1 && !getenv("SALZ_PARSE_KLOG") && ((ws.sigma > 127 && ws.klog > 7) || (ws.klog < 7 && n > (8u << 20))))
         ws.klog = 7;
     if (guard_check(ws, "sa") || (nbz == 1 && check_stage(ws, n, 2))) return -1;
     if (mark(ws, EV_SA)) return -1;
@@ -741,6 +755,7 @@ using namespace salz;
 struct salz_gpu_ctx {
     Workspace ws;
     std::mutex mu;
+    std::atomic<size_t> held{0};  // ws.bytes as of its last pooled call (read without mu)
 };
 
 extern "C" {
@@ -818,6 +833,7 @@ salz_gpu_ctx *salz_gpu_ctx_create(int device, size_t max_block)
         delete c;
         return nullptr;
     }
+    c->held.store(c->ws.bytes);
     return c;
 }
 
@@ -1052,43 +1068,91 @@ int salz_debug_encode_batch_dump(salz_gpu_ctx *ctx, const uint8_t *src, size_t s
 
 // Cached contexts: slot 0 of each device serves salz_encode_safe; salz_encode_blocks uses
 // slots 0..k-1 so that k blocks are in flight per device (their own streams and workspaces).
+// A slot being filled holds kCreating while its context is created outside g_default_mu (a
+// workspace is several hipMallocs of up to tens of GB: no other caller waits behind them).
 constexpr int kMaxSlots = 8;
 static std::mutex g_default_mu;
+static std::condition_variable g_pool_cv;
 static std::vector<salz_gpu_ctx *> g_default;  // [device * kMaxSlots + slot]
+static salz_gpu_ctx g_creating_tag;
+static salz_gpu_ctx *const kCreating = &g_creating_tag;
+
+static bool pool_init_locked()
+{
+    if (g_default.empty()) {
+        const int n = salz_gpu_device_count();
+        g_default.assign(n > 0 ? (size_t)n * kMaxSlots : 0, nullptr);
+    }
+    return !g_default.empty();
+}
+
+// Create the context of a slot that holds kCreating (the caller reserved it), outside the pool
+// lock, and publish it (locked by the caller when `lock`) or clear the reservation on failure.
+static salz_gpu_ctx *pool_fill_slot(size_t idx, int device, size_t need, bool lock)
+{
+    salz_gpu_ctx *c = salz_gpu_ctx_create(device, need);
+    if (c && lock)
+        c->mu.lock();  // not yet visible to anyone else
+    {
+        std::lock_guard<std::mutex> lk(g_default_mu);
+        g_default[idx] = c;
+    }
+    g_pool_cv.notify_all();
+    return c;
+}
 
 static salz_gpu_ctx *default_ctx(int device, size_t need, int slot = 0)
 {
-    std::lock_guard<std::mutex> lk(g_default_mu);
-    if (g_default.empty()) {
-        int n = salz_gpu_device_count();
-        g_default.assign(n > 0 ? (size_t)n * kMaxSlots : 0, nullptr);
-    }
-    if (device < 0 || (size_t)device * kMaxSlots >= g_default.size() || slot < 0 ||
+    std::unique_lock<std::mutex> lk(g_default_mu);
+    if (!pool_init_locked() || device < 0 || (size_t)device * kMaxSlots >= g_default.size() || slot < 0 ||
         slot >= kMaxSlots) {
         set_error("no usable HIP device (gfx950) for salz_encode_safe");
         return nullptr;
     }
-    salz_gpu_ctx *&c = g_default[(size_t)device * kMaxSlots + slot];
-    if (!c)
-        c = salz_gpu_ctx_create(device, need);
-    return c;
+    const size_t idx = (size_t)device * kMaxSlots + slot;
+    g_pool_cv.wait(lk, [&] { return g_default[idx] != kCreating; });
+    if (salz_gpu_ctx *c = g_default[idx])
+        return c;
+    g_default[idx] = kCreating;
+    lk.unlock();
+    return pool_fill_slot(idx, device, need, false);
 }
 
 // salz_encode_safe's context pool. The reference encoder keeps no state between calls
 // (lib/salz.c:175-256, :777-823), so T threads calling it encode T blocks at once. Here a call
-// takes any idle cached context: first an idle one on the caller's current device, then one on
-// another device, then a new context on the device with the fewest (the caller's own on a tie),
-// up to SALZ_SAFE_SLOTS (default 4) per device; when every context is busy it waits for one.
-// Contexts are shared with salz_encode_blocks / salz_encode_stream (same slots, same mutexes).
-static std::condition_variable g_pool_cv;
+// takes an idle cached context on the caller's current device, or creates one there, up to
+// SALZ_SAFE_SLOTS (default 4) per device; when every one is busy it waits for one. Contexts on
+// other devices are borrowed only after salz_gpu_pool_config(any_device = 1). Contexts are
+// shared with salz_encode_blocks / salz_encode_stream (same slots, same mutexes).
+// The reference frees its scratch after every call (lib/salz.c:175-256); the pool keeps
+// workspaces for the next call but caps what idle contexts hold per device (SALZ_SAFE_CACHE_BYTES
+// or salz_gpu_pool_config, default 32 GiB): after a call, idle workspaces are released, the
+// largest first, until the device's pool is under the cap (a released context reallocates
+// on its next call).
+static std::atomic<int> g_pool_slots{0};
+static std::atomic<size_t> g_pool_cap{0};
+static std::atomic<int> g_pool_any_dev{0};
 
 static int safe_slots_per_device()
 {
-    static const int v = [] {
+    int v = g_pool_slots.load();
+    if (v == 0) {
         const char *e = getenv("SALZ_SAFE_SLOTS");
         const int k = e ? atoi(e) : 4;
-        return k < 1 ? 1 : k > kMaxSlots ? kMaxSlots : k;
-    }();
+        v = k < 1 ? 1 : k > kMaxSlots ? kMaxSlots : k;
+        g_pool_slots.store(v);
+    }
+    return v;
+}
+
+static size_t pool_cap_bytes()
+{
+    size_t v = g_pool_cap.load();
+    if (v == 0) {
+        const char *e = getenv("SALZ_SAFE_CACHE_BYTES");
+        v = e ? (size_t)strtoull(e, nullptr, 0) : (size_t)32 << 30;
+        g_pool_cap.store(v ? v : 1);
+    }
     return v;
 }
 
@@ -1103,59 +1167,110 @@ static salz_gpu_ctx *pool_try_acquire(int cur, size_t need, bool *create_failed,
     if (ndev <= 0)
         return nullptr;
     const int per = safe_slots_per_device();
+    const int ndev_use = g_pool_any_dev.load() ? ndev : 1;
     std::vector<salz_gpu_ctx *> snap;
     {
         std::lock_guard<std::mutex> lk(g_default_mu);
-        if (g_default.empty())
-            g_default.assign((size_t)ndev * kMaxSlots, nullptr);
+        if (!pool_init_locked())
+            return nullptr;
         snap = g_default;
     }
-    for (int k = 0; k < ndev; k++) {  // existing idle contexts, current device first
+    for (int k = 0; k < ndev_use; k++) {  // existing idle contexts, current device first
         const int d = (cur + k) % ndev;
         for (int s = 0; s < kMaxSlots; s++) {
             salz_gpu_ctx *c = snap[(size_t)d * kMaxSlots + s];
             *have_any = *have_any || c != nullptr;
-            if (c && c->mu.try_lock())
+            if (c && c != kCreating && c->mu.try_lock())
                 return c;
         }
     }
     // all busy: a new context on the device with the fewest (the caller's own on a tie)
-    int best = -1, best_n = per;
-    for (int k = 0; k < ndev; k++) {
-        const int d = (cur + k) % ndev;
-        int cnt = 0;
-        for (int s = 0; s < per; s++)
-            cnt += snap[(size_t)d * kMaxSlots + s] != nullptr;
-        if (cnt < best_n) {
-            best = d;
-            best_n = cnt;
-        }
-    }
-    if (best < 0)
-        return nullptr;
-    for (int s = 0; s < per; s++) {
+    size_t idx = 0;
+    int best = -1;
+    {
         std::lock_guard<std::mutex> lk(g_default_mu);
-        salz_gpu_ctx *&c = g_default[(size_t)best * kMaxSlots + s];
-        if (c)
-            continue;
-        c = salz_gpu_ctx_create(best, need);
-        if (!c) {
-            *create_failed = true;
-            return nullptr;
+        int best_n = per;
+        for (int k = 0; k < ndev_use; k++) {
+            const int d = (cur + k) % ndev;
+            int cnt = 0;
+            for (int s = 0; s < per; s++)
+                cnt += g_default[(size_t)d * kMaxSlots + s] != nullptr;
+            if (cnt < best_n) {
+                best = d;
+                best_n = cnt;
+            }
         }
-        c->mu.lock();  // new and not yet visible to anyone but the pool lock holder
-        return c;
+        if (best < 0)
+            return nullptr;
+        for (int s = 0; s < per; s++)
+            if (!g_default[(size_t)best * kMaxSlots + s]) {
+                idx = (size_t)best * kMaxSlots + s;
+                g_default[idx] = kCreating;
+                break;
+            }
     }
-    return nullptr;
+    salz_gpu_ctx *c = pool_fill_slot(idx, best, need, true);
+    *create_failed = c == nullptr;
+    return c;
 }
+
+// After a call on `dev`: release idle workspaces (the largest first, `mine` included: its
+// caller still holds it) until the device's cached bytes are under the cap.
+static void pool_trim(int dev, salz_gpu_ctx *mine)
+{
+    const size_t cap = pool_cap_bytes();
+    std::vector<salz_gpu_ctx *> snap;
+    {
+        std::lock_guard<std::mutex> lk(g_default_mu);
+        snap.assign(g_default.begin() + (size_t)dev * kMaxSlots, g_default.begin() + (size_t)(dev + 1) * kMaxSlots);
+    }
+    for (;;) {
+        size_t total = 0, big = 0;
+        salz_gpu_ctx *victim = nullptr;
+        for (salz_gpu_ctx *c : snap) {
+            if (!c || c == kCreating)
+                continue;
+            const size_t b = c->held.load();
+            total += b;
+            if (b > big) {
+                big = b;
+                victim = c;
+            }
+        }
+        if (total <= cap || !victim)
+            return;
+        if (victim != mine && !victim->mu.try_lock()) {
+            // busy: its own caller trims after its call; drop it from this pass
+            for (salz_gpu_ctx *&c : snap)
+                if (c == victim)
+                    c = nullptr;
+            continue;
+        }
+        workspace_release(victim->ws);
+        victim->held.store(0);
+        if (victim != mine)
+            victim->mu.unlock();
+    }
+}
+
+// Restores the calling thread's current HIP device (the pool may create or run a context on
+// another device, and every encode sets the device of its workspace).
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() { (void)hipGetDevice(&dev); }
+    ~DeviceGuard()
+    {
+        if (dev >= 0)
+            (void)hipSetDevice(dev);
+    }
+};
 
 // Called by salz_encode_safe (salz.c) after argument checks.
 int salz_gpu_encode_default(const uint8_t *src, size_t src_len, uint8_t *dst, size_t *dst_len)
 {
-    int cur = 0;
-    if (hipGetDevice(&cur) != hipSuccess)
-        cur = 0;
-    if (salz_gpu_device_count() <= 0 || cur < 0 || cur >= salz_gpu_device_count()) {
+    DeviceGuard guard;
+    const int cur = guard.dev < 0 ? 0 : guard.dev;
+    if (salz_gpu_device_count() <= 0 || cur >= salz_gpu_device_count()) {
         set_error("no usable HIP device (gfx950) for salz_encode_safe");
         return -1;
     }
@@ -1171,9 +1286,35 @@ int salz_gpu_encode_default(const uint8_t *src, size_t src_len, uint8_t *dst, si
         g_pool_cv.wait_for(lk, std::chrono::milliseconds(2));
     }
     int rc = encode_host_locked(c, src, src_len, dst, dst_len, nullptr);
+    c->held.store(c->ws.bytes);
+    pool_trim(c->ws.device >= 0 ? c->ws.device : cur, c);
     c->mu.unlock();
     g_pool_cv.notify_one();
     return rc;
+}
+
+void salz_gpu_pool_config(int slots_per_device, size_t cache_bytes, int any_device)
+{
+    if (slots_per_device > 0)
+        g_pool_slots.store(slots_per_device > kMaxSlots ? kMaxSlots : slots_per_device);
+    if (cache_bytes > 0)
+        g_pool_cap.store(cache_bytes);
+    if (any_device >= 0)
+        g_pool_any_dev.store(any_device ? 1 : 0);
+}
+
+size_t salz_gpu_pool_bytes(int device)
+{
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    size_t total = 0;
+    if (device < 0 || (size_t)(device + 1) * kMaxSlots > g_default.size())
+        return 0;
+    for (int s = 0; s < kMaxSlots; s++) {
+        salz_gpu_ctx *c = g_default[(size_t)device * kMaxSlots + s];
+        if (c && c != kCreating)
+            total += c->held.load();
+    }
+    return total;
 }
 
 // ---- multi-block / multi-GPU container encode ---------------------------------------------
@@ -1278,6 +1419,7 @@ int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, ui
             {
                 std::lock_guard<std::mutex> lk(c->mu);
                 rcs[t] = encode_batch_locked(c->ws, src + off, len, block_size, frames[t].data(), &out);
+                c->held.store(c->ws.bytes);
             }
             if (rcs[t] != 0) {
                 err = g_err;
@@ -1461,6 +1603,7 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
             } else {
                 std::lock_guard<std::mutex> lk(c->mu);
                 rc = encode_batch_locked(c->ws, r.in, r.in_len, block_size, r.out, &out);
+                c->held.store(c->ws.bytes);
             }
             std::lock_guard<std::mutex> lk(mu);
             if (rc != 0) {

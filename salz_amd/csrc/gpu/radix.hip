@@ -39,7 +39,26 @@ __device__ __forceinline__ uint64_t init_key(const TextSrc &t, uint32_t i, const
     return t.a.bits ? round0_key_mapped(t.T, i, t.g.end(i), t.a) : round0_key(t.T, i, t.g.end(i), t.a);
 }
 
-// digit source of a pass: 0 = key bits, 1 = key bits of text-built pairs, 2 = block of value
+// Round-0 key of suffix i from 16 window bytes (w: the 8 at i, w9: the one at i + 8) for the
+// key shapes of round0_key / round0_key_mapped that the single-block text pass serves (raw
+// bytes, or 8 / 9 symbols of a mapped text).
+__device__ __forceinline__ uint64_t window_key(uint64_t w, uint32_t w9, uint32_t left, const Alpha &a)
+{
+    if (left < 8)
+        w &= (1ull << (8u * left)) - 1ull;
+    uint64_t x = __builtin_bswap64(w);
+    if (a.bits == 0)
+        return x;
+    const uint32_t b = a.bits;  // (round0_key_mapped's packing)
+    x = (x & 0x00FF00FF00FF00FFull) | (((x >> 8) & 0x00FF00FF00FF00FFull) << b);
+    x = (x & 0x0000FFFF0000FFFFull) | (((x >> 16) & 0x0000FFFF0000FFFFull) << (2 * b));
+    x = (x & 0xFFFFFFFFull) | ((x >> 32) << (4 * b));
+    if (a.k == 9)
+        x = (x << b) | (left > 8 ? w9 : 0u);
+    return x;
+}
+
+// digit source of a pass: 0 = key bits, 1 / 3 = key bits of text-built pairs, 2 = block of value
 __device__ __forceinline__ unsigned digit_of(int mode, uint64_t k, uint32_t v, int shift, const Blocks &g)
 {
     return mode == 2 ? (g.blk(v) >> shift) & 255u : (unsigned)(k >> shift) & 255u;
@@ -173,6 +192,38 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
     counts[(size_t)tid * ntiles + blockIdx.x] = sum;
 }
 
+// Per-tile digit counts from the digit bytes the previous scatter wrote (16 per thread, one
+// 16-byte load). The load is issued before the counters are cleared, and 16 sub-histograms
+// (4 per wave, by lane & 3; 257 words apart so one digit's copies sit in different banks) keep
+// the LDS at 16 KB: 8 workgroups per CU instead of 4 with 32 copies, and half the clearing and
+// summing per tile (k_radix_hist with 32 copies: 98 us per 100 M digits, latency-bound).
+constexpr int kDigCopies = 16, kDigStride = 257;
+__global__ __launch_bounds__(kThreads) void k_radix_hist_dig(const uint8_t *__restrict__ dig, uint32_t m,
+                                                             uint32_t *__restrict__ counts, uint32_t ntiles)
+{
+    __shared__ uint32_t h[kDigCopies * kDigStride];
+    const unsigned tid = threadIdx.x, wave = tid >> 6;
+    const size_t base = (size_t)blockIdx.x * kTile;
+    const size_t left = m - base;
+    // (the digit buffer has room past m: the load is unconditional)
+    const uint4 x = *reinterpret_cast<const uint4 *>(dig + base + (size_t)tid * kItems);
+    for (int i = tid; i < kDigCopies * kDigStride; i += kThreads)
+        h[i] = 0;
+    __syncthreads();
+    uint32_t *mine = h + (wave * 4 + (tid & 3u)) * kDigStride;
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int j = 0; j < kItems; j++)
+        if ((size_t)tid * kItems + j < left)
+            atomicAdd(&mine[(w[j >> 2] >> (8 * (j & 3))) & 255u], 1u);
+    __syncthreads();
+    uint32_t sum = 0;
+#pragma unroll
+    for (int c = 0; c < kDigCopies; c++)
+        sum += h[c * kDigStride + tid];
+    counts[(size_t)tid * ntiles + blockIdx.x] = sum;
+}
+
 // Digit-major tile counts -> per-digit exclusive prefixes over the tiles (in place), one
 // workgroup per digit, plus the digit totals; k_radix_scatter adds the digit bases (an
 // exclusive scan of the 256 totals) itself. One launch instead of a three-kernel device scan.
@@ -254,8 +305,47 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     uint64_t k[IT];
     uint32_t v[IT];
     uint32_t lrank[IT];
+    // kMode 3: one block. Entry c is suffix c - 7 (c >= 7; the first seven are the short
+    // suffixes n - 1 - c), so a tile's keys come from one text window of kTile + 16 bytes,
+    // staged in LDS (the key stage is free until the ranking is done) with coalesced 8-byte
+    // loads, instead of three unaligned global loads per entry.
+    if (kMode == 3) {
+        uint64_t *W = skey;
+        constexpr uint32_t kWords = kTile / 8 + 3;
+        const size_t tb = (size_t)blockIdx.x * kTile;
+        const size_t w0 = tb ? (tb - 7) >> 3 : 0;
+        const size_t wmax = ((size_t)txt.g.npos + 64) >> 3;  // zero padding past the text
+        for (uint32_t q = tid; q < kWords; q += TH) {
+            const size_t wq = w0 + q;
+            const uint64_t x = reinterpret_cast<const uint64_t *>(txt.T)[wq < wmax ? wq : wmax];
+            W[q] = wq < wmax ? x : 0ull;
+        }
+        __syncthreads();
+        const uint32_t npos = txt.g.npos;
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            const size_t c = base + (size_t)j * 64 + lane;
+            const bool shortsfx = c < 7;
+            const uint32_t sfx = shortsfx ? npos - 1u - (uint32_t)c : (uint32_t)c - 7u;
+            const uint32_t off = shortsfx ? 0u : (uint32_t)((size_t)sfx - (w0 << 3));
+            const uint32_t q = off >> 3, sh = (off & 7u) * 8u;
+            const uint64_t a0 = W[q], a1 = W[q + 1];
+            uint64_t w = (a0 >> sh) | ((a1 << 1) << (63u - sh));
+            uint32_t w9 = (uint32_t)(a1 >> sh) & 255u;
+            if (base + (size_t)j * 64 < 7) {  // (wave-uniform: the short suffixes, tile 0 only)
+                const uint64_t g = load_u64_any(txt.T, shortsfx ? sfx : 0u);
+                w = shortsfx ? g : w;
+                w9 = shortsfx ? 0u : w9;
+            }
+            k[j] = c < m ? window_key(w, w9, npos - sfx, txt.a) : 0ull;
+            v[j] = sfx;
+        }
+        __syncthreads();  // (the window's LDS is the key stage below)
+    }
 #pragma unroll
     for (int j = 0; j < IT; j++) {
+        if (kMode == 3)
+            break;
         size_t i = base + (size_t)j * 64 + lane;
         bool ok = i < m;
         if (kMode == 1) {  // unconditional text loads (clamped entry)
@@ -421,8 +511,10 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     // key passes with 512-thread workgroups (8 items per thread; SALZ_RADIX_WG512=0: 256 threads,
     // 16 items, ~0.5% slower on C2, profiles/r03h_tm_radix_ab.txt)
     static const bool wg512 = !getenv("SALZ_RADIX_WG512") || atoi(getenv("SALZ_RADIX_WG512")) != 0;
+    // one block with raw-byte or 8/9-symbol keys: the text pass builds keys from an LDS window
+    const bool text_win = g.nb == 1 && g.npos >= 7 && (!alpha || alpha->bits == 0 || alpha->k == 8 || alpha->k == 9);
     for (int pass = 0; pass < passes; pass++) {
-        const int mode = pass >= passes_key ? 2 : (text && pass == 0) ? 1 : 0;
+        const int mode = pass >= passes_key ? 2 : (text && pass == 0) ? (text_win ? 3 : 1) : 0;
         const int shift = mode == 2 ? 8 * (pass - passes_key) : bit_lo + 8 * pass;
         TextSrc txt{text, g, Alpha{}};
         // digit bytes: written by a key pass for the next key pass, read by that pass's histogram
@@ -431,12 +523,15 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
         const int nshift = bit_lo + 8 * (pass + 1);
         if (alpha)
             txt.a = *alpha;
-        if (mode == 1)
+        if (mode == 1 || mode == 3)
             hipLaunchKernelGGL(k_radix_hist<1>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
                                shift, ws.radix_counts, ntiles, txt, dig_in);
         else if (mode == 2)
             hipLaunchKernelGGL(k_radix_hist<2>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
                                shift, ws.radix_counts, ntiles, txt, dig_in);
+        else if (dig_in)
+            hipLaunchKernelGGL(k_radix_hist_dig, dim3(ntiles), dim3(kThreads), 0, st, dig_in, m, ws.radix_counts,
+                               ntiles);
         else
             hipLaunchKernelGGL(k_radix_hist<0>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
                                shift, ws.radix_counts, ntiles, txt, dig_in);
@@ -450,7 +545,10 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
         bool timed = ws.timing && mode == 0 && ws.rx_used + 2 <= ws.rx_pool.size();
         if (timed)
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used], st));
-        if (mode == 1)
+        if (mode == 3)
+            hipLaunchKernelGGL((k_radix_scatter<3, 512>), dim3(ntiles), dim3(512), 0, st, kin,
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
+        else if (mode == 1)
             hipLaunchKernelGGL((k_radix_scatter<1, kThreads>), dim3(ntiles), dim3(kThreads), 0, st, kin,
                                vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
         else if (mode == 2)

@@ -183,10 +183,12 @@ def test_stages_every_chunk_length(ctx, klog, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
-@pytest.mark.parametrize("kind,n", [("text", 20_000_000), ("mixed", 24_000_000), ("mixed", 40_000_017)])
+@pytest.mark.parametrize("kind,n", [("text", 12_000_000), ("text", 20_000_000), ("mixed", 24_000_000),
+                                    ("mixed", 40_000_017)])
 def test_large_blocks_match_oracle(salz, kind, n):
-    """Blocks large enough for the default chunk lengths 2^7 / 2^8 (parse_chunk_log), and a mixed
-    block over 32 MiB: more than 127 distinct bytes, so it parses with K = 2^7 (pipeline.hip)."""
+    """Blocks large enough for the default chunk lengths 2^7 / 2^8 (parse_chunk_log); a 12 MB text
+    block, which the 8-16 MiB rule moves from K = 2^6 to 2^7; and a mixed block over 32 MiB: more
+    than 127 distinct bytes, so it parses with K = 2^7 (pipeline.hip)."""
     src = gen(kind, n, 4)
     rc, ref = oracle_encode(src)
     c = salz.Context(0, n)

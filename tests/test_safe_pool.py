@@ -15,7 +15,7 @@ import time
 import numpy as np
 import pytest
 
-from tests.helpers import enc_max, gen, oracle_encode
+from tests.helpers import enc_max, gen, golden, oracle_encode, sha256
 
 pytestmark = pytest.mark.gpu
 
@@ -90,3 +90,54 @@ def test_safe_four_threads_scale(lib, size, count):
     rc, ref = oracle_encode(blocks[0])
     assert outs[0] == ref
     assert mbs4 >= 1.5 * mbs1, f"4 threads {mbs4:.0f} MB/s vs 1 thread {mbs1:.0f} MB/s"
+
+
+def test_safe_pool_cache_cap(lib):
+    """The pool caps what idle workspaces hold per device: after one
+    256 MiB call (about 30 GB of workspace) the device's pool falls back under the cap, and
+    1 MiB calls that follow keep it there; every stream still equals the reference's."""
+    cap = 8 << 30
+    lib.salz_gpu_pool_config(0, cap, -1)
+    try:
+        vec = next(v for v in golden("appendix_c.json")["vectors"] if v["n"] == 1 << 28)
+        out = _encode_safe(lib, gen("fib", vec["n"]))
+        assert sha256(out) == vec["out_sha256"]
+        held = lib.salz_gpu_pool_bytes(0)
+        assert held <= cap, f"{held} bytes held after the 256 MiB call"
+        blocks = _blocks("text", 1 << 20, 8)
+        outs, _ = _run(lib, blocks, 4)
+        assert outs == [oracle_encode(b)[1] for b in blocks]
+        held = lib.salz_gpu_pool_bytes(0)
+        assert 0 < held <= cap, f"{held} bytes held after the 1 MiB calls"
+    finally:
+        lib.salz_gpu_pool_config(0, 32 << 30, -1)
+
+
+def test_safe_keeps_caller_device(lib):
+    """salz_encode_safe leaves the calling thread's current HIP device as it found it (ADVICE r03:
+    the pool may run or create a context elsewhere), also under concurrent calls."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    ndev = ctypes.c_int(0)
+    assert hip.hipGetDeviceCount(ctypes.byref(ndev)) == 0
+    blocks = _blocks("text", 300_000, 8)
+    bad = []
+
+    def work(dev):
+        assert hip.hipSetDevice(dev) == 0
+        for b in blocks:
+            _encode_safe(lib, b)
+            cur = ctypes.c_int(-1)
+            hip.hipGetDevice(ctypes.byref(cur))
+            if cur.value != dev:
+                bad.append((dev, cur.value))
+
+    lib.salz_gpu_pool_config(0, 0, 1)  # borrowing across devices on: the harder case
+    try:
+        ths = [threading.Thread(target=work, args=(k % ndev.value,)) for k in range(4)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+    finally:
+        lib.salz_gpu_pool_config(0, 0, 0)
+    assert bad == []
