@@ -511,19 +511,14 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
         SALZ_HIP(hipMemsetAsync(tlcp + nblocks + used_blocks, 0xff,
                                 sizeof(uint32_t) * (nblocks - used_blocks), st));
     }
-    static const bool prof_on = getenv("SALZ_PROF_ANSV") != nullptr;
+    static const bool prof_on = env_flag("SALZ_DEBUG", "ansv");
     unsigned long long *prof = prof_on ? reinterpret_cast<unsigned long long *>(ws.dscal) + 200 : nullptr;
     if (prof)
         SALZ_HIP(hipMemsetAsync(prof, 0, 32, st));
     // Staging: text ranges of 2^rlog positions (cand windows of 16 << rlog bytes; 16 MB by
     // default: 2^19 and 2^21 measured slower), at most kMaxRanges of them. Slots sp / stage
     // alias scratch that is free here.
-    static const uint32_t rlog_env = [] {
-        const char *e = getenv("SALZ_ANSV_RLOG");
-        const int v = e ? atoi(e) : 20;
-        return (uint32_t)(v < 12 ? 12 : v > 30 ? 30 : v);
-    }();
-    uint32_t rlog = rlog_env;
+    uint32_t rlog = 20;
     while ((((uint64_t)npos - 1) >> rlog) + 1 > kMaxRanges)
         rlog++;
     uint32_t *rfill = ws.radix_counts;

@@ -120,6 +120,11 @@ int copy_d2h(Workspace &ws, uint8_t *dst, const uint8_t *src, size_t bytes);
 
 constexpr size_t kHostScal = 64 << 10;  // mapped host buffer: scalars below, read_device above
 
+// Test and diagnostic switches: SALZ_DEBUG, SALZ_CHECK, SALZ_SA and SALZ_PARSE
+// each hold comma-separated names, bare ("noskip") or with a value ("klog=7").
+bool env_flag(const char *var, const char *name);               // `name` listed in $var
+long env_num(const char *var, const char *name, long dflt);     // its value (bare name: 1)
+
 int workspace_alloc(Workspace &ws, int device, size_t max_block);
 void workspace_release(Workspace &ws);  // free the buffers, keep the device
 
@@ -155,6 +160,13 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
                      const uint8_t *text = nullptr, const Blocks *blocks = nullptr,
                      const Alpha *alpha = nullptr, uint8_t *digits = nullptr, bool digits_ready = false);
+
+// Stable radix sort of (key, value) pairs whose values are indices into the extraction ranges of
+// GL large groups (lrec[g] >> 32 = start of group g's range, ascending; tmap[t] = the group of
+// index 256 t, groups longer than 256): by the group of each value, so a list sorted by key
+// becomes sorted by (group, key) (sa.hip's text round).
+int radix_sort_by_group(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt, uint32_t m,
+                        const uint64_t *lrec, const uint32_t *tmap, uint32_t GL, Workspace &ws, hipStream_t st);
 
 // Blocks per batch (one pipeline pass over several blocks, common.hpp Blocks).
 constexpr uint32_t kMaxBatchBlocks = 4096;

@@ -801,10 +801,10 @@ __global__ __launch_bounds__(kT) void k_cost_rest(ExitBits eb, const uint32_t *_
 }
 
 // Lazy passes, after the exact costs of the exit set: per chunk, whether its costs all moved by
-// one delta (no decision changed in this pass's walk, at most two distinct exits, both moving by
-// the same delta, both costs under 2^29 so that no cost of the chunk reaches 2^30: a path inside
-// one chunk adds far less) -> Lnew = Lcur + delta; otherwise the chunk is rewritten
-// (k_lazy_rewrite) with offset 0.
+// one delta (no decision changed in this pass's walk, at most kSumm (8) distinct exits, all
+// moving by the same delta, every exit cost under 2^29 so that no cost of the chunk reaches
+// 2^30: a path inside one chunk adds far less) -> Lnew = Lcur + delta; otherwise the chunk is
+// rewritten (k_lazy_rewrite) with offset 0.
 __global__ __launch_bounds__(kT) void k_lazy_chunks(uint32_t nchunks, const uint32_t *__restrict__ summ,
                                                     const uint8_t *__restrict__ chg, ExitBits eb,
                                                     const uint32_t *__restrict__ js, const uint32_t *__restrict__ ce,
@@ -920,11 +920,9 @@ int parse_materialize_cost(Workspace &ws)
 // 32 MiB + 8 -> 256, 64 MiB / 100 MB / 256 MiB -> 512 (tests/test_abi.py pins these).
 uint32_t parse_chunk_log(size_t N)
 {
-    if (const char *e = getenv("SALZ_PARSE_KLOG")) {  // tests: force a chunk length
-        int k = atoi(e);
-        if (k >= 6 && k <= (int)kMaxChunkLog)
-            return (uint32_t)k;
-    }
+    const long k = env_num("SALZ_PARSE", "klog", 0);  // tests: force a chunk length
+    if (k >= 6 && k <= (long)kMaxChunkLog)
+        return (uint32_t)k;
     const uint64_t min_chunks = N > (1ull << 25) ? (1ull << 16) : (1ull << 17);
     uint32_t klog = kMaxChunkLog;
     while (klog > 6 && ((uint64_t)N >> klog) <= min_chunks)
@@ -962,38 +960,35 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     uint32_t *changed = reinterpret_cast<uint32_t *>(ws.dscal) + 48;
     uint32_t *etotal = reinterpret_cast<uint32_t *>(ws.dscal) + 49;
     uint32_t *ndirty = reinterpret_cast<uint32_t *>(ws.dscal) + 50;
-    static const bool verbose = getenv("SALZ_DEBUG_PARSE") != nullptr;
-    // Wave skipping from the third pass on (k_parse_mark); SALZ_PARSE_SKIP=0 runs every chunk
+    static const bool verbose = env_flag("SALZ_DEBUG", "parse");
+    // Wave skipping from the third pass on (k_parse_mark); SALZ_PARSE=noskip runs every chunk
     // every pass (tests compare both).
-    const bool skip_on = !getenv("SALZ_PARSE_SKIP") || atoi(getenv("SALZ_PARSE_SKIP")) != 0;
+    const bool skip_on = !env_flag("SALZ_PARSE", "noskip");
     // per chunk: uniform cost shift since its last pass; per wave: dirty flag (lsc is free here)
     uint32_t *dsum = reinterpret_cast<uint32_t *>(ws.lsc);
     uint8_t *wdirty = reinterpret_cast<uint8_t *>(dsum + ps.nchunks);
     SALZ_HIP(hipMemsetAsync(dsum, 0, sizeof(uint32_t) * ps.nchunks, st));
-    // Range test of k_parse_mark (SALZ_PARSE_RANGE=0: per-candidate test only): each chunk's
+    // Range test of k_parse_mark (SALZ_PARSE=norange: per-candidate test only): each chunk's
     // farthest target, and per test the shift breaks per chunk and their prefix counts.
-    const bool range_on = !getenv("SALZ_PARSE_RANGE") || atoi(getenv("SALZ_PARSE_RANGE")) != 0;
+    const bool range_on = !env_flag("SALZ_PARSE", "norange");
     uint32_t *reach = dsum + 2 * ((size_t)ps.nchunks + 64);
     uint32_t *brk = reach + ps.nchunks + 64, *pbrk = brk + ps.nchunks + 64;
-    // Large blocks test for skipping only late in the iteration (SALZ_PARSE_EARLY=1: from the
-    // third pass like smaller blocks; mixed 100 MB: 22.3 -> 23.7 ms, text 4.5 -> 5.0 ms)
-    const bool early = getenv("SALZ_PARSE_EARLY") && atoi(getenv("SALZ_PARSE_EARLY")) != 0;
-    // Packed candidates from the second pass on (g64 is free during the parse; SALZ_PARSE_PACK=0:
+    // Packed candidates from the second pass on (g64 is free during the parse; SALZ_PARSE=nopack:
     // the full ones every pass)
-    const bool pack = n < kPackLen && (!getenv("SALZ_PARSE_PACK") || atoi(getenv("SALZ_PARSE_PACK")) != 0);
+    const bool pack = n < kPackLen && !env_flag("SALZ_PARSE", "nopack");
     uint2 *cand8 = pack ? reinterpret_cast<uint2 *>(ws.g64) : nullptr;
-    // Lazy costs from the first skipping pass on (SALZ_PARSE_LAZY=0: every pass rewrites every
+    // Lazy costs from the first skipping pass on (SALZ_PARSE=nolazy: every pass rewrites every
     // cost): per-chunk offsets (two generations), deltas, uniform / changed flags, exit summaries,
     // and the pre-pass cost of every exit node.
-    const bool lazy_on = skip_on && (!getenv("SALZ_PARSE_LAZY") || atoi(getenv("SALZ_PARSE_LAZY")) != 0);
+    const bool lazy_on = skip_on && !env_flag("SALZ_PARSE", "nolazy");
     const size_t nc64 = (size_t)ps.nchunks + 64;
     uint32_t *Lv[2] = {pbrk + nc64, pbrk + 2 * nc64};
     uint32_t *dl = pbrk + 3 * nc64;
     uint8_t *uni = reinterpret_cast<uint8_t *>(pbrk + 4 * nc64), *chg = uni + nc64;
     uint32_t *summ = pbrk + 5 * nc64;
     uint32_t *rlo = pbrk + (5 + kSummW) * nc64;  // per chunk: first row reaching past its end
-    // split test (k_mark_rows; SALZ_PARSE_SPLIT=0: the per-candidate test inside k_parse_mark)
-    const bool split_on = range_on && (!getenv("SALZ_PARSE_SPLIT") || atoi(getenv("SALZ_PARSE_SPLIT")) != 0);
+    // split test (k_mark_rows; SALZ_PARSE=nosplit: the per-candidate test inside k_parse_mark)
+    const bool split_on = range_on && !env_flag("SALZ_PARSE", "nosplit");
     uint32_t *ms_count = reinterpret_cast<uint32_t *>(ws.dscal) + 51;
     const MarkSplit ms{split_on ? pbrk + (6 + kSummW) * nc64 : nullptr, ms_count,
                        reinterpret_cast<uint8_t *>(pbrk + (8 + kSummW) * nc64), pbrk + (7 + kSummW) * nc64};
@@ -1004,9 +999,9 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     }
     bool lazy = false;
     int lc = 0;
-    // exit compaction per node where E is sparse (SALZ_PARSE_NODES=0: per 8 slots always, 2: per
+    // exit compaction per node where E is sparse (SALZ_PARSE=nodes=0: per 8 slots always, 2: per
     // node always)
-    const int node_compact = getenv("SALZ_PARSE_NODES") ? atoi(getenv("SALZ_PARSE_NODES")) : 1;
+    const int node_compact = (int)env_num("SALZ_PARSE", "nodes", 1);
     uint32_t prev_listed = ps.nchunks;  // chunks the last split test listed (sizes k_mark_rows' grid)
     uint32_t *lzC = nullptr, *lzD = nullptr;
     ps.lzC = nullptr;
@@ -1043,7 +1038,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                           (it == 2 || (uint64_t)prev_changed * 4096 < n);
         // (with lazy costs the test is cheap after its first pass: large blocks skip from the third
         // pass too)
-        const bool skipping = it >= 2 && (n < (1u << 25) || late || early || lazy_on);
+        const bool skipping = it >= 2 && (n < (1u << 25) || late || lazy_on);
         // The first skipping pass enters the lazy costs (its test still reads the cost arrays).
         // (Entering at the second pass, so that the first test reads the shifts per chunk, was
         // slower on text: C2 parse 4.09 -> 4.23 ms, its second pass changes too many chunks.)

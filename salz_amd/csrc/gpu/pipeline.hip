@@ -37,7 +37,30 @@ void set_error(const char *fmt, ...)
     va_end(ap);
 }
 
-// SALZ_GUARD=1 (diagnostics): every workspace buffer gets a guard zone filled with a
+// value of `name` in the comma-separated list $var: "" for a bare name, nullptr if absent
+static const char *env_find(const char *var, const char *name)
+{
+    const char *v = getenv(var);
+    const size_t nl = strlen(name);
+    for (const char *p = v; p && *p;) {
+        const char *end = strchr(p, ',');
+        const size_t len = end ? (size_t)(end - p) : strlen(p);
+        if (len >= nl && !strncmp(p, name, nl) && (len == nl || p[nl] == '='))
+            return len == nl ? "" : p + nl + 1;
+        p = end ? end + 1 : nullptr;
+    }
+    return nullptr;
+}
+
+bool env_flag(const char *var, const char *name) { return env_find(var, name) != nullptr; }
+
+long env_num(const char *var, const char *name, long dflt)
+{
+    const char *v = env_find(var, name);
+    return !v ? dflt : *v ? strtol(v, nullptr, 0) : 1;
+}
+
+// SALZ_CHECK=guard (diagnostics): every workspace buffer gets a guard zone filled with a
 // pattern; guard_check() reports the first buffer whose zone was written.
 constexpr size_t kGuardBytes = 1 << 20;
 struct Guard {
@@ -45,7 +68,7 @@ struct Guard {
     uint8_t *zone;
 };
 static thread_local std::vector<Guard> *g_guards = nullptr;
-static bool guard_on() { static const bool on = getenv("SALZ_GUARD") != nullptr; return on; }
+static bool guard_on() { static const bool on = env_flag("SALZ_CHECK", "guard"); return on; }
 
 template <typename T> static int dalloc_named(T **p, size_t count, const char *name, size_t *held)
 {
@@ -163,14 +186,13 @@ int copy_h2d(Workspace &ws, uint8_t *dst, const uint8_t *src, size_t bytes)
     for (size_t o = 0, k = 0; o < bytes; o += kStageChunk, k++) {
         const size_t len = bytes - o < kStageChunk ? bytes - o : kStageChunk;
         const int b = (int)(k & 1);
-        if (k >= 2)  // the DMA that last read this chunk
-            SALZ_HIP(hipEventSynchronize(ws.hstage_ev[b]));
+        // the DMA that last read this chunk, in this call or an earlier one (an event that was
+        // never recorded, or has completed, returns at once)
+        SALZ_HIP(hipEventSynchronize(ws.hstage_ev[b]));
         memcpy(ws.hstage[b], src + o, len);
         SALZ_HIP(hipMemcpyAsync(dst + o, ws.hstage[b], len, hipMemcpyHostToDevice, ws.stream));
         SALZ_HIP(hipEventRecord(ws.hstage_ev[b], ws.stream));
     }
-    // (a later copy_h2d on this context waits on these events before reusing a chunk; every
-    // caller synchronises the stream before returning anyway)
     return 0;
 }
 
@@ -245,10 +267,10 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
         return -1;
     }
     ws.bytes = held;
-    if (const char *pz = getenv("SALZ_POISON")) {
-        // tests/diagnostics: fill the workspace with a pattern so reads of never-written
-        // memory misbehave deterministically instead of depending on what VRAM held before
-        const int v = atoi(pz) & 0xff;
+    if (env_flag("SALZ_CHECK", "poison")) {
+        // tests/diagnostics (SALZ_CHECK=poison=N): fill the workspace with a pattern so reads of
+        // never-written memory misbehave deterministically instead of depending on what VRAM held
+        const int v = (int)env_num("SALZ_CHECK", "poison", 0) & 0xff;
         void *ptrs[] = {ws.rank, ws.sa, ws.keyA, ws.keyB, ws.valA, ws.valB, ws.u0, ws.u1, ws.u2,
                         ws.u3, ws.g64, ws.offA, ws.offB, ws.cand, ws.pst, ws.lsc};
         size_t sizes[] = {4 * n1, 4 * n1, 8 * n1, 8 * n1, 4 * n1, 4 * n1, 4 * n1, 4 * n1, 4 * n1,
@@ -372,7 +394,7 @@ __global__ void k_check_cand(const uint4 *cand, uint32_t n, uint32_t klog, uint3
 
 static int check_stage(Workspace &ws, uint32_t n, int which, const uint32_t *lcp = nullptr)
 {
-    static const bool on = getenv("SALZ_CHECK_STAGES") != nullptr;
+    static const bool on = env_flag("SALZ_CHECK", "stages");
     if (!on)
         return 0;
     uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
@@ -586,7 +608,7 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P
     // 3224 / 3191 -> 3570 / 3567 MB/s (profiles/r03zzz_c3text_klog_ab.txt), though one block alone
     // parses 0.4 ms slower than at K = 64: fewer chunks and exits cost less GPU time in total
     // while other slots keep the GPU busy.
-    if (nbz == 1 && !getenv("SALZ_PARSE_KLOG") && ((ws.sigma > 127 && ws.klog > 7) || (ws.klog < 7 && n > (8u << 20))))
+    if (nbz == 1 && !env_flag("SALZ_PARSE", "klog") && ((ws.sigma > 127 && ws.klog > 7) || (ws.klog < 7 && n > (8u << 20))))
         ws.klog = 7;
     if (guard_check(ws, "sa") || (nbz == 1 && check_stage(ws, n, 2))) return -1;
     if (mark(ws, EV_SA)) return -1;

@@ -30,7 +30,19 @@ struct TextSrc {
     const uint8_t *T;  // padded text
     Blocks g;
     Alpha a;
+    const uint64_t *lrec;  // kMode 4: extraction ranges of the large groups (start << 32 | ...)
+    const uint32_t *tmap;  // kMode 4: large group of the first index of every 256
+    uint32_t GL;
 };
+
+// kMode 4: the large group whose extraction range holds index x (the value). A large group
+// outlasts 256 indices, so it is the group of x's 256-tile start or the next one.
+__device__ __forceinline__ uint32_t group_of(const TextSrc &t, uint32_t x)
+{
+    const uint32_t g = t.tmap[x >> 8];
+    const uint32_t g1 = g + 1u < t.GL ? g + 1u : g;
+    return g1 != g && x >= (uint32_t)(t.lrec[g1] >> 32) ? g1 : g;
+}
 
 // (alphabet keys: t.T is the text mapped to symbols, round0_key_mapped)
 __device__ __forceinline__ uint64_t init_key(const TextSrc &t, uint32_t i, const uint8_t *code)
@@ -58,10 +70,13 @@ __device__ __forceinline__ uint64_t window_key(uint64_t w, uint32_t w9, uint32_t
     return x;
 }
 
-// digit source of a pass: 0 = key bits, 1 / 3 = key bits of text-built pairs, 2 = block of value
-__device__ __forceinline__ unsigned digit_of(int mode, uint64_t k, uint32_t v, int shift, const Blocks &g)
+// digit source of a pass: 0 = key bits, 1 / 3 = key bits of text-built pairs, 2 = block of value,
+// 4 = large group of value
+__device__ __forceinline__ unsigned digit_of(int mode, uint64_t k, uint32_t v, int shift, const TextSrc &t)
 {
-    return mode == 2 ? (g.blk(v) >> shift) & 255u : (unsigned)(k >> shift) & 255u;
+    return mode == 2 ? (t.g.blk(v) >> shift) & 255u
+           : mode == 4 ? (group_of(t, v) >> shift) & 255u
+                       : (unsigned)(k >> shift) & 255u;
 }
 constexpr int kItems = 16;
 constexpr int kTile = kThreads * kItems;
@@ -89,11 +104,11 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
     const size_t base = (size_t)blockIdx.x * kTile;
     const uint4 *kp = reinterpret_cast<const uint4 *>(keys + base);
     const size_t left = m > base ? m - base : 0;
-    if (kMode == 2) {
+    if (kMode == 2 || kMode == 4) {
         for (int j = 0; j < kItems; j++) {
             const size_t i = (size_t)j * kThreads + tid;
             if (i < left)
-                atomicAdd(&mine[digit_of(2, 0, vals[base + i], shift, txt.g)], 1u);
+                atomicAdd(&mine[digit_of(kMode, 0, vals[base + i], shift, txt)], 1u);
         }
     } else if (kMode == 1 && shift == 0 && (txt.a.bits == 0 || ((txt.a.k == 8 || txt.a.k == 9) && txt.a.bits >= 4))) {
         // Round 0's first digit is its key's low byte: the 8th byte (raw keys), or the last
@@ -363,7 +378,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     for (int j = 0; j < IT; j++) {
         size_t i = base + (size_t)j * 64 + lane;
         bool ok = i < m;
-        unsigned d = digit_of(kMode, k[j], v[j], shift, txt.g);
+        unsigned d = digit_of(kMode, k[j], v[j], shift, txt);
         uint64_t peers = wave_ballot(ok);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
@@ -431,16 +446,45 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     }
     __syncthreads();
 
-    if (kMode == 2) {  // block passes (a batch's round 0 only): scatter from registers
+    if (kMode == 2 || kMode == 4) {
+        // block / group passes: the digit is a function of the value, so the values are staged
+        // first (their digits give each slot's destination), then the keys
+        uint32_t pos[IT];
 #pragma unroll
         for (int j = 0; j < IT; j++) {
             const size_t i = base + (size_t)j * 64 + lane;
-            const unsigned d = digit_of(2, 0, v[j], shift, txt.g);
-            if (i < m) {
-                const uint32_t dst = gbase[d] + cnt[wave][d] + lrank[j];
-                kout[dst] = k[j];
-                vout[dst] = v[j];
+            const unsigned d = digit_of(kMode, 0, v[j], shift, txt);
+            pos[j] = dstart[d] + cnt[wave][d] + lrank[j];
+            if (i < m)
+                sval[pos[j]] = v[j];
+        }
+        __syncthreads();
+        const size_t tbase = (size_t)blockIdx.x * kTile;
+        const uint32_t tcount = (uint32_t)((m - tbase) < (size_t)kTile ? (m - tbase) : (size_t)kTile);
+        uint32_t gdst[IT];
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            const uint32_t s = tid + (uint32_t)j * TH;
+            if (s < tcount) {
+                const uint32_t val = sval[s];
+                const unsigned d = digit_of(kMode, 0, val, shift, txt);
+                gdst[j] = gbase[d] + (s - dstart[d]);
+                vout[gdst[j]] = val;
             }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            const size_t i = base + (size_t)j * 64 + lane;
+            if (i < m)
+                skey[pos[j]] = k[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            const uint32_t s = tid + (uint32_t)j * TH;
+            if (s < tcount)
+                kout[gdst[j]] = skey[s];
         }
         return;
     }
@@ -508,15 +552,14 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     // (stable), so the list is ordered by (block, key).
     const int blk_bits = blocks && g.nb > 1 ? bit_width(g.nb - 1u) : 0;
     const int passes_key = (bit_hi - bit_lo + 7) / 8, passes = passes_key + (blk_bits + 7) / 8;
-    // key passes with 512-thread workgroups (8 items per thread; SALZ_RADIX_WG512=0: 256 threads,
-    // 16 items, ~0.5% slower on C2, profiles/r03h_tm_radix_ab.txt)
-    static const bool wg512 = !getenv("SALZ_RADIX_WG512") || atoi(getenv("SALZ_RADIX_WG512")) != 0;
+    // key passes with 512-thread workgroups (8 items per thread; 256 threads with 16 items measured
+    // ~0.5% slower on C2, profiles/r03h_tm_radix_ab.txt)
     // one block with raw-byte or 8/9-symbol keys: the text pass builds keys from an LDS window
     const bool text_win = g.nb == 1 && g.npos >= 7 && (!alpha || alpha->bits == 0 || alpha->k == 8 || alpha->k == 9);
     for (int pass = 0; pass < passes; pass++) {
         const int mode = pass >= passes_key ? 2 : (text && pass == 0) ? (text_win ? 3 : 1) : 0;
         const int shift = mode == 2 ? 8 * (pass - passes_key) : bit_lo + 8 * pass;
-        TextSrc txt{text, g, Alpha{}};
+        TextSrc txt{text, g, Alpha{}, nullptr, nullptr, 0u};
         // digit bytes: written by a key pass for the next key pass, read by that pass's histogram
         const uint8_t *dig_in = digits && (pass > 0 || digits_ready) && mode == 0 ? digits : nullptr;
         uint8_t *dig_out = digits && pass + 1 < passes_key ? digits : nullptr;
@@ -554,11 +597,8 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
         else if (mode == 2)
             hipLaunchKernelGGL((k_radix_scatter<2, kThreads>), dim3(ntiles), dim3(kThreads), 0, st, kin,
                                vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
-        else if (wg512)
-            hipLaunchKernelGGL((k_radix_scatter<0, 512>), dim3(ntiles), dim3(512), 0, st, kin,
-                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
         else
-            hipLaunchKernelGGL((k_radix_scatter<0, kThreads>), dim3(ntiles), dim3(kThreads), 0, st, kin,
+            hipLaunchKernelGGL((k_radix_scatter<0, 512>), dim3(ntiles), dim3(512), 0, st, kin,
                                vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
         SALZ_LAUNCH_CHECK();
         if (timed) {
@@ -568,6 +608,43 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
             ws.stats.radix_scatter_elems += m;
             ws.stats.radix_scatter_bytes += (uint64_t)m * (dig_out ? 25u : 24u);
         }
+        uint64_t *tk = kin;
+        kin = kout;
+        kout = tk;
+        uint32_t *tv = vin;
+        vin = vout;
+        vout = tv;
+    }
+    *keys = kin;
+    *vals = vin;
+    return 0;
+}
+
+int radix_sort_by_group(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt, uint32_t m,
+                        const uint64_t *lrec, const uint32_t *tmap, uint32_t GL, Workspace &ws, hipStream_t st)
+{
+    if (m <= 1 || GL <= 1)
+        return 0;
+    const uint32_t ntiles = (m + kTile - 1) / kTile;
+    const size_t ncounts = (size_t)ntiles * 256;
+    if (ncounts + 256 > ws.radix_counts_elems) {
+        set_error("radix: count buffer too small");
+        return -1;
+    }
+    uint64_t *kin = *keys, *kout = keys_alt;
+    uint32_t *vin = *vals, *vout = vals_alt;
+    TextSrc txt{nullptr, Blocks{0xffffffffu, 1u, m}, Alpha{}, lrec, tmap, GL};
+    const int passes = (bit_width(GL - 1u) + 7) / 8;
+    uint32_t *totals = ws.radix_counts + ncounts;
+    for (int pass = 0; pass < passes; pass++) {
+        hipLaunchKernelGGL(k_radix_hist<4>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, 8 * pass,
+                           ws.radix_counts, ntiles, txt, nullptr);
+        SALZ_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(kRowThreads), 0, st, ws.radix_counts, ntiles, totals);
+        SALZ_LAUNCH_CHECK();
+        hipLaunchKernelGGL((k_radix_scatter<4, kThreads>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, kout, vout,
+                           m, 8 * pass, ws.radix_counts, ntiles, totals, txt, nullptr, 0);
+        SALZ_LAUNCH_CHECK();
         uint64_t *tk = kin;
         kin = kout;
         kout = tk;

@@ -255,10 +255,8 @@ __global__ void k_headpos(HeadBits hb, uint32_t m, uint32_t *__restrict__ headpo
 
 // Survivor masks of wave word w of the list (entries 64w .. 64w + 63): entry c is in a
 // singleton group iff it is a head and so is c + 1 (or c is the last entry). se: entries of
-// groups of size >= 2; sh: heads of those groups. Groups of two that k_pairs finished (their
-// head's bit in pf) leave the list like singletons. All loads unconditional (clamped word).
-__device__ __forceinline__ void surv_masks(const HeadBits &hb, const uint64_t *pf, size_t w, uint32_t m,
-                                           uint64_t &se, uint64_t &sh)
+// groups of size >= 2; sh: heads of those groups. All loads unconditional (clamped word).
+__device__ __forceinline__ void surv_masks(const HeadBits &hb, size_t w, uint32_t m, uint64_t &se, uint64_t &sh)
 {
     const size_t nw = ((size_t)m + 63) / 64;
     const bool more = w + 1 < nw;
@@ -270,115 +268,17 @@ __device__ __forceinline__ void surv_masks(const HeadBits &hb, const uint64_t *p
         nh |= 1ull << (left - 1);  // the last entry's successor is past the list
     se = valid & ~(h & nh);
     sh = valid & h & ~nh;
-    if (pf) {
-        const uint64_t fh = pf[w], fp = pf[w ? w - 1 : 0];
-        const uint64_t fs = (fh << 1) | (w ? fp >> 63 : 0ull);  // the pairs' second entries
-        se &= ~(fh | fs);
-        sh &= ~fh;
-    }
 }
 
 // Per wave word: (survivor entries << 32 | survivor heads); k_commit reads their exclusive scan.
-__global__ __launch_bounds__(kT) void k_surv(HeadBits hb, const uint64_t *__restrict__ pf, uint32_t m,
-                                             uint64_t *__restrict__ P)
+__global__ __launch_bounds__(kT) void k_surv(HeadBits hb, uint32_t m, uint64_t *__restrict__ P)
 {
     const size_t w = (size_t)blockIdx.x * kT + threadIdx.x;
     if (w >= ((size_t)m + 63) / 64)
         return;
     uint64_t se, sh;
-    surv_masks(hb, pf, w, m, se, sh);
+    surv_masks(hb, w, m, se, sh);
     P[w] = ((uint64_t)__popcll(se) << 32) | (uint64_t)__popcll(sh);
-}
-
-// Groups of exactly two members at depth h (a head c whose successor is no head and whose
-// successor's successor is a head or past the list) are decided here by comparing their two
-// suffixes directly past the shared h bytes, eight lanes per pair and 128 bytes per step (the
-// long-compare shape of k_heads_lcp), for at most kPairMax bytes. A decided pair's head gets
-// its bit in pf and its record in pr (mismatch offset L | the second entry sorts first << 31);
-// k_commit then places both suffixes for good (SA, final ranks, and the LCP h + L of the second)
-// instead of keeping them for the next doubling round. Past the end of their block the shorter
-// suffix sorts first, as everywhere in this sort. On text, about a third of the survivors of
-// each round are such pairs, and they are what the late rounds consist of.
-// Final ranks are finer than a depth-h group rank: a later round may then split two suffixes
-// whose h + hk bytes still agree, so k_heads_lcp compares past hk without a bound.
-constexpr uint32_t kPairMax = 1024;
-__global__ __launch_bounds__(kT) void k_pairs(const uint32_t *__restrict__ V, HeadBits hb, uint32_t m, Blocks bl,
-                                              uint32_t h, const uint8_t *__restrict__ T, uint64_t *__restrict__ pf,
-                                              uint32_t *__restrict__ pr, uint32_t *__restrict__ npairs)
-{
-    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
-    const size_t w = c >> 6;
-    if (w * 64 >= m)
-        return;  // whole wave past the end
-    const size_t nw = ((size_t)m + 63) / 64;
-    const bool more = w + 1 < nw;
-    const uint64_t H = hb.hmask[w], Hn = hb.hmask[more ? w + 1 : w];
-    const uint64_t left = (uint64_t)m - (uint64_t)w * 64;  // >= 1
-    const uint64_t valid = left >= 64 ? ~0ull : (1ull << left) - 1ull;
-    const uint64_t past1 = left >= 65 ? 0ull : ~0ull << (left - 1);  // c + 1 >= m
-    const uint64_t past2 = left >= 66 ? 0ull : ~0ull << (left >= 2 ? left - 2 : 0);  // c + 2 >= m
-    const uint64_t nh = (H >> 1) | (more ? Hn << 63 : 0ull) | past1;
-    const uint64_t nnh = (H >> 2) | (more ? Hn << 62 : 0ull) | past2;
-    const uint64_t ph = valid & H & ~nh & nnh;  // heads of groups of two
-    uint64_t pend = ph, done = 0;
-    const uint32_t lane = lane_id(), sub = lane >> 3, sl8 = lane & 7u;
-    while (pend) {
-        uint64_t pk = pend;  // group `sub` takes the sub-th pending pair in lane order
-        for (uint32_t u = 0; u < sub; u++)
-            pk &= pk - 1;
-        const bool have = pk != 0;
-        const uint32_t src = have ? (uint32_t)__ffsll((unsigned long long)pk) - 1u : 0u;
-        uint64_t batch = pend;  // the (up to) eight pairs of this step, for the result bits
-        for (uint32_t u = 0; u < 8; u++)
-            pend &= pend - 1;
-        batch &= ~pend;
-        const size_t ch = w * 64 + src;
-        const uint32_t i = V[have ? ch : w * 64], j = V[have ? ch + 1 : w * 64];  // (clamped: c + 1 < m)
-        const uint32_t e = bl.end(i), mx = i > j ? i : j;
-        const uint32_t lim = e - mx > h ? e - mx - h : 0u;  // bytes both suffixes have past h
-        const uint32_t sl = have ? (lim < kPairMax ? lim : kPairMax) : 0u;
-        // (a lane without a pair reads the text's first bytes: a list entry may be shorter than h)
-        const size_t si = have ? (size_t)i + h : 0, sj = have ? (size_t)j + h : 0;
-        uint32_t mis = 0xffffffffu;
-        for (uint32_t base = 0;; base += 8 * 16) {
-            const uint32_t off = base + sl8 * 16, offc = off < sl ? off : 0u;
-            const uint64_t x0 = load_u64_any(T, si + offc) ^ load_u64_any(T, sj + offc);
-            const uint64_t x1 = load_u64_any(T, si + offc + 8) ^ load_u64_any(T, sj + offc + 8);
-            uint32_t mm = 0xffffffffu;
-            if (off < sl && (x0 | x1))
-                mm = x0 ? off + ((uint32_t)__builtin_ctzll(x0) >> 3) : off + 8u + ((uint32_t)__builtin_ctzll(x1) >> 3);
-            mm = umin_(mm, shfl_xor_u32(mm, 1));
-            mm = umin_(mm, shfl_xor_u32(mm, 2));
-            mm = umin_(mm, shfl_xor_u32(mm, 4));
-            if (mis == 0xffffffffu)
-                mis = mm;
-            const bool fin = mis != 0xffffffffu || base + 8 * 16 >= sl;
-            if (!wave_ballot(!fin))
-                break;
-        }
-        // decided: a mismatch inside both suffixes, or one of them ends within kPairMax bytes
-        const bool hit = mis < sl;
-        const bool decided = have && (hit || lim <= kPairMax);
-        if (decided && sl8 == 0) {
-            const uint32_t L = hit ? mis : lim;
-            // the second entry sorts first when its byte at the mismatch is smaller, or when
-            // the first entry's suffix is the longer one and the shorter ran out
-            const bool swap = hit ? T[sj + L] < T[si + L] : j > i;
-            pr[ch] = L | (swap ? 0x80000000u : 0u);
-        }
-        const uint64_t dl = wave_ballot(decided && sl8 == 0);  // bit 8 * sub
-        for (uint32_t u = 0; u < 8 && batch; u++) {
-            const uint64_t b = batch & (~batch + 1ull);  // u-th pair of the step, in lane order
-            batch &= batch - 1;
-            if ((dl >> (8 * u)) & 1ull)
-                done |= b;
-        }
-    }
-    if (lane == 0) {
-        pf[w] = done;
-        if (npairs && done)
-            atomicAdd(npairs, (uint32_t)__popcll(done));
-    }
 }
 
 // Next round's group table (ginfo: size << 32 | compact start) is written by each surviving
@@ -389,6 +289,9 @@ struct GroupTab {
     uint32_t *lg2g;
 };
 
+// gin: the text round (round 1 keyed by text, below): entry c's group id, which its key no
+// longer holds; every rank is written there (no entry keeps one: round 0 wrote no survivor's).
+// surv_rank = 0: round 0 before a text round writes only the ranks of the suffixes it finishes.
 __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
                          HeadBits hb, const uint32_t *__restrict__ headpos,
                          const uint64_t *__restrict__ P, unsigned long long *__restrict__ lcount,
@@ -397,8 +300,7 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
                          uint32_t *__restrict__ rank, uint32_t *__restrict__ sa, GroupTab tab,
                          uint32_t m, uint32_t n, uint32_t nsa, int kb_old, int round0, uint32_t *err,
                          uint32_t ihi, uint32_t *__restrict__ later, uint32_t gbase,
-                         const uint64_t *__restrict__ pf, const uint32_t *__restrict__ pr,
-                         uint32_t *__restrict__ lcps, uint32_t hdepth)
+                         const uint32_t *__restrict__ gin, int surv_rank)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
@@ -407,40 +309,31 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     const uint32_t g = gid1(hb, c, bit) - 1u;
     uint32_t hp = headpos[g];
     uint32_t size = headpos[g + 1] - hp;
-    uint32_t o = round0 ? 0u : off_old[(uint32_t)(key[c] >> kb_old)];
+    uint32_t o = round0 ? 0u : off_old[gin ? gin[c] : (uint32_t)(key[c] >> kb_old)];
     uint32_t i = val[c];
     if (bad_index(i >= n || c + o >= nsa || hp > c || size > m, err, kErrCommit))
         return;
     // The first subgroup of an old group keeps the old group's head, so its members' ranks
-    // are unchanged; every other rank (and all of round 0) is written.
-    const bool same = !round0 && (hp == 0 || (key[hp - 1] >> kb_old) != (key[hp] >> kb_old));
-    // A group of two that k_pairs decided: both members take their final places now (the
-    // second of them also its LCP with the first); ranks are final positions + 1.
-    const bool pair = size == 2 && pf && ((pf[hp >> 6] >> (hp & 63u)) & 1ull);
-    uint32_t slot = c + o, rpos = hp + o;  // SA slot (singletons, pairs); rank = group head's + 1
-    if (pair) {
-        const uint32_t rec = pr[hp];
-        slot = rpos = hp + o + (((uint32_t)c - hp) ^ (rec >> 31));
-        if (lcps && slot == hp + o + 1u)
-            lcps[slot] = hdepth + (rec & 0x7fffffffu);
-    }
+    // are unchanged; every other rank (and all of round 0 and the text round) is written.
+    const bool same = !round0 && !gin && (hp == 0 || (key[hp - 1] >> kb_old) != (key[hp] >> kb_old));
+    const uint32_t slot = c + o, rpos = hp + o;  // SA slot (singletons); rank = group head's + 1
     // rank[i] is a random 4-byte scatter (a read-modify-write of a whole HBM burst). Large
     // rounds write only the ranks of i < ihi here and leave every update in list order in
     // `later` for the split passes (k_rank_upper) or the staged scatter (k_rank_apply); small
     // ones write rank directly (ihi = ~0, no `later`). The entry that keeps its old head's
     // place keeps its rank.
-    const bool keep = same && rpos == hp + o;
+    const bool keep = (same && rpos == hp + o) || (!surv_rank && size > 1);
     const uint32_t rv = keep ? 0xffffffffu : gbase + rpos + 1u;  // (gbase: a split block's bucket)
     if (!keep && i < ihi)
         rank[i] = rv;
     if (later)
         later[c] = rv;
-    if (size == 1 || pair) {
+    if (size == 1) {
         sa[slot] = i;
     } else {
         // compact index = survivor entries before c, new group id = survivor heads up to c - 1
         uint64_t se, sh;
-        surv_masks(hb, pf, c >> 6, m, se, sh);
+        surv_masks(hb, c >> 6, m, se, sh);
         const uint64_t pw = P[c >> 6], below = (1ull << (c & 63u)) - 1ull;
         const uint32_t idx = (uint32_t)(pw >> 32) + (uint32_t)__popcll(se & below);
         const uint32_t ng = (uint32_t)pw + (uint32_t)__popcll(sh & (below | (below + 1ull))) - 1u;
@@ -507,9 +400,8 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
             pos = (uint32_t)c + o;
             // (same group, so the same block: e1 bounds both suffixes)
             if (!bad_index(i >= e1 || j >= e1 || pos >= bl.nsa() || e1 - mx < hk, err, kErrCommit)) {
-                // Up to the end of the text: the keys differ, so normally within hk bytes, but
-                // a pair finished early (k_pairs) carries final ranks, which can split two
-                // suffixes whose next hk bytes still agree.
+                // (the keys differ, so the suffixes differ within hk bytes; lim bounds the
+                // compare by the end of the text)
                 lim = e1 - mx - hk;
                 if (hk <= kLcpLane) {
                     uint32_t l = lim;
@@ -1011,6 +903,330 @@ __global__ void k_keys(const uint32_t *__restrict__ nval, const uint32_t *__rest
     key[c] = ((uint64_t)ngid[c] << kb) | (uint64_t)rank[i + h];
 }
 
+// ---- round 1 keyed by text ------------------------------------------------------------------
+// Round 1 orders each depth-h0 group by rank[i + h0], the depth-h0 rank of suffix i + h0. That
+// rank is an order-preserving name of the h0 symbols at i + h0, so the round can compare those
+// symbols themselves (the round-0 key at i + h0) instead. Then round 0 writes only the ranks of
+// the suffixes it finishes (16% of a text block) instead of all n, and the LCP of round 1's new
+// heads comes from the two keys instead of a random text read per head; round 1 writes every
+// rank of its list. The keys are h0 symbols of >= 1 (an alphabet of at most 127 bytes, Alpha):
+// a key padded with zeros past the end of the text is then never equal to a longer suffix's.
+// The group of an entry is no longer in its key: `gin` holds it.
+
+// Round 1's key of survivor nval[c]: the round-0 key at i + h0 (a survivor has h0 symbols left),
+// from the text mapped to symbols (Tm).
+__global__ void k_keys_text(const uint32_t *__restrict__ nval, uint32_t m, Blocks bl, Alpha a, uint32_t h0,
+                            const uint8_t *__restrict__ Tm, uint64_t *__restrict__ key)
+{
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (c >= m)
+        return;
+    const uint32_t i = nval[c];
+    key[c] = round0_key_mapped(Tm, i + h0, bl.end(i), a);
+}
+
+// Group heads of the text round's sorted list, and the LCP of each new head (two suffixes of one
+// depth-h0 group: h0 + the equal leading symbols of their keys; a key padded past the end of the
+// text stops at its first zero symbol, so the LCP is exact).
+__global__ __launch_bounds__(kT) void k_heads_text(const uint64_t *__restrict__ K, const uint32_t *__restrict__ gin,
+                                                   HeadBits hb, const uint32_t *__restrict__ off_old, uint32_t m,
+                                                   Alpha a, uint32_t h0, uint32_t *__restrict__ lcps)
+{
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    const bool in = c < m;
+    const size_t cc = in ? c : 0, cp = cc ? cc - 1 : 0;  // (unconditional loads)
+    const uint64_t k0 = K[cp], k1 = K[cc];
+    const uint32_t g0 = gin[cp], g1 = gin[cc];
+    const bool head = cc == 0 || g0 != g1 || k0 != k1;
+    put_heads(hb, c, m, in && head);
+    if (lcps && in && head && cc > 0 && g0 == g1)
+        lcps[(uint32_t)cc + off_old[g1]] = h0 + round0_lcp(k0 ^ k1, a);
+}
+
+// The small groups of one window sorted by (group, key) in LDS. The LSD passes sort (local group,
+// top key bits, slot), with as many top bits as keep the sort at 40 bits (5 passes); the runs of
+// equal (group, top bits) that remain are marked (rb, need) and ordered by the whole key in
+// k_seg_text_fix. Windows of tiny groups count on the whole key here.
+__global__ __launch_bounds__(kSegThreads) void k_seg_small_text(uint64_t *__restrict__ K, uint32_t *__restrict__ V,
+                                                                const uint32_t *__restrict__ gin, SegPlan plan,
+                                                                const uint64_t *__restrict__ ginfo, uint32_t m,
+                                                                int tbits, uint32_t tiny,
+                                                                uint64_t *__restrict__ rb, uint32_t *__restrict__ need,
+                                                                uint32_t *err)
+{
+    __shared__ uint64_t sk[kSegCap];
+    __shared__ uint32_t sv[kSegCap];
+    __shared__ uint32_t cnt[4][256];
+    __shared__ uint32_t wsum[4];
+
+    const unsigned tid = threadIdx.x;
+    const uint32_t w = blockIdx.x;
+    const uint32_t lo = plan.lo[w];
+    if (lo == 0xffffffffu)
+        return;
+    const uint32_t hi = plan.hi[w], g0 = plan.g0[w], g1 = plan.g1[w];
+    if (bad_index(hi > m || hi <= lo || hi - lo >= kSegCap || g1 < g0, err, kErrSeg))
+        return;
+    const uint32_t count = hi - lo;
+    const int gbits = 32 - __builtin_clz((g1 - g0) | 1u);
+    // top key bits in the LSD key: a 40-bit sort (5 passes; 48 and 52 bits measured slower, the
+    // extra passes costing more than the shorter runs save in k_seg_text_fix)
+    const int kbt = tbits < 40 - gbits ? tbits : 40 - gbits;
+    const int items = count <= 1024u ? 4 : (int)((count + 255u) / 256u);
+    constexpr uint32_t kPer = kSegCap / kSegThreads;
+
+    uint32_t gmax = 0;
+    if (tiny) {
+        for (uint32_t g = g0 + tid; g <= g1; g += kSegThreads) {
+            const uint32_t sz = (uint32_t)(ginfo[g] >> 32);
+            gmax = sz > gmax ? sz : gmax;
+        }
+        gmax = wave_max_u32(gmax);
+        if (lane_id() == 0)
+            wsum[tid >> 6] = gmax;
+    }
+    __syncthreads();
+    const uint32_t m01 = wsum[0] > wsum[1] ? wsum[0] : wsum[1], m23 = wsum[2] > wsum[3] ? wsum[2] : wsum[3];
+    if (tiny && (m01 > m23 ? m01 : m23) <= tiny) {
+        // tiny groups: each entry's place is its group's start + the members with a smaller
+        // (key, slot)
+        for (uint32_t i = tid; i < count; i += kSegThreads) {
+            sk[i] = K[lo + i];
+            sv[i] = V[lo + i];
+        }
+        __syncthreads();
+        uint32_t dst[kPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j++) {
+            const uint32_t i = tid + j * kSegThreads, ii = i < count ? i : 0u;
+            const uint64_t ki = sk[ii];
+            const uint64_t gi = ginfo[gin[lo + ii]];  // (unconditional loads: clamped entry)
+            const uint32_t gs = (uint32_t)gi - lo, sz = (uint32_t)(gi >> 32);
+            uint32_t r = 0;
+            for (uint32_t x = gs; x < gs + sz; x++) {
+                const uint64_t kx = sk[x];
+                r += (kx < ki || (kx == ki && x < ii)) ? 1u : 0u;
+            }
+            dst[j] = lo + gs + r;
+        }
+        __syncthreads();  // (every dst computed before any store: they may land in this window)
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j++) {
+            const uint32_t i = tid + j * kSegThreads;
+            if (i < count) {
+                K[dst[j]] = sk[i];
+                V[dst[j]] = sv[i];
+            }
+        }
+        return;
+    }
+    for (uint32_t i = tid; i < (uint32_t)items * kSegThreads; i += kSegThreads) {
+        uint64_t key = ~0ull;  // padding sorts last in every digit
+        if (i < count) {
+            const uint64_t kk = K[lo + i];
+            sv[i] = V[lo + i];
+            key = ((uint64_t)(gin[lo + i] - g0) << (kbt + 12)) | ((kk >> (tbits - kbt)) << 12) | i;
+        }
+        sk[i] = key;
+    }
+    const int nbits = gbits + kbt;
+    switch (items) {
+    case 4: seg_lsd<4>(sk, cnt, wsum, nbits); break;
+    case 5: seg_lsd<5>(sk, cnt, wsum, nbits); break;
+    case 6: seg_lsd<6>(sk, cnt, wsum, nbits); break;
+    case 7: seg_lsd<7>(sk, cnt, wsum, nbits); break;
+    case 8: seg_lsd<8>(sk, cnt, wsum, nbits); break;
+    case 9: seg_lsd<9>(sk, cnt, wsum, nbits); break;
+    case 10: seg_lsd<10>(sk, cnt, wsum, nbits); break;
+    case 11: seg_lsd<11>(sk, cnt, wsum, nbits); break;
+    case 12: seg_lsd<12>(sk, cnt, wsum, nbits); break;
+    case 13: seg_lsd<13>(sk, cnt, wsum, nbits); break;
+    case 14: seg_lsd<14>(sk, cnt, wsum, nbits); break;
+    case 15: seg_lsd<15>(sk, cnt, wsum, nbits); break;
+    default: seg_lsd<16>(sk, cnt, wsum, nbits); break;
+    }
+    // Runs of equal (group, top bits): their starts as bits (to rb, for k_seg_text_fix); every
+    // entry written back in this order with its whole key (re-read from K: this window's range
+    // is written only at the end) and its value.
+    uint64_t full[kPer];
+    uint32_t vv[kPer];
+    bool tie = false;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t i = tid + j * kSegThreads, ii = i < count ? i : 0u;
+        const uint64_t key = sk[ii], prev = sk[ii ? ii - 1 : 0];
+        const uint32_t slot = (uint32_t)key & 0xfffu;
+        if (j < (uint32_t)items) {
+            full[j] = K[lo + slot];
+            vv[j] = sv[slot];
+        }
+        const bool start = ii == 0 || (key >> 12) != (prev >> 12);
+        tie = tie || (i < count && !start);
+        const uint64_t bits = wave_ballot(i < count && start);
+        if (lane_id() == 0 && j < (uint32_t)items)
+            rb[(size_t)w * (kSegCap / 64) + ((j * kSegThreads + (tid & ~63u)) >> 6)] = bits;
+    }
+    if (__syncthreads_or(tie) && tid == 0)
+        need[w] = 1u;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t i = tid + j * kSegThreads;
+        if (j < (uint32_t)items && i < count) {
+            K[lo + i] = full[j];
+            V[lo + i] = vv[j];
+        }
+    }
+}
+
+// The runs of equal (group, top key bits) that k_seg_small_text left (windows flagged in need),
+// each ordered by the whole key: runs of up to kRunCount entries by counting (each entry's place
+// is the run start + the entries with a smaller (key, index): at depth 13-14 of text a run holds
+// 14-20 entries on average), longer ones (a window may hold one of 2000) by a bitonic sort of the
+// run in LDS, the whole workgroup on one run at a time.
+constexpr uint32_t kRunCount = 64;
+constexpr uint32_t kMaxLongRuns = 64;
+__global__ __launch_bounds__(kSegThreads) void k_seg_text_fix(uint64_t *__restrict__ K, uint32_t *__restrict__ V,
+                                                              SegPlan plan, const uint64_t *__restrict__ rb,
+                                                              const uint32_t *__restrict__ need)
+{
+    __shared__ uint64_t sk[kSegCap];
+    __shared__ uint32_t sv[kSegCap];
+    __shared__ uint64_t runb[kSegCap / 64];
+    __shared__ uint32_t longs[kMaxLongRuns];  // (start << 16 | end) of the long runs
+    __shared__ uint32_t nlong;
+    const unsigned tid = threadIdx.x;
+    const uint32_t w = blockIdx.x;
+    if (!need[w])
+        return;
+    const uint32_t lo = plan.lo[w], count = plan.hi[w] - lo;  // (checked by k_seg_small_text)
+    const uint32_t nwords = (count + 63u) >> 6;
+    if (tid == 0)
+        nlong = 0;
+    for (uint32_t i = tid; i < count; i += kSegThreads) {
+        sk[i] = K[lo + i];
+        sv[i] = V[lo + i];
+    }
+    for (uint32_t q = tid; q < nwords; q += kSegThreads)
+        runb[q] = rb[(size_t)w * (kSegCap / 64) + q];
+    __syncthreads();
+    // run [rs, re) of entry i: the last start at or below i, the next start above it
+    auto run_of = [&](uint32_t i, uint32_t &rs, uint32_t &re) {
+        uint32_t wi = i >> 6;
+        uint64_t x = runb[wi] & (~0ull >> (63u - (i & 63u)));
+        while (!x)
+            x = runb[--wi];
+        rs = wi * 64u + 63u - (uint32_t)__builtin_clzll(x);
+        wi = i >> 6;
+        x = (i & 63u) == 63u ? 0ull : runb[wi] & (~0ull << ((i & 63u) + 1u));
+        while (!x && ++wi < nwords)
+            x = runb[wi];
+        re = x ? wi * 64u + (uint32_t)__builtin_ctzll(x) : count;
+    };
+    // the long runs, listed by their first entries
+    for (uint32_t i = tid; i < count; i += kSegThreads)
+        if ((runb[i >> 6] >> (i & 63u)) & 1ull) {
+            uint32_t rs, re;
+            run_of(i, rs, re);
+            if (re - rs > kRunCount) {
+                const uint32_t k = atomicAdd(&nlong, 1u);
+                if (k < kMaxLongRuns)
+                    longs[k] = (rs << 16) | re;
+            }
+        }
+    __syncthreads();
+    const uint32_t nl = nlong < kMaxLongRuns ? nlong : kMaxLongRuns;  // (a window holds < 64 runs of > 64)
+    for (uint32_t r = 0; r < nl; r++) {
+        const uint32_t rs = longs[r] >> 16, len = (longs[r] & 0xffffu) - rs;
+        uint32_t P = 1;
+        while (P < len)
+            P <<= 1;
+        // ascending-only bitonic network (first step of each merge pairs i with its mirror), so
+        // the entries past len act as +inf and are never touched
+        for (uint32_t k = 2; k <= P; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t t = tid; t < P / 2; t += kSegThreads) {
+                    const uint32_t i = 2 * t - (t & (j - 1));
+                    const uint32_t p = j == (k >> 1) ? (i | (k - 1)) - (i & (k - 1)) : i + j;
+                    if (p < len) {
+                        const uint64_t a = sk[rs + i], b = sk[rs + p];
+                        if (b < a) {
+                            const uint32_t va = sv[rs + i], vb = sv[rs + p];
+                            sk[rs + i] = b;
+                            sk[rs + p] = a;
+                            sv[rs + i] = vb;
+                            sv[rs + p] = va;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+    }
+    for (uint32_t i = tid; i < count; i += kSegThreads) {
+        uint32_t rs, re;
+        run_of(i, rs, re);
+        if (re - rs < 2)
+            continue;
+        uint32_t dst = i;
+        const uint64_t ki = sk[i];
+        if (re - rs <= kRunCount) {
+            uint32_t r = 0;
+#pragma unroll 8
+            for (uint32_t y = rs; y < re; y++) {
+                const uint64_t ky = sk[y];
+                r += (ky < ki || (ky == ki && y < i)) ? 1u : 0u;
+            }
+            dst = rs + r;
+        }
+        K[lo + dst] = ki;
+        V[lo + dst] = sv[i];
+    }
+}
+
+// The text round's large groups: extracted with their keys, their extraction index as the value
+// (so a radix sort on the keys followed by one on the large group of the value orders them by
+// (group, key)) and their suffixes aside in PC.
+__global__ void k_extract_text(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
+                               const uint64_t *__restrict__ lrec, const uint32_t *__restrict__ tmap, uint32_t GL,
+                               uint32_t m, uint32_t mL, uint64_t *__restrict__ KC, uint32_t *__restrict__ VC,
+                               uint32_t *__restrict__ PC, uint32_t *err)
+{
+    const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (x >= mL)
+        return;
+    const uint32_t lg0 = tmap[blockIdx.x];
+    const uint64_t r0 = lrec[lg0], r1 = lrec[lg0 + 1u < GL ? lg0 + 1u : lg0];  // unconditional loads
+    const bool next = lg0 + 1u < GL && x >= (r1 >> 32);
+    const uint64_t r = next ? r1 : r0;
+    const uint32_t orig = (uint32_t)r + (uint32_t)(x - (r >> 32));
+    if (bad_index(orig >= m, err, kErrExtract))
+        return;
+    KC[x] = K[orig];
+    VC[x] = (uint32_t)x;
+    PC[x] = V[orig];
+}
+
+// Sorted position y of the extracted array (now in (large group, key) order, so y lies in its
+// group's extraction range) back to its place in the list.
+__global__ void k_putback_text(const uint64_t *__restrict__ KS, const uint32_t *__restrict__ VS,
+                               const uint32_t *__restrict__ PC, const uint64_t *__restrict__ lrec,
+                               const uint32_t *__restrict__ tmap, uint32_t GL, uint32_t m, uint32_t mL,
+                               uint64_t *__restrict__ K, uint32_t *__restrict__ V, uint32_t *err)
+{
+    const size_t y = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (y >= mL)
+        return;
+    const uint32_t lg0 = tmap[blockIdx.x];
+    const uint64_t r0 = lrec[lg0], r1 = lrec[lg0 + 1u < GL ? lg0 + 1u : lg0];
+    const bool next = lg0 + 1u < GL && y >= (r1 >> 32);
+    const uint64_t r = next ? r1 : r0;
+    const uint32_t orig = (uint32_t)r + (uint32_t)(y - (r >> 32));
+    const uint32_t x = VS[y];
+    if (bad_index(orig >= m || x >= mL, err, kErrPutback))
+        return;
+    K[orig] = KS[y];
+    V[orig] = PC[x];
+}
+
 }  // namespace
 
 int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
@@ -1040,23 +1256,23 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     GroupTab tab{reinterpret_cast<uint64_t *>(cb + 4 * ws.cap_s), ws.lrec, ws.lg2g};
     uint64_t *KC = ws.pst;
 
-    static const bool dbg_rounds = getenv("SALZ_CHECK_ROUNDS") != nullptr;
-    const char *lcp_env = getenv("SALZ_LCP_SA");  // tests: "0" forces the Phi/PLCP stage
-    ws.lcps_ok = !lcp_env || atoi(lcp_env) != 0;
+    // Test switches (SALZ_SA, a comma-separated list): plcp, noalpha, dc3, doubling,
+    // noprobe, global, segmented, tiny=N, rank1; SALZ_CHECK=rounds,sa and SALZ_DEBUG=sa.
+    static const bool dbg_rounds = env_flag("SALZ_CHECK", "rounds");
+    ws.lcps_ok = !env_flag("SALZ_SA", "plcp");  // plcp: the LCP from the Phi/PLCP stage instead
     // Round 0's alphabet: texts of at most 127 distinct bytes get compacted keys (Alpha,
-    // common.hpp); SALZ_ALPHA=0 keeps raw 8-byte keys (tests run both).
+    // common.hpp); SALZ_SA=noalpha keeps raw 8-byte keys (tests run both).
     Alpha alpha{};
-    const bool alpha_on = !getenv("SALZ_ALPHA") || atoi(getenv("SALZ_ALPHA")) != 0;
-    // DC3 (dc3.hip) instead of doubling for repetitive single blocks: SALZ_SA_ALGO=dc3 forces it,
+    const bool alpha_on = !env_flag("SALZ_SA", "noalpha");
+    // DC3 (dc3.hip) instead of doubling for repetitive single blocks: SALZ_SA=dc3 forces it,
     // =doubling never. By default a block of >= 1 MiB starts with DC3 when the repetition probe
     // finds half of its sampled 32-grams repeated, and otherwise switches once the sort has reached depth 32
     // with more than 3/4 of its suffixes still unfinished (long repeats: the following rounds stay
     // that wide; text keeps ~17% at depth 32, Fibonacci and periodic blocks all of them).
-    const char *algo_env = getenv("SALZ_SA_ALGO");
-    const bool dc3_force = algo_env && !strcmp(algo_env, "dc3") && bl.nb == 1 && n >= 2 && !dist;
-    const bool dc3_auto = !(algo_env && !strcmp(algo_env, "doubling")) && bl.nb == 1 && n >= (1u << 20) && !dist;
-    // SALZ_SA_PROBE=0: no repetition probe (only the depth-32 switch)
-    const bool dc3_probe_off = getenv("SALZ_SA_PROBE") && atoi(getenv("SALZ_SA_PROBE")) == 0;
+    const bool dc3_force = env_flag("SALZ_SA", "dc3") && bl.nb == 1 && n >= 2 && !dist;
+    const bool dc3_auto = !env_flag("SALZ_SA", "doubling") && bl.nb == 1 && n >= (1u << 20) && !dist;
+    // SALZ_SA=noprobe: no repetition probe (only the depth-32 switch)
+    const bool dc3_probe_off = env_flag("SALZ_SA", "noprobe");
     bool dc3_now = false;
     Alpha codes{};  // the block's byte codes 1..sigma for DC3 (raw bytes + 1 when not known)
     int codes_raw = 1;
@@ -1089,21 +1305,21 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         if (bits <= 7) {
             // As many symbols as fit 64 bits: 7-bit alphabets (text) sort round 0 to depth 9 in
             // 8 passes rather than depth 8 in 7; the deeper start leaves fewer suffixes to the
-            // doubling rounds (text surrogate: 12% fewer after round 0, 14% after round 1).
-            // SALZ_ALPHA_K8=1 keeps 8 symbols for 5..7-bit alphabets (the round-2 choice).
-            static const bool k8 = getenv("SALZ_ALPHA_K8") && atoi(getenv("SALZ_ALPHA_K8")) != 0;
+            // doubling rounds (text surrogate: 12% fewer after round 0, 14% after round 1; C2 SA
+            // 22.2 -> 21.6 ms against 8 symbols, profiles/r03g_alpha9_ab.txt).
             alpha.bits = bits;
-            alpha.k = bits >= 5 && k8 ? 8u : 64u / bits;
+            alpha.k = 64u / bits;
         }
     }
     if (dc3_force || dc3_now)
         return stage_suffix_array_dc3(ws, bl, codes, codes_raw);
     const uint32_t h0 = alpha.bits ? alpha.k : 8u;
-    // The text mapped to symbols for the text-sourced radix pass (u1 is free until round 0's
-    // group sums): one byte per position, zero padded.
+    // The text mapped to symbols for the text-sourced radix pass and the text round's keys (u3
+    // is free until round 0's commit writes the group ids, which go to `gin` before a text
+    // round): one byte per position, zero padded.
     uint8_t *tmapped = nullptr;
     if (alpha.bits) {
-        tmapped = reinterpret_cast<uint8_t *>(ws.u1);
+        tmapped = reinterpret_cast<uint8_t *>(ws.u3);
         const size_t P = (size_t)n + 8;
         hipLaunchKernelGGL(k_map_text, dim3(grid_for(P + 64, kT * 16)), dim3(kT), 0, st, ws.text, P, alpha,
                            tmapped);
@@ -1116,15 +1332,12 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     }
     // Round 0's first radix pass reads the text itself (radix.hip, TextSrc); the initial
     // key/value arrays are only materialised for the per-round checks, and for n = 1 (the
-    // sort has nothing to do and would leave them unwritten).
-    // SALZ_TEXT_FIRST=0: a single block's list is materialised (k_sa_init, with the first
-    // pass's digit bytes) and every pass reads it
-    const bool text_src_env = !getenv("SALZ_TEXT_FIRST") || atoi(getenv("SALZ_TEXT_FIRST")) != 0;
-    const bool text_first = !dbg_rounds && nsa > 1 && !dist && (bl.nb > 1 || text_src_env);
+    // sort has nothing to do and would leave them unwritten; the materialised list measured
+    // 0.1-0.2 ms slower).
+    const bool text_first = !dbg_rounds && nsa > 1 && !dist;
     // Digit bytes of the radix passes (radix.hip) in u2, free during every sort (the head
-    // positions are written after it); SALZ_RADIX_DIGITS=0: histograms read the keys
-    uint8_t *rdig = getenv("SALZ_RADIX_DIGITS") && atoi(getenv("SALZ_RADIX_DIGITS")) == 0
-                        ? nullptr : reinterpret_cast<uint8_t *>(ws.u2);
+    // positions are written after it)
+    uint8_t *rdig = reinterpret_cast<uint8_t *>(ws.u2);
     if (dist) {
         hipLaunchKernelGGL(k_list_init, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.text, dist->list, nsa, n, alpha,
                            K, V);
@@ -1151,19 +1364,20 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     uint32_t m = nsa, h = h0, G_act = 0, GL = 0, mL = 0;
     int kb_old = 0, round0 = 1;
     const int kb = bit_width(n);
-    static const bool verbose = getenv("SALZ_DEBUG_SA") != nullptr;
-    const char *mode_env = getenv("SALZ_SA_MODE");  // tests: "global" or "segmented"
+    static const bool verbose = env_flag("SALZ_DEBUG", "sa");
+    const bool mode_global = env_flag("SALZ_SA", "global"), mode_seg = env_flag("SALZ_SA", "segmented");
     // k_seg_small windows whose groups all have at most seg_tiny members are ordered by counting
-    // (SALZ_SEG_TINY=0: LSD passes everywhere)
+    // (SALZ_SA=tiny=0: LSD passes everywhere)
     // (64: 32, 96 and 128 measured within 0.2 ms of it, 32 up to 0.2 ms slower on mixed data)
-    const uint32_t seg_tiny = getenv("SALZ_SEG_TINY") ? (uint32_t)atoi(getenv("SALZ_SEG_TINY")) : 64u;
-    // Groups of two finished by a direct compare each round (k_pairs, SALZ_SA_PAIRS=1), from the
-    // round whose groups share SALZ_SA_PAIRS_H bytes on. Off by default: on the text surrogate
-    // it measured even at every threshold (C2 SA 22.2 ms at 64 and 256 bytes, 22.9 from 16,
-    // against 22.2 without; profiles/r03e_pairs_ab.txt): what the smaller late rounds save,
-    // k_pairs and the longer head compares it causes (k_heads_lcp) spend again.
-    const bool pairs_on = getenv("SALZ_SA_PAIRS") && atoi(getenv("SALZ_SA_PAIRS")) != 0;
-    const uint32_t pairs_h = getenv("SALZ_SA_PAIRS_H") ? (uint32_t)atoi(getenv("SALZ_SA_PAIRS_H")) : 64u;
+    const uint32_t seg_tiny = (uint32_t)env_num("SALZ_SA", "tiny", 64);
+    // Round 1 keyed by text (see k_keys_text): one block or a batch, the block's own sort (not a
+    // split block's bucket), an alphabet of at most 127 bytes (symbols >= 1, so zero padding
+    // is unambiguous). SALZ_SA=rank1 keeps round 1 on ranks.
+    const bool text1 = !env_flag("SALZ_SA", "rank1") && !dist && !dbg_rounds && alpha.bits > 0;
+    const int tbits = (int)(alpha.k * alpha.bits);
+    // group ids of the text round's list (its keys are the text): the upper half of lsc, free
+    // during every round (the window plan and tile map take its first entries)
+    uint32_t *gin = reinterpret_cast<uint32_t *>(ws.lsc) + 2 * ws.cap_s;
     auto t_round = std::chrono::steady_clock::now();
     for (;;) {
         ws.stats.sa_rounds++;
@@ -1172,7 +1386,50 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         uint32_t *Vx = (V == ws.valA) ? ws.valB : ws.valA;
         const char *how = "global";
         bool seg_round = false;
-        if (round0) {
+        const bool textr = text1 && ws.stats.sa_rounds == 2;  // this round is keyed by text
+        if (textr) {
+            // small groups in LDS by (group, key); large ones extracted, radix-sorted on the key
+            // and then on their large group (values = extraction index), put back
+            how = "text";
+            seg_round = true;
+            const uint32_t nwin = grid_for(m, kSegT);
+            uint32_t *pw = reinterpret_cast<uint32_t *>(ws.lsc);
+            SegPlan plan{pw, pw + nwin, pw + 2 * nwin, pw + 3 * nwin};
+            SALZ_HIP(hipMemsetAsync(plan.lo, 0xff, sizeof(uint32_t) * nwin, st));
+            hipLaunchKernelGGL(k_seg_plan, dim3(grid_for(G_act, kT)), dim3(kT), 0, st, tab.ginfo, G_act, plan);
+            SALZ_LAUNCH_CHECK();
+            // run-start bits per window (64 words each) and fix flags, in pst (free until the large
+            // groups' extraction)
+            uint64_t *rb = ws.pst;
+            uint32_t *need = reinterpret_cast<uint32_t *>(ws.pst + (size_t)nwin * (kSegCap / 64));
+            SALZ_HIP(hipMemsetAsync(need, 0, sizeof(uint32_t) * nwin, st));
+            hipLaunchKernelGGL(k_seg_small_text, dim3(nwin), dim3(kSegThreads), 0, st, K, V, gin, plan, tab.ginfo,
+                               m, tbits, seg_tiny, rb, need, derr);
+            SALZ_LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_seg_text_fix, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, rb, need);
+            SALZ_LAUNCH_CHECK();
+            if (mL) {
+                uint32_t *tmap = pw + 4 * nwin;
+                const uint32_t ntile = grid_for(mL, kT);
+                // the extracted suffixes beside the group table in cand (16 B per slot: VC 4,
+                // ginfo 8, PC 4)
+                uint32_t *PC = reinterpret_cast<uint32_t *>(cb + 12 * ws.cap_s);
+                hipLaunchKernelGGL(k_tile_lg, dim3(grid_for(ntile, kT)), dim3(kT), 0, st, tab.lrec, GL, mL, tmap);
+                SALZ_LAUNCH_CHECK();
+                hipLaunchKernelGGL(k_extract_text, dim3(ntile), dim3(kT), 0, st, K, V, tab.lrec, tmap, GL, m, mL, KC,
+                                   VC, PC, derr);
+                SALZ_LAUNCH_CHECK();
+                uint64_t *KS = KC;
+                uint32_t *VS = VC;
+                if (radix_sort_pairs(&KS, &VS, Kx, Vx, mL, 0, tbits, ws, st, nullptr, nullptr, nullptr, rdig) != 0 ||
+                    radix_sort_by_group(&KS, &VS, KS == KC ? Kx : KC, VS == VC ? Vx : VC, mL, tab.lrec, tmap, GL, ws,
+                                        st) != 0)
+                    return -1;
+                hipLaunchKernelGGL(k_putback_text, dim3(ntile), dim3(kT), 0, st, KS, VS, PC, tab.lrec, tmap, GL, m,
+                                   mL, K, V, derr);
+                SALZ_LAUNCH_CHECK();
+            }
+        } else if (round0) {
             if (!text_first && bl.nb > 1) {
                 set_error("suffix sort: a batch of blocks needs the text-built first pass");
                 return -1;
@@ -1193,8 +1450,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             const double c_seg = (double)(m - mL) * 24.0 + m * 8.0 +
                                  (double)mL * (((bits_large + 7) / 8) * 32.0 + 48.0);
             bool seg = c_seg < c_all;
-            if (mode_env)
-                seg = strcmp(mode_env, "segmented") == 0;
+            if (mode_global || mode_seg)
+                seg = mode_seg;
             if (!seg) {
                 if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, bits_all, ws, st, nullptr, nullptr, nullptr, rdig) != 0)
                     return -1;
@@ -1241,7 +1498,10 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         }
         if (ws.lcps_ok && !round0 && h / 2 > kLcpMaxHk)
             ws.lcps_ok = false;  // long repeats: the PLCP stage is cheaper than these compares
-        if (ws.lcps_ok)
+        if (textr)
+            hipLaunchKernelGGL(k_heads_text, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, gin, hb, offo, m, alpha,
+                               h / 2, ws.lcps_ok ? ws.lcps : nullptr);
+        else if (ws.lcps_ok)
             hipLaunchKernelGGL(k_heads_lcp, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, offo, m, bl,
                                alpha, kb_old, round0 ? 0u : h / 2, round0, ws.text, ws.lcps, derr);
         else
@@ -1253,19 +1513,6 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         hipLaunchKernelGGL(k_headpos, dim3(grid_for(((size_t)m + 64 * kHpWords - 1) / (64 * kHpWords) * 64, kT)),
                            dim3(kT), 0, st, hb, m, headpos);
         SALZ_LAUNCH_CHECK();
-        // Groups of two decided by a direct compare (k_pairs): pf / pr in scratch that is free
-        // between this round's sort and the next one's (lsc; Kx past k_commit's `later`).
-        uint64_t *pf = nullptr;
-        uint32_t *pr = nullptr;
-        if (pairs_on && h >= pairs_h) {
-            pf = reinterpret_cast<uint64_t *>(ws.lsc);
-            pr = reinterpret_cast<uint32_t *>(Kx) + m;
-            if (verbose)  // (the count is a same-address atomic per wave: diagnostics only)
-                SALZ_HIP(hipMemsetAsync(d32 + 24, 0, sizeof(uint32_t), st));
-            hipLaunchKernelGGL(k_pairs, dim3(grid_for(m, kT)), dim3(kT), 0, st, V, hb, m, bl, h, ws.text, pf, pr,
-                               verbose ? d32 + 24 : nullptr);
-            SALZ_LAUNCH_CHECK();
-        }
         // The host needs G only for the debug checks; no round waits for it.
         const bool need_G = dbg_rounds || verbose;
         uint32_t G = 0;
@@ -1285,13 +1532,13 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         uint64_t *P = reinterpret_cast<uint64_t *>(ws.u1);
         {
             const size_t nw = ((size_t)m + 63) / 64;
-            hipLaunchKernelGGL(k_surv, dim3(grid_for(nw, kT)), dim3(kT), 0, st, hb, pf, m, P);
+            hipLaunchKernelGGL(k_surv, dim3(grid_for(nw, kT)), dim3(kT), 0, st, hb, m, P);
             SALZ_LAUNCH_CHECK();
             if (scan_sum_u64(P, P, nw, false, d64, ws, st) != 0)
                 return -1;
             SALZ_HIP(hipMemsetAsync(d64 + 1, 0, sizeof(uint64_t), st));
         }
-        // Rank updates (SALZ_RANK_MODE=direct|split|stage for experiments):
+        // Rank updates:
         //   direct  k_commit writes rank[i] (small rounds);
         //   split   k_commit writes the lower text part, k_rank_upper passes the rest, parts of
         //           at most ~200 MB of rank array each (Infinity-Cache-sized windows);
@@ -1300,21 +1547,20 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         // Default: up to 512 MB of ranks split from 32M updates, above it stage from 4M, 1 MB
         // windows (Fibonacci 256 MiB: SA 554 -> 505 ms; text 100 MB: SA 24.8 ms split, 25.3
         // staged; profiles/r02l_*).
-        static const char *rank_mode = getenv("SALZ_RANK_MODE");
-        static const uint32_t rlog_min = getenv("SALZ_RANK_RLOG") ? (uint32_t)atoi(getenv("SALZ_RANK_RLOG")) : 18;
         int mode = (uint64_t)n * 4 <= (512ull << 20) ? (m >= (32u << 20) ? 1 : 0) : (m >= (4u << 20) ? 2 : 0);
-        if (rank_mode)
-            mode = !strcmp(rank_mode, "direct") ? 0 : !strcmp(rank_mode, "split") ? 1 : 2;
+        // round 0 before the text round writes only the ranks of the suffixes it finishes
+        const bool textnext = round0 && text1;
+        if (textnext && mode == 1)
+            mode = 0;
         const uint32_t parts_all = (uint32_t)(((uint64_t)n * 4 + (200u << 20) - 1) / (200u << 20));
         const uint32_t parts = mode == 1 ? (parts_all > 1 ? parts_all : 2) : 1;
         const uint32_t span = (uint32_t)(((uint64_t)n + parts - 1) / parts);
         uint32_t *later = reinterpret_cast<uint32_t *>(Kx);  // free until k_keys
         const uint32_t ihi = mode == 0 ? 0xffffffffu : mode == 1 ? span : 0u;
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, headpos,
-                           P, reinterpret_cast<unsigned long long *>(d64 + 1), offo, offn, Vx, ngid, ws.rank,
-                           ws.sa, tab, m, n, nsa, kb_old,
-                           round0, derr, ihi, mode ? later : nullptr, dist ? dist->gbase : 0u, pf, pr,
-                           ws.lcps_ok ? ws.lcps : nullptr, h);
+                           P, reinterpret_cast<unsigned long long *>(d64 + 1), offo, offn, Vx, textnext ? gin : ngid,
+                           ws.rank, ws.sa, tab, m, n, nsa, kb_old, round0, derr, ihi, mode ? later : nullptr,
+                           dist ? dist->gbase : 0u, textr ? gin : nullptr, textnext ? 0 : 1);
         SALZ_LAUNCH_CHECK();
         for (uint32_t q = 1; q < parts; q++) {
             hipLaunchKernelGGL(k_rank_upper, dim3(grid_for(m, kT)), dim3(kT), 0, st, V, later, m,
@@ -1322,7 +1568,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             SALZ_LAUNCH_CHECK();
         }
         if (mode == 2) {
-            uint32_t rlog = rlog_min < 9 ? 9 : rlog_min;
+            uint32_t rlog = 18;
             while ((((uint64_t)n - 1) >> rlog) + 1 > kStageRanges)
                 rlog++;
             const uint32_t nranges = (uint32_t)((((uint64_t)n - 1) >> rlog) + 1);
@@ -1359,10 +1605,9 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         }
         if (verbose) {  // the round's wall time (this round synchronised with the host twice)
             const auto now = std::chrono::steady_clock::now();
-            fprintf(stderr, "sa round %d (%s) h=%u m=%u (large %u in %u groups) groups=%u pairs=%u -> "
+            fprintf(stderr, "sa round %d (%s) h=%u m=%u (large %u in %u groups) groups=%u -> "
                     "survivors %u in %u groups  %.3f ms\n", ws.stats.sa_rounds, how, h, m, mL, GL, G,
-                    pairs_on ? reinterpret_cast<uint32_t *>(ws.hscal)[24] : 0u, mnew, Gnew,
-                    std::chrono::duration<double, std::milli>(now - t_round).count());
+                    mnew, Gnew, std::chrono::duration<double, std::milli>(now - t_round).count());
             t_round = now;
         }
         if (dist) {  // a split block ends when every rank's bucket is sorted
@@ -1394,6 +1639,10 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         if (dist) {  // rank[i + h] lives with the rank that owns suffix i + h
             if (dist_keys(ws, *dist, Vx, ngid, mnew, h, kb, Kx) != 0)
                 return -1;
+        } else if (textnext) {  // the text round's keys: the h0 symbols at i + h0
+            hipLaunchKernelGGL(k_keys_text, dim3(grid_for(mnew, kT)), dim3(kT), 0, st, Vx, mnew, bl, alpha, h,
+                               tmapped, Kx);
+            SALZ_LAUNCH_CHECK();
         } else {
             hipLaunchKernelGGL(k_keys, dim3(grid_for(mnew, kT)), dim3(kT), 0, st, Vx, ngid, ws.rank,
                                mnew, n, h, kb, Kx, derr);
@@ -1412,7 +1661,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         offo = offn;
         offn = t;
     }
-    static const bool check = getenv("SALZ_CHECK_SA") != nullptr;
+    static const bool check = env_flag("SALZ_CHECK", "sa");
     if (check && !dist) {
         SALZ_HIP(hipMemsetAsync(ws.u0, 0, sizeof(uint32_t) * n, st));
         hipLaunchKernelGGL(k_sa_check, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.sa, nsa, n, ws.u0, derr);

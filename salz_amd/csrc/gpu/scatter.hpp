@@ -103,8 +103,7 @@ int scatter_staged(Src src, uint32_t m, uint32_t nidx, uint32_t *dst, uint32_t s
 // always direct, =1: always staged).
 inline bool scatter_stage_wanted(size_t dst_bytes)
 {
-    const char *e = getenv("SALZ_SCATTER_STAGE");
-    const int env = e ? atoi(e) : -1;
+    const long env = env_num("SALZ_SA", "stage", -1);  // tests: stage=1 always, stage=0 never
     return env < 0 ? dst_bytes > (256u << 20) : env != 0;
 }
 

@@ -102,6 +102,10 @@ def gather_container(packed, nbytes: int, block_size: int, rank: int = 0, world:
         pass
     if dist is None and world > 1:
         raise RuntimeError("gather_container: world > 1 needs an initialised process group")
+    if dist is not None and dist.get_world_size(group) != world:
+        # (a local container inside a larger job would wait on peers that never join)
+        raise RuntimeError(f"gather_container: world={world} but the process group has "
+                           f"{dist.get_world_size(group)} ranks")
     host = dist is not None and dist.get_backend(group) == "gloo" and packed.is_cuda
     cdev = torch.device("cpu") if host else dev
     if dist is not None:

@@ -142,14 +142,14 @@ def test_parse_chunk_log_boundaries(monkeypatch):
     on (C1/C3: K = 64, C2/C4/C5: K = 512) and the 32 MiB edge."""
     import salz_amd
 
-    monkeypatch.delenv("SALZ_PARSE_KLOG", raising=False)
+    monkeypatch.delenv("SALZ_PARSE", raising=False)
     f = salz_amd.lib.salz_gpu_parse_chunk_log
     MiB = 1 << 20
     want = {9: 6, 1 * MiB - 1: 6, 16 * MiB: 6, 16 * MiB + 1: 6, 24_000_000: 7, 32 * MiB: 7,
             32 * MiB + 8: 8, 40 * MiB: 9, 64 * MiB: 9, 100_000_000: 9, 256 * MiB: 9}
     for N, k in want.items():
         assert f(N) == k, (N, f(N), k)
-    monkeypatch.setenv("SALZ_PARSE_KLOG", "8")
+    monkeypatch.setenv("SALZ_PARSE", "klog=8")
     assert f(16 * MiB) == 8
 
 

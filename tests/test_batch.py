@@ -91,9 +91,9 @@ def test_batch_matches_per_block_oracle(ctx, kind, size, block):
     _check(ctx, _src(kind, size, 3), block)
 
 
-@pytest.mark.parametrize("env", [("SALZ_LCP_SA", "0"), ("SALZ_SA_MODE", "global"),
-                                 ("SALZ_SA_MODE", "segmented"), ("SALZ_PARSE_KLOG", "6"),
-                                 ("SALZ_PARSE_KLOG", "9"), ("SALZ_PARSE_SKIP", "0")])
+@pytest.mark.parametrize("env", [("SALZ_SA", "plcp"), ("SALZ_SA", "global"), ("SALZ_SA", "segmented"),
+                                 ("SALZ_SA", "rank1"), ("SALZ_PARSE", "klog=6"), ("SALZ_PARSE", "klog=9"),
+                                 ("SALZ_PARSE", "noskip")])
 @pytest.mark.parametrize("kind,size,block", [("mixed", 16384 * 25 + 4321, 16384),
                                              ("patch", 8192 * 30 + 100, 8192)])
 def test_batch_equivalent_paths(ctx, monkeypatch, env, kind, size, block):

@@ -92,7 +92,7 @@ def test_c3_silesia_16mib_blocks_four_slots(salz):
 
 
 def test_mixed_40mib_default_chunk_length(salz, monkeypatch):
-    monkeypatch.delenv("SALZ_PARSE_KLOG", raising=False)
+    monkeypatch.delenv("SALZ_PARSE", raising=False)
     N = 40 * MiB + 3
     assert salz.lib.salz_gpu_parse_chunk_log(N) == 9
     src = gen("mixed", N, 8)

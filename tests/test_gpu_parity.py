@@ -162,8 +162,8 @@ def test_device_resident_api(salz):
 
 @pytest.fixture
 def klog(request, monkeypatch):
-    """Force the parse chunk length (2^klog positions per lane) through SALZ_PARSE_KLOG."""
-    monkeypatch.setenv("SALZ_PARSE_KLOG", str(request.param))
+    """Force the parse chunk length (2^klog positions per lane) through SALZ_PARSE=klog=N."""
+    monkeypatch.setenv("SALZ_PARSE", f"klog={request.param}")
     return request.param
 
 
@@ -252,32 +252,20 @@ def test_encode_batch_grows_workspace(salz, cap, block, size):
         assert rc == 0 and got[k] == s, k
 
 
-@pytest.mark.parametrize("keys", ["1", "0", "1d0", "1t0", "1s0", "1s2048", "1p1", "0p1", "1p8"])
+@pytest.mark.parametrize("keys", ["", "noalpha", "tiny=0", "tiny=2048", "rank1", "rank1,tiny=0"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
                                                ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
                                                ("smx", 150000, 3, 20), ("runs", 120000, 0, 0),
-                                               ("zeros", 70000, 0, 0)])
+                                               ("zeros", 70000, 0, 0), ("smx", 300000, 4, 100)])
 def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
     """Both doubling-round sorts (global radix on (group, rank); LDS sort of small groups +
-    extracted large groups), with round-0 keys from the compacted alphabet (SALZ_ALPHA=1, the
-    default for texts of <= 127 distinct bytes: 2 to 32 symbols per key) or raw bytes, give the
-    unique suffix array; the radix histograms from the digit bytes (the default) or from the
-    keys ("1d0", SALZ_RADIX_DIGITS=0); round 0's first pass from the text (the default) or from
-    the materialised list ("1t0", SALZ_TEXT_FIRST=0); LDS windows placed by counting up to the
-    default group size, never ("1s0") or always ("1s2048", SALZ_SEG_TINY); groups of two kept in
-    the doubling (the default) or finished by a direct compare (k_pairs, SALZ_SA_PAIRS=1) from
-    depth 64 ("1p1", "0p1") or from round 0 ("1p8", SALZ_SA_PAIRS_H=8)."""
-    monkeypatch.setenv("SALZ_SA_MODE", mode)
-    monkeypatch.setenv("SALZ_SA_PAIRS", "1" if "p" in keys else "0")
-    monkeypatch.setenv("SALZ_SA_PAIRS_H", "8" if keys.endswith("p8") else "64")
-    monkeypatch.setenv("SALZ_ALPHA", keys[0])
-    monkeypatch.setenv("SALZ_RADIX_DIGITS", "0" if keys == "1d0" else "1")
-    monkeypatch.setenv("SALZ_TEXT_FIRST", "0" if keys == "1t0" else "1")
-    if keys.startswith("1s"):
-        monkeypatch.setenv("SALZ_SEG_TINY", keys[2:])
-    else:
-        monkeypatch.delenv("SALZ_SEG_TINY", raising=False)
+    extracted large groups; SALZ_SA=global / segmented), with round-0 keys from the compacted
+    alphabet (the default for texts of <= 127 distinct bytes: 2 to 32 symbols per key) or raw
+    bytes ("noalpha"), give the unique suffix array; round 1 keyed by the text at i + h0 (the
+    default for such alphabets) or by ranks ("rank1"); LDS windows placed by counting up to the
+    default group size, never ("tiny=0") or always ("tiny=2048")."""
+    monkeypatch.setenv("SALZ_SA", ",".join(x for x in (mode, keys) if x))
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
     o = oracle_stages(src)
@@ -294,10 +282,9 @@ DC3_CASES = STAGE_CASES + [("text", 300001, 4, 0), ("smx", 40000, 7, 200), ("mix
 @pytest.mark.parametrize("keys", ["1", "0"])
 @pytest.mark.parametrize("kind,n,seed,alpha", DC3_CASES)
 def test_dc3_matches_oracle(ctx, monkeypatch, keys, kind, n, seed, alpha):
-    """The DC3 suffix sorter (dc3.hip, forced with SALZ_SA_ALGO=dc3) gives the unique suffix
-    array on every input kind, from the block's byte codes (SALZ_ALPHA=1) or raw bytes + 1."""
-    monkeypatch.setenv("SALZ_SA_ALGO", "dc3")
-    monkeypatch.setenv("SALZ_ALPHA", keys)
+    """The DC3 suffix sorter (dc3.hip, forced with SALZ_SA=dc3) gives the unique suffix array on
+    every input kind, from the block's byte codes (the default) or raw bytes + 1 ("noalpha")."""
+    monkeypatch.setenv("SALZ_SA", "dc3" if keys == "1" else "dc3,noalpha")
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
     assert ctx.stats()["sa_dc3_levels"] > 0
@@ -312,11 +299,9 @@ def test_dc3_matches_oracle(ctx, monkeypatch, keys, kind, n, seed, alpha):
                                                ("zeros", 70_000, 0, 0), ("smx", 200_000, 2, 4)])
 def test_staged_scatters(ctx, monkeypatch, kind, n, seed, alpha):
     """The staged scatters (scatter.hpp: Phi of the PLCP stage, the DC3 levels' rank and name
-    arrays), forced on with SALZ_SCATTER_STAGE=1 (by default only past 256 MB), give the same
+    arrays), forced on with SALZ_SA=stage=1 (by default only past 256 MB), give the same
     suffix array, LCPs and stream."""
-    monkeypatch.setenv("SALZ_SCATTER_STAGE", "1")
-    monkeypatch.setenv("SALZ_SA_ALGO", "dc3")
-    monkeypatch.setenv("SALZ_LCP_SA", "0")
+    monkeypatch.setenv("SALZ_SA", "stage=1,dc3,plcp")
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
     o = oracle_stages(src)
@@ -332,7 +317,7 @@ def test_staged_scatters(ctx, monkeypatch, kind, n, seed, alpha):
 def test_dc3_large_blocks_match_oracle(ctx, monkeypatch, kind, n):
     """DC3 at a few MB (several levels with staged-size arrays, forced on for the random
     4-letter text) against the CPU port's suffix array and stream."""
-    monkeypatch.setenv("SALZ_SA_ALGO", "dc3")
+    monkeypatch.setenv("SALZ_SA", "dc3")
     src = gen("smx", n, 9, 4) if kind == "smx4" else _make(kind, n, 0, 0)
     out, d = ctx.encode_dump(src)
     assert ctx.stats()["sa_dc3_levels"] > 0
@@ -346,7 +331,7 @@ def test_dc3_large_blocks_match_oracle(ctx, monkeypatch, kind, n):
 def test_dc3_edge_sizes(ctx, monkeypatch):
     """DC3 at every suffix count 1..200 (each n mod 3, the dummy sample, one-level and
     recursing strings) and around powers of two."""
-    monkeypatch.setenv("SALZ_SA_ALGO", "dc3")
+    monkeypatch.setenv("SALZ_SA", "dc3")
     rng = np.random.default_rng(13)
     sizes = list(range(9, 209)) + [4096 + 8 + d for d in (-1, 0, 1, 2)] + [65536 + 8 + d for d in (0, 1, 2)]
     for N in sizes:
@@ -365,12 +350,9 @@ def test_dc3_edge_sizes(ctx, monkeypatch):
 @pytest.mark.parametrize("algo", ["", "noprobe", "doubling"])
 def test_dc3_auto_switch(ctx, monkeypatch, algo):
     """A repetitive block of >= 1 MiB goes to DC3 by default: before round 0 when the repetition
-    probe finds its sampled 32-grams repeated, else (SALZ_SA_PROBE=0) at depth 32; text does
-    not; SALZ_SA_ALGO=doubling keeps prefix doubling. All give the reference stream."""
-    monkeypatch.delenv("SALZ_SA_ALGO", raising=False)
-    monkeypatch.setenv("SALZ_SA_PROBE", "0" if algo == "noprobe" else "1")
-    if algo == "doubling":
-        monkeypatch.setenv("SALZ_SA_ALGO", algo)
+    probe finds its sampled 32-grams repeated, else (SALZ_SA=noprobe) at depth 32; text does
+    not; SALZ_SA=doubling keeps prefix doubling. All give the reference stream."""
+    monkeypatch.setenv("SALZ_SA", algo if algo in ("noprobe", "doubling") else "")
     for kind, n in (("fib", 3 << 20), ("period3", 2 << 20), ("text", 2 << 20)):
         src = _make(kind, n, 1, 0)
         out = ctx.encode(src)
@@ -390,8 +372,8 @@ def test_dc3_auto_switch(ctx, monkeypatch, algo):
                                                ("smx", 100000, 5, 256)])
 def test_lcp_paths(ctx, monkeypatch, lcp_sa, kind, n, seed, alpha):
     """Both LCP sources give the reference stream: the LCP left behind by the suffix sort
-    (sa.hip k_heads_lcp, SALZ_LCP_SA=1, the default) and the Phi/PLCP stage (lcp.hip)."""
-    monkeypatch.setenv("SALZ_LCP_SA", lcp_sa)
+    (sa.hip k_heads_lcp, the default) and the Phi/PLCP stage (lcp.hip, SALZ_SA=plcp)."""
+    monkeypatch.setenv("SALZ_SA", "" if lcp_sa == "1" else "plcp")
     src = _make(kind, n, seed, alpha)
     out = ctx.encode(src)
     rc, ref = oracle_encode(src)
@@ -406,21 +388,17 @@ def test_lcp_paths(ctx, monkeypatch, lcp_sa, kind, n, seed, alpha):
                                                     ("runs", 400_000, 0, 0, "6")])
 def test_parse_wave_skip(ctx, monkeypatch, skip, kind, n, seed, alpha, klog):
     """From the third pass on, waves of chunks whose decisions would repeat skip the pass
-    (parse.hip k_parse_mark, SALZ_PARSE_SKIP=1, the default): decisions, the exact suffix
+    (parse.hip k_parse_mark; SALZ_PARSE=noskip turns it off): decisions, the exact suffix
     costs and the stream match the oracle with and without skipping, with the chunk range test
-    (SALZ_PARSE_RANGE=1, the default) and the per-candidate test alone ("1r0"), on the packed
-    candidates (SALZ_PARSE_PACK=1, the default) and the full ones ("1p0"), with the lazy
-    per-chunk cost offsets of the skipping passes (SALZ_PARSE_LAZY=1, the default) and without
-    ("1l0"), and with the per-candidate test as a wave per listed chunk (SALZ_PARSE_SPLIT=1, the
-    default) or inside the test kernel ("1s0"), and with the exit set compacted a thread per node
-    ("1n2"; by default only where it is sparse)."""
-    monkeypatch.setenv("SALZ_PARSE_SKIP", skip[0])
-    monkeypatch.setenv("SALZ_PARSE_LAZY", "0" if skip == "1l0" else "1")
-    monkeypatch.setenv("SALZ_PARSE_SPLIT", "0" if skip == "1s0" else "1")
-    monkeypatch.setenv("SALZ_PARSE_NODES", "2" if skip == "1n2" else "1")
-    monkeypatch.setenv("SALZ_PARSE_RANGE", "0" if skip == "1r0" else "1")
-    monkeypatch.setenv("SALZ_PARSE_PACK", "0" if skip == "1p0" else "1")
-    monkeypatch.setenv("SALZ_PARSE_KLOG", klog)
+    (the default) and the per-candidate test alone ("1r0", norange), on the packed candidates
+    (the default) and the full ones ("1p0", nopack), with the lazy per-chunk cost offsets of the
+    skipping passes (the default) and without ("1l0", nolazy), and with the per-candidate test
+    as a wave per listed chunk (the default) or inside the test kernel ("1s0", nosplit), and with
+    the exit set compacted a thread per node ("1n2", nodes=2; by default only where it is
+    sparse)."""
+    flags = {"0": "noskip", "1l0": "nolazy", "1s0": "nosplit", "1n2": "nodes=2", "1r0": "norange",
+             "1p0": "nopack"}.get(skip)
+    monkeypatch.setenv("SALZ_PARSE", f"klog={klog}" + (f",{flags}" if flags else ""))
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
     o = oracle_stages(src)
