@@ -641,22 +641,37 @@ __device__ __forceinline__ void seg_lsd(uint64_t *sk, uint32_t (*cnt)[256], uint
     }
 }
 
-// Small groups of one 2048-entry window of the active list, sorted in LDS by rank[i + h].
-// The window owns every small group that starts in it (a group of <= kSmall members ends
-// before the window's end + kSmall, and no large group can sit between two of them), so
-// the owned range [lo, hi) has < kSegCap entries. Sort key: local group << (kb + 12) |
-// rank << 12 | slot; a stable 8-bit LSD pass per digit of the (group, rank) part.
-__global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict__ K,
-                                                           uint32_t *__restrict__ V, SegPlan plan,
-                                                           const uint64_t *__restrict__ ginfo, uint32_t m,
-                                                           int kb, uint32_t tiny, uint32_t *err)
-{
-    __shared__ uint64_t sk[kSegCap];  // keys
-    __shared__ uint32_t sv[kSegCap];  // the window's values, loaded with the keys
-    __shared__ uint32_t cnt[4][256];
-    __shared__ uint32_t wsum[4];
+// Groups of one window of the active list, sorted in LDS. The window owns every small group that
+// starts in it (a group of <= kSmall members ends before the window's end + kSmall, and no large
+// group can sit between two of them), so the owned range [lo, hi) has < kSegCap entries.
+//   - A group of at most `tiny` members is ordered by counting: each entry's place is its group's
+//     start plus the members with a smaller (key, window index).
+//   - The members of the larger groups are gathered at the front of the LDS array and sorted by
+//     (local group, key bits, window index) with stable 8-bit LSD passes; an entry's place is then
+//     its group's start plus its sorted position minus the group's first sorted position (a
+//     binary search: the groups stay contiguous in the sorted array).
+// Rank rounds (TEXT = 0): key = group << kb | rank; the LSD passes take the kb rank bits. The
+// text round (TEXT = 1, keys = kb text bits, groups in gin): the LSD passes take the top bits of
+// the key that keep the sort at 40 bits (5 passes); the runs of equal (group, top bits) they leave
+// are marked (rb, need) and ordered by the whole key in k_seg_text_fix.
+constexpr uint32_t kPer = kSegCap / kSegThreads;
 
-    const unsigned tid = threadIdx.x;
+template <bool TEXT>
+__global__ __launch_bounds__(kSegThreads) void k_seg_sort(uint64_t *__restrict__ K, uint32_t *__restrict__ V,
+                                                          const uint32_t *__restrict__ gin, SegPlan plan,
+                                                          const uint64_t *__restrict__ ginfo, uint32_t m, int kb,
+                                                          uint32_t tiny, uint64_t *__restrict__ rb,
+                                                          uint32_t *__restrict__ need, uint32_t *err)
+{
+    __shared__ uint64_t sk[kSegCap];  // the window's keys, then the larger groups' LSD keys
+    __shared__ uint32_t sv[kSegCap];  // the window's values (by window index)
+    __shared__ uint32_t cnt[4][256];  // LSD counters; after the LSD, runb
+    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t nbig;
+    uint64_t *runb = reinterpret_cast<uint64_t *>(&cnt[0][0]);  // TEXT: run starts by window index
+    static_assert(sizeof(cnt) >= kSegCap / 8, "LDS alias");
+
+    const unsigned tid = threadIdx.x, lane = tid & 63u;
     const uint32_t w = blockIdx.x;
     const uint32_t lo = plan.lo[w];
     if (lo == 0xffffffffu)
@@ -665,67 +680,70 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
     if (bad_index(hi > m || hi <= lo || hi - lo >= kSegCap || g1 < g0, err, kErrSeg))
         return;
     const uint32_t count = hi - lo;
-    const uint64_t mask = (1ull << kb) - 1ull;
-    const int nbits = kb + (32 - __builtin_clz((g1 - g0) | 1u));
-
-    // slots actually sorted: count rounded up to 256 (4 waves x 64 lanes x ITEMS), at least 1024
-    // (a window's owned span is about 2048 entries, so windows a little over it sort 2304 or 2560
-    // slots, not 3072)
-    const int items = count <= 1024u ? 4 : (int)((count + 255u) / 256u);
-    for (uint32_t i = tid; i < (uint32_t)items * kSegThreads; i += kSegThreads) {
-        uint64_t key = ~0ull;  // padding sorts last in every digit
-        if (i < count) {
-            const uint64_t kk = K[lo + i];
-            sv[i] = V[lo + i];
-            key = (((kk >> kb) - g0) << (kb + 12)) | ((kk & mask) << 12) | i;
-        }
-        sk[i] = key;
-    }
-    // the largest owned group (its sizes are contiguous in ginfo), for the counting order
-    uint32_t gmax = 0;
-    if (tiny) {
-        for (uint32_t g = g0 + tid; g <= g1; g += kSegThreads) {
-            const uint32_t s = (uint32_t)(ginfo[g] >> 32);
-            gmax = s > gmax ? s : gmax;
-        }
-        gmax = wave_max_u32(gmax);
-        if (lane_id() == 0)
-            wsum[tid >> 6] = gmax;
+    const uint64_t mask = kb >= 64 ? ~0ull : (1ull << kb) - 1ull;
+    const int gbits = 32 - __builtin_clz((g1 - g0) | 1u);
+    const int kr = TEXT ? (kb < 40 - gbits ? kb : 40 - gbits) : kb;  // key bits in the LSD key
+    if (tid == 0)
+        nbig = 0;
+    for (uint32_t i = tid; i < count; i += kSegThreads) {
+        sk[i] = K[lo + i];
+        sv[i] = V[lo + i];
     }
     __syncthreads();
-    const uint32_t m01 = wsum[0] > wsum[1] ? wsum[0] : wsum[1], m23 = wsum[2] > wsum[3] ? wsum[2] : wsum[3];
-    if (tiny && (m01 > m23 ? m01 : m23) <= tiny) {
-        // Windows of tiny groups only: each entry's place is its group's start plus the members
-        // with smaller (rank, slot), counted in LDS (at most `tiny` reads per entry instead of
-        // nbits / 8 LSD passes). Same order as the stable LSD passes.
-        // (every key and value of the window is staged: the stores below may overwrite them)
-        constexpr uint32_t kPer = kSegCap / kSegThreads;
-        uint32_t dst[kPer];
-        uint64_t nk[kPer];
+    // counted groups: placed now; the larger groups' members: their LSD keys, collected
+    uint64_t lk[kPer];
+    bool big[kPer];
 #pragma unroll
-        for (uint32_t j = 0; j < kPer; j++) {
-            const uint32_t i = tid + j * kSegThreads, ii = i < count ? i : 0u;
-            const uint64_t ki = sk[ii];
-            const uint64_t g = g0 + (ki >> (kb + 12));
-            const uint64_t gi = ginfo[g];  // unconditional loads (clamped entry)
-            const uint32_t gs = (uint32_t)gi - lo, s = (uint32_t)(gi >> 32);
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t i = tid + j * kSegThreads, ii = i < count ? i : 0u;
+        const uint64_t ki = sk[ii];
+        const uint32_t lg = (TEXT ? gin[lo + ii] : (uint32_t)(ki >> kb)) - g0;  // (unconditional loads)
+        const uint64_t gi = ginfo[g0 + lg];
+        uint32_t gs = (uint32_t)gi - lo, sz = (uint32_t)(gi >> 32);
+        big[j] = false;
+        if (i >= count)
+            continue;
+        if (bad_index(gs > i || gs + sz > count || sz > kSmall, err, kErrSeg)) {
+            gs = i;  // (the error ends the sort)
+            sz = 0;
+        }
+        if (sz <= tiny) {
             uint32_t r = 0;
-            for (uint32_t x = gs; x < gs + s; x++)
-                r += sk[x] < ki ? 1u : 0u;
-            dst[j] = lo + gs + r;
-            nk[j] = (g << kb) | ((ki >> 12) & mask);
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kPer; j++) {
-            const uint32_t i = tid + j * kSegThreads;
-            if (i < count) {
-                K[dst[j]] = nk[j];
-                V[dst[j]] = sv[i];
+            for (uint32_t x = gs; x < gs + sz; x++) {
+                const uint64_t kx = sk[x];
+                r += (kx < ki || (kx == ki && x < i)) ? 1u : 0u;
             }
+            K[lo + gs + r] = ki;
+            V[lo + gs + r] = sv[i];
+        } else {
+            big[j] = true;
+            const uint64_t kbits = TEXT ? ki >> (kb - kr) : ki & mask;
+            lk[j] = ((uint64_t)lg << (kr + 12)) | (kbits << 12) | i;
         }
-        return;
     }
+    __syncthreads();  // (the window's keys are no longer read from sk)
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint64_t bm = wave_ballot(big[j]);
+        uint32_t base = 0;
+        if (lane == 0 && bm)
+            base = atomicAdd(&nbig, (uint32_t)__popcll(bm));
+        base = shfl_u32(base, 0);
+        if (big[j])
+            sk[base + count_below(bm)] = lk[j];
+    }
+    __syncthreads();
+    const uint32_t nb = nbig;
+    if (nb == 0)
+        return;
+    const int items = (int)((nb + 255u) / 256u);
+    for (uint32_t i = nb + tid; i < (uint32_t)items * kSegThreads; i += kSegThreads)
+        sk[i] = ~0ull;  // padding sorts last in every digit
+    const int nbits = gbits + kr;
     switch (items) {
+    case 1: seg_lsd<1>(sk, cnt, wsum, nbits); break;
+    case 2: seg_lsd<2>(sk, cnt, wsum, nbits); break;
+    case 3: seg_lsd<3>(sk, cnt, wsum, nbits); break;
     case 4: seg_lsd<4>(sk, cnt, wsum, nbits); break;
     case 5: seg_lsd<5>(sk, cnt, wsum, nbits); break;
     case 6: seg_lsd<6>(sk, cnt, wsum, nbits); break;
@@ -740,18 +758,62 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_small(uint64_t *__restrict_
     case 15: seg_lsd<15>(sk, cnt, wsum, nbits); break;
     default: seg_lsd<16>(sk, cnt, wsum, nbits); break;
     }
-
-    // The values were staged with the keys (a separate 16 KB stage: their HBM load overlaps the
-    // keys' instead of following the sort, and no sorted keys wait in registers).
-    for (uint32_t i = tid; i < count; i += kSegThreads) {
-        const uint64_t key = sk[i];
-        const uint64_t g = g0 + (key >> (kb + 12));
-        K[lo + i] = (g << kb) | ((key >> 12) & mask);
-        V[lo + i] = sv[key & 0xfffu];
+    if (TEXT) {  // (cnt is free again)
+        for (uint32_t q = tid; q < kSegCap / 64; q += kSegThreads)
+            runb[q] = ~0ull;
+        __syncthreads();
+    }
+    uint64_t outk[kPer];
+    uint32_t dst[kPer], vv[kPer];
+    bool tie = false;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t t = tid + j * kSegThreads;
+        if (t >= nb)
+            continue;
+        const uint64_t key = sk[t];
+        const uint32_t lg = (uint32_t)(key >> (kr + 12)), i = (uint32_t)key & 0xfffu;
+        // the group's first sorted position: the first t' with local group lg
+        uint32_t a = 0, z = t;
+        while (a < z) {
+            const uint32_t mid = (a + z) >> 1;
+            if ((uint32_t)(sk[mid] >> (kr + 12)) < lg)
+                a = mid + 1;
+            else
+                z = mid;
+        }
+        dst[j] = (uint32_t)ginfo[g0 + lg] - lo + (t - a);
+        if (TEXT) {
+            outk[j] = K[lo + i];  // the whole key (this range of K is written only below)
+            if (t > a && (sk[t - 1] >> 12) == (key >> 12)) {  // not a run start
+                tie = true;
+                atomicAnd(reinterpret_cast<unsigned long long *>(&runb[dst[j] >> 6]), ~(1ull << (dst[j] & 63u)));
+            }
+        } else {
+            outk[j] = ((uint64_t)(g0 + lg) << kb) | ((key >> 12) & mask);
+        }
+        vv[j] = sv[i];
+    }
+    __syncthreads();  // (every whole key read from K before any entry is written)
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t t = tid + j * kSegThreads;
+        if (t < nb) {
+            K[lo + dst[j]] = outk[j];
+            V[lo + dst[j]] = vv[j];
+        }
+    }
+    if (TEXT) {
+        if (__syncthreads_or(tie)) {
+            for (uint32_t q = tid; q < kSegCap / 64; q += kSegThreads)
+                rb[(size_t)w * (kSegCap / 64) + q] = runb[q];
+            if (tid == 0)
+                need[w] = 1u;
+        }
     }
 }
 
-// SALZ_CHECK_SA=1: every position must appear exactly once in the suffix array.
+// SALZ_CHECK=sa: every position must appear exactly once in the suffix array.
 __global__ void k_sa_check(const uint32_t *__restrict__ sa, uint32_t nsa, uint32_t n, uint32_t *seen,
                            uint32_t *err)
 {
@@ -943,142 +1005,7 @@ __global__ __launch_bounds__(kT) void k_heads_text(const uint64_t *__restrict__ 
         lcps[(uint32_t)cc + off_old[g1]] = h0 + round0_lcp(k0 ^ k1, a);
 }
 
-// The small groups of one window sorted by (group, key) in LDS. The LSD passes sort (local group,
-// top key bits, slot), with as many top bits as keep the sort at 40 bits (5 passes); the runs of
-// equal (group, top bits) that remain are marked (rb, need) and ordered by the whole key in
-// k_seg_text_fix. Windows of tiny groups count on the whole key here.
-__global__ __launch_bounds__(kSegThreads) void k_seg_small_text(uint64_t *__restrict__ K, uint32_t *__restrict__ V,
-                                                                const uint32_t *__restrict__ gin, SegPlan plan,
-                                                                const uint64_t *__restrict__ ginfo, uint32_t m,
-                                                                int tbits, uint32_t tiny,
-                                                                uint64_t *__restrict__ rb, uint32_t *__restrict__ need,
-                                                                uint32_t *err)
-{
-    __shared__ uint64_t sk[kSegCap];
-    __shared__ uint32_t sv[kSegCap];
-    __shared__ uint32_t cnt[4][256];
-    __shared__ uint32_t wsum[4];
-
-    const unsigned tid = threadIdx.x;
-    const uint32_t w = blockIdx.x;
-    const uint32_t lo = plan.lo[w];
-    if (lo == 0xffffffffu)
-        return;
-    const uint32_t hi = plan.hi[w], g0 = plan.g0[w], g1 = plan.g1[w];
-    if (bad_index(hi > m || hi <= lo || hi - lo >= kSegCap || g1 < g0, err, kErrSeg))
-        return;
-    const uint32_t count = hi - lo;
-    const int gbits = 32 - __builtin_clz((g1 - g0) | 1u);
-    // top key bits in the LSD key: a 40-bit sort (5 passes; 48 and 52 bits measured slower, the
-    // extra passes costing more than the shorter runs save in k_seg_text_fix)
-    const int kbt = tbits < 40 - gbits ? tbits : 40 - gbits;
-    const int items = count <= 1024u ? 4 : (int)((count + 255u) / 256u);
-    constexpr uint32_t kPer = kSegCap / kSegThreads;
-
-    uint32_t gmax = 0;
-    if (tiny) {
-        for (uint32_t g = g0 + tid; g <= g1; g += kSegThreads) {
-            const uint32_t sz = (uint32_t)(ginfo[g] >> 32);
-            gmax = sz > gmax ? sz : gmax;
-        }
-        gmax = wave_max_u32(gmax);
-        if (lane_id() == 0)
-            wsum[tid >> 6] = gmax;
-    }
-    __syncthreads();
-    const uint32_t m01 = wsum[0] > wsum[1] ? wsum[0] : wsum[1], m23 = wsum[2] > wsum[3] ? wsum[2] : wsum[3];
-    if (tiny && (m01 > m23 ? m01 : m23) <= tiny) {
-        // tiny groups: each entry's place is its group's start + the members with a smaller
-        // (key, slot)
-        for (uint32_t i = tid; i < count; i += kSegThreads) {
-            sk[i] = K[lo + i];
-            sv[i] = V[lo + i];
-        }
-        __syncthreads();
-        uint32_t dst[kPer];
-#pragma unroll
-        for (uint32_t j = 0; j < kPer; j++) {
-            const uint32_t i = tid + j * kSegThreads, ii = i < count ? i : 0u;
-            const uint64_t ki = sk[ii];
-            const uint64_t gi = ginfo[gin[lo + ii]];  // (unconditional loads: clamped entry)
-            const uint32_t gs = (uint32_t)gi - lo, sz = (uint32_t)(gi >> 32);
-            uint32_t r = 0;
-            for (uint32_t x = gs; x < gs + sz; x++) {
-                const uint64_t kx = sk[x];
-                r += (kx < ki || (kx == ki && x < ii)) ? 1u : 0u;
-            }
-            dst[j] = lo + gs + r;
-        }
-        __syncthreads();  // (every dst computed before any store: they may land in this window)
-#pragma unroll
-        for (uint32_t j = 0; j < kPer; j++) {
-            const uint32_t i = tid + j * kSegThreads;
-            if (i < count) {
-                K[dst[j]] = sk[i];
-                V[dst[j]] = sv[i];
-            }
-        }
-        return;
-    }
-    for (uint32_t i = tid; i < (uint32_t)items * kSegThreads; i += kSegThreads) {
-        uint64_t key = ~0ull;  // padding sorts last in every digit
-        if (i < count) {
-            const uint64_t kk = K[lo + i];
-            sv[i] = V[lo + i];
-            key = ((uint64_t)(gin[lo + i] - g0) << (kbt + 12)) | ((kk >> (tbits - kbt)) << 12) | i;
-        }
-        sk[i] = key;
-    }
-    const int nbits = gbits + kbt;
-    switch (items) {
-    case 4: seg_lsd<4>(sk, cnt, wsum, nbits); break;
-    case 5: seg_lsd<5>(sk, cnt, wsum, nbits); break;
-    case 6: seg_lsd<6>(sk, cnt, wsum, nbits); break;
-    case 7: seg_lsd<7>(sk, cnt, wsum, nbits); break;
-    case 8: seg_lsd<8>(sk, cnt, wsum, nbits); break;
-    case 9: seg_lsd<9>(sk, cnt, wsum, nbits); break;
-    case 10: seg_lsd<10>(sk, cnt, wsum, nbits); break;
-    case 11: seg_lsd<11>(sk, cnt, wsum, nbits); break;
-    case 12: seg_lsd<12>(sk, cnt, wsum, nbits); break;
-    case 13: seg_lsd<13>(sk, cnt, wsum, nbits); break;
-    case 14: seg_lsd<14>(sk, cnt, wsum, nbits); break;
-    case 15: seg_lsd<15>(sk, cnt, wsum, nbits); break;
-    default: seg_lsd<16>(sk, cnt, wsum, nbits); break;
-    }
-    // Runs of equal (group, top bits): their starts as bits (to rb, for k_seg_text_fix); every
-    // entry written back in this order with its whole key (re-read from K: this window's range
-    // is written only at the end) and its value.
-    uint64_t full[kPer];
-    uint32_t vv[kPer];
-    bool tie = false;
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) {
-        const uint32_t i = tid + j * kSegThreads, ii = i < count ? i : 0u;
-        const uint64_t key = sk[ii], prev = sk[ii ? ii - 1 : 0];
-        const uint32_t slot = (uint32_t)key & 0xfffu;
-        if (j < (uint32_t)items) {
-            full[j] = K[lo + slot];
-            vv[j] = sv[slot];
-        }
-        const bool start = ii == 0 || (key >> 12) != (prev >> 12);
-        tie = tie || (i < count && !start);
-        const uint64_t bits = wave_ballot(i < count && start);
-        if (lane_id() == 0 && j < (uint32_t)items)
-            rb[(size_t)w * (kSegCap / 64) + ((j * kSegThreads + (tid & ~63u)) >> 6)] = bits;
-    }
-    if (__syncthreads_or(tie) && tid == 0)
-        need[w] = 1u;
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) {
-        const uint32_t i = tid + j * kSegThreads;
-        if (j < (uint32_t)items && i < count) {
-            K[lo + i] = full[j];
-            V[lo + i] = vv[j];
-        }
-    }
-}
-
-// The runs of equal (group, top key bits) that k_seg_small_text left (windows flagged in need),
+// The runs of equal (group, top key bits) that k_seg_sort<1> left (windows flagged in need),
 // each ordered by the whole key: runs of up to kRunCount entries by counting (each entry's place
 // is the run start + the entries with a smaller (key, index): at depth 13-14 of text a run holds
 // 14-20 entries on average), longer ones (a window may hold one of 2000) by a bitonic sort of the
@@ -1098,7 +1025,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_text_fix(uint64_t *__restri
     const uint32_t w = blockIdx.x;
     if (!need[w])
         return;
-    const uint32_t lo = plan.lo[w], count = plan.hi[w] - lo;  // (checked by k_seg_small_text)
+    const uint32_t lo = plan.lo[w], count = plan.hi[w] - lo;  // (checked by k_seg_sort)
     const uint32_t nwords = (count + 63u) >> 6;
     if (tid == 0)
         nlong = 0;
@@ -1366,10 +1293,11 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     const int kb = bit_width(n);
     static const bool verbose = env_flag("SALZ_DEBUG", "sa");
     const bool mode_global = env_flag("SALZ_SA", "global"), mode_seg = env_flag("SALZ_SA", "segmented");
-    // k_seg_small windows whose groups all have at most seg_tiny members are ordered by counting
-    // (SALZ_SA=tiny=0: LSD passes everywhere)
-    // (64: 32, 96 and 128 measured within 0.2 ms of it, 32 up to 0.2 ms slower on mixed data)
-    const uint32_t seg_tiny = (uint32_t)env_num("SALZ_SA", "tiny", 64);
+    // groups of at most seg_tiny members are ordered by counting in k_seg_sort (SALZ_SA=tiny=0:
+    // LSD passes everywhere). C2 SA 21.9 / 21.0 / 20.9 / 20.8 / 20.6 / 20.5 / 20.4 / 22.7 ms at
+    // 0 / 8 / 16 / 32 / 64 / 128 / 256 / 2048; mixed 100 MB 27.2 (0) -> 25.7 ms (64-256)
+    // (profiles/r04n_tiny_sweep.txt)
+    const uint32_t seg_tiny = (uint32_t)env_num("SALZ_SA", "tiny", 128);
     // Round 1 keyed by text (see k_keys_text): one block or a batch, the block's own sort (not a
     // split block's bucket), an alphabet of at most 127 bytes (symbols >= 1, so zero padding
     // is unambiguous). SALZ_SA=rank1 keeps round 1 on ranks.
@@ -1403,7 +1331,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             uint64_t *rb = ws.pst;
             uint32_t *need = reinterpret_cast<uint32_t *>(ws.pst + (size_t)nwin * (kSegCap / 64));
             SALZ_HIP(hipMemsetAsync(need, 0, sizeof(uint32_t) * nwin, st));
-            hipLaunchKernelGGL(k_seg_small_text, dim3(nwin), dim3(kSegThreads), 0, st, K, V, gin, plan, tab.ginfo,
+            hipLaunchKernelGGL(k_seg_sort<true>, dim3(nwin), dim3(kSegThreads), 0, st, K, V, gin, plan, tab.ginfo,
                                m, tbits, seg_tiny, rb, need, derr);
             SALZ_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_seg_text_fix, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, rb, need);
@@ -1465,8 +1393,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                 hipLaunchKernelGGL(k_seg_plan, dim3(grid_for(G_act, kT)), dim3(kT), 0, st, tab.ginfo,
                                    G_act, plan);
                 SALZ_LAUNCH_CHECK();
-                hipLaunchKernelGGL(k_seg_small, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, tab.ginfo, m,
-                                   kb, seg_tiny, derr);
+                hipLaunchKernelGGL(k_seg_sort<false>, dim3(nwin), dim3(kSegThreads), 0, st, K, V, nullptr, plan,
+                                   tab.ginfo, m, kb, seg_tiny, nullptr, nullptr, derr);
                 SALZ_LAUNCH_CHECK();
                 if (mL) {
                     uint32_t *tmap = pw + 4 * nwin;  // (lsc, after the window plan)

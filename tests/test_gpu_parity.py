@@ -252,7 +252,7 @@ def test_encode_batch_grows_workspace(salz, cap, block, size):
         assert rc == 0 and got[k] == s, k
 
 
-@pytest.mark.parametrize("keys", ["", "noalpha", "tiny=0", "tiny=2048", "rank1", "rank1,tiny=0"])
+@pytest.mark.parametrize("keys", ["", "noalpha", "tiny=2048", "rank1", "rank1,tiny=2048", "noalpha,tiny=2048"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
                                                ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
@@ -263,8 +263,9 @@ def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
     extracted large groups; SALZ_SA=global / segmented), with round-0 keys from the compacted
     alphabet (the default for texts of <= 127 distinct bytes: 2 to 32 symbols per key) or raw
     bytes ("noalpha"), give the unique suffix array; round 1 keyed by the text at i + h0 (the
-    default for such alphabets) or by ranks ("rank1"); LDS windows placed by counting up to the
-    default group size, never ("tiny=0") or always ("tiny=2048")."""
+    default for such alphabets) or by ranks ("rank1"); groups of up to 64 members placed by
+    counting and larger ones by LSD passes in LDS (the default), or every group by counting
+    ("tiny=2048")."""
     monkeypatch.setenv("SALZ_SA", ",".join(x for x in (mode, keys) if x))
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
