@@ -289,6 +289,15 @@ class Context:
             raise SalzError(f"encode failed: {last_error()}")
         return out[: n.value].tobytes()
 
+    def encode_into(self, src, out: np.ndarray) -> int:
+        """salz_gpu_encode_host into a caller-owned buffer (reused across calls, as the reference
+        CLI reuses its block buffers, programs/salzcli.c); returns the stream length."""
+        s = _buf(src)
+        n = ctypes.c_size_t(len(out))
+        if lib.salz_gpu_encode_host(self.handle, _ptr(s), len(s), _ptr(out), ctypes.byref(n)) != 0:
+            raise SalzError(f"encode failed: {last_error()}")
+        return n.value
+
     def encode_batch(self, src, block_size: int) -> list[bytes]:
         """salz_gpu_encode_batch: every block of src in one pipeline pass; the streams."""
         s = _buf(src)

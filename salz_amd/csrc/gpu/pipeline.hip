@@ -173,11 +173,18 @@ static int stage_ready(Workspace &ws)
     return 0;
 }
 
+constexpr size_t kRuntimeCopy = 16u << 20;
+
 int copy_h2d(Workspace &ws, uint8_t *dst, const uint8_t *src, size_t bytes)
 {
     if (bytes == 0)
         return 0;
-    if (bytes <= (64u << 10) || dma_ready(src)) {
+    // Pageable copies of 16 MiB and more go through the runtime (ROCm 7.2: C2 from host buffers
+    // 2950 -> 3190 MB/s, Silesia-sized blocks 2578 -> 2691, four salz_encode_safe threads on
+    // 16 MiB blocks 3394 -> 3509; profiles/r04q_h2d_ab.txt); smaller ones (the batches of the
+    // container encoders, several in flight) through the context's pinned chunks, which the
+    // 512 KiB-block level sweep ran faster (1760 vs 1313 MB/s).
+    if (bytes <= (64u << 10) || bytes >= kRuntimeCopy || dma_ready(src)) {
         SALZ_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ws.stream));
         return 0;
     }
@@ -200,7 +207,7 @@ int copy_d2h(Workspace &ws, uint8_t *dst, const uint8_t *src, size_t bytes)
 {
     if (bytes == 0)
         return 0;
-    if (bytes <= (64u << 10) || dma_ready(dst)) {
+    if (bytes <= (64u << 10) || bytes >= kRuntimeCopy || dma_ready(dst)) {
         SALZ_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ws.stream));
         SALZ_HIP(hipStreamSynchronize(ws.stream));
         return 0;

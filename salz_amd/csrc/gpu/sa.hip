@@ -1243,9 +1243,10 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     const uint32_t h0 = alpha.bits ? alpha.k : 8u;
     // The text mapped to symbols for the text-sourced radix pass and the text round's keys (u3
     // is free until round 0's commit writes the group ids, which go to `gin` before a text
-    // round): one byte per position, zero padded.
+    // round): one byte per position, zero padded. (A split block's bucket list lives in u3 and
+    // its round 0 reads the raw text: no mapped copy there.)
     uint8_t *tmapped = nullptr;
-    if (alpha.bits) {
+    if (alpha.bits && !dist) {
         tmapped = reinterpret_cast<uint8_t *>(ws.u3);
         const size_t P = (size_t)n + 8;
         hipLaunchKernelGGL(k_map_text, dim3(grid_for(P + 64, kT * 16)), dim3(kT), 0, st, ws.text, P, alpha,
