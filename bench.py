@@ -423,8 +423,25 @@ def main():
         return ctxs[k].encode_device(d_src[j].data_ptr(), e - s, d_dst[j].data_ptr(), caps[j],
                                      streams_t[k].cuda_stream)
 
-    def run_slot(k):  # slot k encodes units k, k + nslots, ... (ctypes drops the GIL)
-        return [(j, enc(k, j)) for j in range(k, len(units), nslots)]
+    # Units are handed out largest first to whichever slot is free (the last block of a sharded
+    # input is the short one: it no longer runs alone at the end of the step).
+    order = sorted(range(len(units)), key=lambda j: units[j][0] - units[j][1])
+    import threading
+
+    take_lock = threading.Lock()
+    take_next = [0]
+
+    def take():
+        with take_lock:
+            i = take_next[0]
+            take_next[0] += 1
+        return order[i] if i < len(order) else None
+
+    def run_slot(k):  # slot k encodes units until none is left (ctypes drops the GIL)
+        done = []
+        while (j := take()) is not None:
+            done.append((j, enc(k, j)))
+        return done
 
     def step():
         """One step: encode this rank's blocks into HBM, their frames packed in block order,
@@ -434,6 +451,7 @@ def main():
             lens = [enc(0, j) for j in range(len(units))]
         else:
             lens = [0] * len(units)
+            take_next[0] = 0
             for part in pool.map(run_slot, range(nslots)):
                 for j, v in part:
                     lens[j] = v
@@ -585,11 +603,15 @@ def main():
             return ctxs[k].encode_into(host_units[j], host_out[j])
 
         def run_slot_host(k):
-            return [enc_host(k, j) for j in range(k, len(units), nslots)]
+            done = []
+            while (j := take()) is not None:
+                done.append(enc_host(k, j))
+            return done
 
         def step_host():
             if pool is None:
                 return [enc_host(0, j) for j in range(len(units))]
+            take_next[0] = 0
             return list(pool.map(run_slot_host, range(nslots)))
 
         step_host()

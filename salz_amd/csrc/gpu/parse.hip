@@ -1088,17 +1088,8 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                                    wdirty, dsum, ndirty);
                 SALZ_LAUNCH_CHECK();
             }
-            if (read_scalars(ws, 0, 256, "parse.mark", 50, 2) != 0)  // (ndirty, listed chunks reset)
-                return -1;
-            const uint32_t nd = reinterpret_cast<uint32_t *>(ws.hscal)[50];
-            prev_listed = reinterpret_cast<uint32_t *>(ws.hscal)[51];
-            if (verbose)
-                fprintf(stderr, "parse it=%d dirty waves %u of %u\n", it, nd, (ps.nchunks + 63) / 64);
-            if (nd == 0) {
-                ps.choice = chold;
-                ps.cost = cin;
-                break;
-            }
+            // (no host read here: a pass with no dirty wave runs its chunk pass as a no-op, every
+            // wave clean, and stops at the read below with nothing changed)
         }
         if (entering) {  // offsets 0 (entries past the last chunk: uniform, delta 0)
             SALZ_HIP(hipMemsetAsync(Lv[0], 0, sizeof(uint32_t) * 4 * nc64, st));  // Lv[0], Lv[1], dl
@@ -1121,15 +1112,30 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                                it == 0 ? cand8 : nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr,
                                eflag, wd, dsum, rch, rlo, lzw);
         SALZ_LAUNCH_CHECK();
-        if (read_scalars(ws, 0, 256, "parse.changed", 48, 1) != 0)  // (changed reset)
+        // The exit set of the new decisions (E was marked by the chunk pass) as bits and word
+        // counts, numbered by the scan, before the pass's one host read: that read then returns
+        // the changed count, |E| (etotal), the dirty waves and the chunks the test listed
+        // together. A pass that changed nothing leaves E as it was, so these are unchanged then.
+        hipLaunchKernelGGL(k_exit_pack, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st,
+                           reinterpret_cast<const uint64_t *>(eflag), S / 8, eb);
+        SALZ_LAUNCH_CHECK();
+        if (scan_sum_u32(eb.wcnt, eb.wpre, S / 64, false, etotal, ws, st) != 0)
+            return -1;
+        if (read_scalars(ws, 0, 256, "parse.pass", 48, 4) != 0)  // (changed, ndirty, listed reset)
             return -1;
         const uint32_t nchanged = reinterpret_cast<uint32_t *>(ws.hscal)[48];
         if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
             set_error("parse: device index check failed (code 0x%x): candidate length past the end", e);
             return -1;
         }
-        if (verbose)
+        if (skipping)
+            prev_listed = reinterpret_cast<uint32_t *>(ws.hscal)[51];
+        if (verbose) {
+            if (skipping)
+                fprintf(stderr, "parse it=%d dirty waves %u of %u\n", it, reinterpret_cast<uint32_t *>(ws.hscal)[50],
+                        (ps.nchunks + 63) / 64);
             fprintf(stderr, "parse it=%d K=%u changed=%u\n", it, ps.chunk, nchanged);
+        }
         if (nchanged == 0) {
             ps.choice = chnew;
             ps.cost = cin;
@@ -1143,14 +1149,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             set_error("parse fixed point did not converge");
             return -1;
         }
-        // Exact costs for the new decisions (E was marked by the chunk pass).
-        hipLaunchKernelGGL(k_exit_pack, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st,
-                           reinterpret_cast<const uint64_t *>(eflag), S / 8, eb);
-        SALZ_LAUNCH_CHECK();
-        if (scan_sum_u32(eb.wcnt, eb.wpre, S / 64, false, etotal, ws, st) != 0)
-            return -1;
-        if (read_scalars(ws, 0, 256, "parse.ne") != 0)
-            return -1;
+        // Exact costs for the new decisions.
         const uint32_t ne = reinterpret_cast<uint32_t *>(ws.hscal)[49];
         const uint32_t K = (uint32_t)bit_width(ne > 1 ? ne - 1 : 0);
         // Every level's parents are kept for emission's path marking when they fit (the usual

@@ -242,22 +242,34 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist_dig(const uint8_t *__re
 // Digit-major tile counts -> per-digit exclusive prefixes over the tiles (in place), one
 // workgroup per digit, plus the digit totals; k_radix_scatter adds the digit bases (an
 // exclusive scan of the 256 totals) itself. One launch instead of a three-kernel device scan.
-constexpr int kRowThreads = 1024;
-constexpr int kRowItems = 4;
-__global__ __launch_bounds__(kRowThreads) void k_radix_rowscan(uint32_t *__restrict__ counts,
-                                                               uint32_t ntiles,
-                                                               uint32_t *__restrict__ totals)
+// A step takes TH * IT counts: coalesced loads into LDS (one pad word per 32, so that a thread's
+// IT consecutive words are conflict-free), IT per thread scanned in registers, a block scan of
+// the thread sums, and coalesced stores back. radix_rowscan picks the shape by the tile count:
+// 256-thread workgroups for the small sorts that run beside other encodes (a 1024-thread
+// workgroup waits for a whole free CU), one step for rows of up to 24576 tiles (100 MB).
+__device__ __forceinline__ uint32_t rs_pad(uint32_t x) { return x + (x >> 5); }
+
+template <int TH, int IT>
+__global__ __launch_bounds__(TH) void k_radix_rowscan(uint32_t *__restrict__ counts, uint32_t ntiles,
+                                                      uint32_t *__restrict__ totals)
 {
-    __shared__ uint32_t wsum[kRowThreads / 64];
+    constexpr uint32_t kStep = TH * IT;
+    __shared__ uint32_t buf[kStep + kStep / 32];
+    __shared__ uint32_t wsum[TH / 64];
     uint32_t *row = counts + (size_t)blockIdx.x * ntiles;
     const unsigned tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     uint32_t carry = 0;
-    for (uint32_t base = 0; base < ntiles; base += kRowThreads * kRowItems) {
-        uint32_t v[kRowItems], sum = 0;
+    for (uint32_t base = 0; base < ntiles; base += kStep) {
 #pragma unroll
-        for (int j = 0; j < kRowItems; j++) {
-            const uint32_t i = base + tid * kRowItems + j;
-            v[j] = i < ntiles ? row[i] : 0u;
+        for (int j = 0; j < IT; j++) {
+            const uint32_t i = base + j * TH + tid;
+            buf[rs_pad(j * TH + tid)] = i < ntiles ? row[i] : 0u;
+        }
+        __syncthreads();
+        uint32_t v[IT], sum = 0;
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            v[j] = buf[rs_pad(tid * IT + j)];
             sum += v[j];
         }
         uint32_t x = sum;
@@ -271,24 +283,40 @@ __global__ __launch_bounds__(kRowThreads) void k_radix_rowscan(uint32_t *__restr
             wsum[wave] = x;
         __syncthreads();
         uint32_t pre = carry, all = 0;
-        for (unsigned w = 0; w < kRowThreads / 64; w++) {
+#pragma unroll
+        for (unsigned w = 0; w < TH / 64; w++) {
             const uint32_t ws = wsum[w];
             pre += w < wave ? ws : 0u;
             all += ws;
         }
         uint32_t run = pre + x - sum;
 #pragma unroll
-        for (int j = 0; j < kRowItems; j++) {
-            const uint32_t i = base + tid * kRowItems + j;
-            if (i < ntiles)
-                row[i] = run;
+        for (int j = 0; j < IT; j++) {
+            buf[rs_pad(tid * IT + j)] = run;
             run += v[j];
         }
         carry += all;
         __syncthreads();
+#pragma unroll
+        for (int j = 0; j < IT; j++) {
+            const uint32_t i = base + j * TH + tid;
+            if (i < ntiles)
+                row[i] = buf[rs_pad(j * TH + tid)];
+        }
+        __syncthreads();
     }
     if (tid == 0)
         totals[blockIdx.x] = carry;
+}
+
+void radix_rowscan(uint32_t *counts, uint32_t ntiles, uint32_t *totals, hipStream_t st)
+{
+    if (ntiles <= 256 * 16)
+        hipLaunchKernelGGL((k_radix_rowscan<256, 16>), dim3(256), dim3(256), 0, st, counts, ntiles, totals);
+    else if (ntiles <= 512 * 16)
+        hipLaunchKernelGGL((k_radix_rowscan<512, 16>), dim3(256), dim3(512), 0, st, counts, ntiles, totals);
+    else
+        hipLaunchKernelGGL((k_radix_rowscan<1024, 24>), dim3(256), dim3(1024), 0, st, counts, ntiles, totals);
 }
 
 // TH threads per 4096-element tile (256: 16 items per thread; 512: 8 items, half the registers
@@ -580,8 +608,7 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
                                shift, ws.radix_counts, ntiles, txt, dig_in);
         SALZ_LAUNCH_CHECK();
         uint32_t *totals = ws.radix_counts + ncounts;
-        hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(kRowThreads), 0, st, ws.radix_counts,
-                           ntiles, totals);
+        radix_rowscan(ws.radix_counts, ntiles, totals, st);
         SALZ_LAUNCH_CHECK();
         // bench.py prices the timed launches at 24 B per element (key + value in and out);
         // the text-sourced and block passes are left out of that roofline
@@ -640,7 +667,7 @@ int radix_sort_by_group(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, ui
         hipLaunchKernelGGL(k_radix_hist<4>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, 8 * pass,
                            ws.radix_counts, ntiles, txt, nullptr);
         SALZ_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_radix_rowscan, dim3(256), dim3(kRowThreads), 0, st, ws.radix_counts, ntiles, totals);
+        radix_rowscan(ws.radix_counts, ntiles, totals, st);
         SALZ_LAUNCH_CHECK();
         hipLaunchKernelGGL((k_radix_scatter<4, kThreads>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, kout, vout,
                            m, 8 * pass, ws.radix_counts, ntiles, totals, txt, nullptr, 0);
