@@ -83,6 +83,8 @@ def parse_args():
                          "(payload staged through host memory; ranks may share a GPU)")
     ap.add_argument("--launch", action="store_true",
                     help="go through torch.distributed.run even at --gpus 1 (world-1 RCCL path)")
+    ap.add_argument("--ctx-streams", action="store_true",
+                    help="tuning: each slot encodes on its context's own HIP stream instead of a torch stream")
     ap.add_argument("--slots", type=int, default=0,
                     help="concurrent encoder contexts per GPU for the sharded workloads "
                          "(0 = auto: 4; one block per GPU: 1)")
@@ -419,9 +421,9 @@ def main():
         s, e, _ = units[j]
         if use_batch:
             return ctxs[k].encode_batch_device(d_src[j].data_ptr(), e - s, block, d_dst[j].data_ptr(),
-                                               caps[j], streams_t[k].cuda_stream)
+                                               caps[j], None if args.ctx_streams else streams_t[k].cuda_stream)
         return ctxs[k].encode_device(d_src[j].data_ptr(), e - s, d_dst[j].data_ptr(), caps[j],
-                                     streams_t[k].cuda_stream)
+                                     None if args.ctx_streams else streams_t[k].cuda_stream)
 
     # Units are handed out largest first to whichever slot is free (the last block of a sharded
     # input is the short one: it no longer runs alone at the end of the step).

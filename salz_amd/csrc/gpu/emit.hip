@@ -120,15 +120,30 @@ __device__ __forceinline__ uint32_t walk_end(uint32_t g, uint32_t chunk, const B
     return (e - a) < chunk ? e : a + chunk;
 }
 
+// A chunk's token records (the path walk of k_emit_count, read back by k_emit_write): token k of
+// chunk g at slot tok_slot(g, k), the chunk-interleaved layout of common.hpp (the 64 lanes of a
+// wave store and load their k-th tokens as one contiguous run). A record is len << 32 | off for
+// a factor and 1 << 32 | byte for a literal; a chunk's walk covers at most K positions, so at
+// most K tokens.
+__device__ __forceinline__ size_t tok_slot(uint32_t g, uint32_t k, uint32_t klog)
+{
+    return (((size_t)(g >> 6) << (klog + 6)) | (g & 63u)) + ((size_t)k << 6);
+}
+
+// Per chunk: the path's bits and raw bytes (scanned into the chunks' origins) and its tokens.
+// The walk is a chain of dependent loads (the next position is this token's length past it);
+// the writing pass then reads the records back in batches instead of walking again.
 __global__ void k_emit_count(const uint4 *__restrict__ cand, const uint8_t *__restrict__ choice,
-                             const uint32_t *__restrict__ entry, Blocks bl, uint32_t N_last,
-                             uint32_t chunk, uint32_t nch, uint64_t *__restrict__ cbits,
-                             uint64_t *__restrict__ cbytes, uint32_t klog)
+                             const uint8_t *__restrict__ T, const uint32_t *__restrict__ entry, Blocks bl,
+                             uint32_t N_last, uint32_t chunk, uint32_t nch, uint64_t *__restrict__ cbits,
+                             uint64_t *__restrict__ cbytes, uint32_t klog, uint64_t *__restrict__ tok,
+                             uint32_t *__restrict__ ntok)
 {
     uint32_t g = blockIdx.x * kT + threadIdx.x;
     if (g > nch)
         return;
     uint64_t bits = 0, bytes = 0;
+    uint32_t k = 0;
     if (g == nch) {
         bits = N_last - bl.n_last();
         bytes = N_last - bl.n_last();
@@ -137,21 +152,29 @@ __global__ void k_emit_count(const uint4 *__restrict__ cand, const uint8_t *__re
         if (p != kNone) {
             const uint32_t b = walk_end(g, chunk, bl), e = bl.end(g * chunk);
             while (p < b) {
+                // (the text byte is loaded with the token, unconditionally: the text is padded)
+                const uint32_t lit = T[p];
                 Token t = p < e ? token_at(cand, choice, p, klog) : Token{1u, 0u};
+                uint64_t rec;
                 if (t.len == 1) {
                     bits += 1;
                     bytes += 1;
+                    rec = (1ull << 32) | lit;
                 } else {
                     uint32_t gl = t.len - 3u;
                     bits += 1u + 4u * vn_size((t.off - 1u) >> 8) + (gl >> 3) + 4u;
                     bytes += 1;
+                    rec = ((uint64_t)t.len << 32) | t.off;
                 }
+                tok[tok_slot(g, k, klog)] = rec;
+                k++;
                 p += t.len;
             }
         }
     }
     cbits[g] = bits;
     cbytes[g] = bytes;
+    ntok[g] = k;
 }
 
 struct Sink {
@@ -239,14 +262,27 @@ struct BlockOut {
     uint64_t bs, ys, wbase, len;
 };
 
-__global__ void k_emit_write(const uint8_t *__restrict__ T, const uint4 *__restrict__ cand,
-                             const uint8_t *__restrict__ choice, const uint32_t *__restrict__ entry,
-                             Blocks bl, uint32_t N_last, uint32_t chunk, uint32_t nch,
-                             const uint64_t *__restrict__ bst, const uint64_t *__restrict__ yst,
+// Records are read in batches of kBatch, all lanes at once (clamped slots, a wave-uniform trip
+// count), and the whole batch has arrived before any is used, so the stores of one batch (under
+// the branches' masks) are never separated by a partial vmcnt wait from the next batch's loads
+// ("Concurrent encodes and the unaligned text load"; tests/test_codegen.py).
+constexpr uint32_t kBatch = 8;
+
+__global__ void k_emit_write(const uint8_t *__restrict__ T, const uint64_t *__restrict__ tok,
+                             const uint32_t *__restrict__ ntok, Blocks bl, uint32_t N_last, uint32_t chunk,
+                             uint32_t nch, const uint64_t *__restrict__ bst, const uint64_t *__restrict__ yst,
                              uint64_t btotal, uint64_t *W, uint32_t *Yk, uint8_t *out, size_t stride,
                              const BlockOut *__restrict__ binfo, uint32_t klog)
 {
-    uint32_t g = blockIdx.x * kT + threadIdx.x;
+    const uint32_t g = blockIdx.x * kT + threadIdx.x;
+    // the wave's largest token count (every lane still active here)
+    const uint32_t nt = g < nch ? ntok[g] : 0u;
+    uint32_t ntmax = nt;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint32_t o = shfl_xor_u32(ntmax, m);
+        ntmax = o > ntmax ? o : ntmax;
+    }
     if (g > nch)
         return;
     const uint32_t blk = g == nch ? bl.nb - 1u : bl.blk(g * chunk);
@@ -262,32 +298,44 @@ __global__ void k_emit_write(const uint8_t *__restrict__ T, const uint4 *__restr
     s.cur = 0;
     s.kc = 0;
     s.have = false;
-    if (s.B1 == s.B0)
-        return;
     if (g == nch) {
+        if (s.B1 == s.B0)
+            return;
         for (uint32_t i = bl.npos; i < bl.npos + (N_last - bl.n_last()); i++) {
             s.put(0, 1);
             s.byte(T[i]);
         }
-    } else {
-        uint32_t p = walk_start(entry, g, chunk, bl);
-        const uint32_t b = walk_end(g, chunk, bl), e = bl.end(g * chunk);
-        while (p < b) {
-            Token t = p < e ? token_at(cand, choice, p, klog) : Token{1u, 0u};
-            if (t.len == 1) {
+        s.flush();
+        return;
+    }
+    for (uint32_t k0 = 0; k0 < ntmax; k0 += kBatch) {
+        uint64_t r[kBatch];
+#pragma unroll
+        for (uint32_t q = 0; q < kBatch; q++) {
+            const uint32_t k = k0 + q;
+            r[q] = tok[tok_slot(g, k < nt ? k : 0u, klog)];
+        }
+        // every record of the batch is an operand: one full wait after the batch's loads
+        static_assert(kBatch == 8, "operand list");
+        asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
+#pragma unroll
+        for (uint32_t q = 0; q < kBatch; q++) {
+            if (k0 + q >= nt)
+                break;
+            const uint32_t len = (uint32_t)(r[q] >> 32);
+            if (len == 1) {
                 s.put(0, 1);
-                s.byte(T[p]);
+                s.byte((uint8_t)r[q]);
             } else {
-                uint32_t v = t.off - 1u;
-                uint32_t k = vn_size(v >> 8);
+                uint32_t v = (uint32_t)r[q] - 1u;
+                uint32_t kv = vn_size(v >> 8);
                 s.put(1, 1);
-                s.put(vn_bits(v >> 8, k), 4 * k);
+                s.put(vn_bits(v >> 8, kv), 4 * kv);
                 s.byte((uint8_t)(v & 0xffu));
-                uint32_t gl = t.len - 3u;
+                uint32_t gl = len - 3u;
                 s.zeros(gl >> 3);
                 s.put(8u | (gl & 7u), 4);  // unary terminator + 3 low bits
             }
-            p += t.len;
         }
     }
     s.flush();
@@ -435,8 +483,13 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
                            n, ps.chunk, entry);
         SALZ_LAUNCH_CHECK();
     }
+    // token records (keyB: the parse's jump snapshots, read only by the marking above) and their
+    // counts per chunk (u3)
+    uint64_t *tok = ws.keyB;
+    uint32_t *ntok = ws.u3;
     hipLaunchKernelGGL(k_emit_count, dim3(grid_for((size_t)nch + 1, kT)), dim3(kT), 0, st,
-                       ws.cand, ps.choice, entry, bl, N_last, ps.chunk, nch, cbits, cbytes, ws.klog);
+                       ws.cand, ps.choice, ws.text, entry, bl, N_last, ps.chunk, nch, cbits, cbytes, ws.klog, tok,
+                       ntok);
     SALZ_LAUNCH_CHECK();
     if (scan_sum_u64(cbits, cbits, (size_t)nch + 1, false, tot + 0, ws, st) != 0)
         return -1;
@@ -470,8 +523,8 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
     SALZ_HIP(hipMemsetAsync(W, 0, sizeof(uint64_t) * (nwords + 1), st));
     SALZ_HIP(hipMemsetAsync(Yk, 0, sizeof(uint32_t) * (nwords + 1), st));
     hipLaunchKernelGGL(k_emit_write, dim3(grid_for((size_t)nch + 1, kT)), dim3(kT), 0, st,
-                       ws.text, ws.cand, ps.choice, entry, bl, N_last, ps.chunk, nch, cbits, cbytes,
-                       btotal, W, Yk, dst, stride, binfo, ws.klog);
+                       ws.text, tok, ntok, bl, N_last, ps.chunk, nch, cbits, cbytes, btotal, W, Yk, dst, stride,
+                       binfo, ws.klog);
     SALZ_LAUNCH_CHECK();
     // Yk of the words inside zero runs (Sink::zeros): Yk is non-decreasing in k
     if (nwords && scan_max_u32(Yk, Yk, nwords, true, nullptr, ws, st) != 0)

@@ -614,8 +614,12 @@ __global__ __launch_bounds__(kT) void k_mark_final(uint32_t n, uint32_t klog, co
 // Exit flags (bytes marked by the chunk pass, storage-slot order) -> ExitBits: the set as one
 // bit per slot, 64 slots a word (one row of a 64-chunk tile), and per-word popcounts for the
 // scan that numbers E. A thread packs 8 flag bytes, 8 lanes one word.
-__global__ __launch_bounds__(kT) void k_exit_pack(const uint64_t *__restrict__ eflag8, size_t S8, ExitBits eb)
+// (nd: the pass's dirty-wave count when its test ran; none dirty -> E unchanged, nothing to pack)
+__global__ __launch_bounds__(kT) void k_exit_pack(const uint64_t *__restrict__ eflag8, size_t S8, ExitBits eb,
+                                                  const uint32_t *__restrict__ nd)
 {
+    if (nd && *nd == 0u)
+        return;
     const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;  // slots [8x, 8x + 8)
     uint64_t v = eflag8[x < S8 ? x : 0];  // (unconditional load, clamped)
     v |= v >> 4;
@@ -1117,7 +1121,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         // the changed count, |E| (etotal), the dirty waves and the chunks the test listed
         // together. A pass that changed nothing leaves E as it was, so these are unchanged then.
         hipLaunchKernelGGL(k_exit_pack, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st,
-                           reinterpret_cast<const uint64_t *>(eflag), S / 8, eb);
+                           reinterpret_cast<const uint64_t *>(eflag), S / 8, eb, skipping ? ndirty : nullptr);
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u32(eb.wcnt, eb.wpre, S / 64, false, etotal, ws, st) != 0)
             return -1;
