@@ -319,6 +319,15 @@ void radix_rowscan(uint32_t *counts, uint32_t ntiles, uint32_t *totals, hipStrea
         hipLaunchKernelGGL((k_radix_rowscan<1024, 24>), dim3(256), dim3(1024), 0, st, counts, ntiles, totals);
 }
 
+// Tile of scatter workgroup b: workgroups are dealt round-robin to the 8 XCDs (b mod 8), so XCD x
+// takes the x-th eighth of the tiles in order, and consecutive tiles, whose runs of one digit are
+// adjacent in the output, write them through the same L2 (a run's partial end lines merge there).
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t ntiles)
+{
+    const uint32_t x = b & 7u, i = b >> 3, per = ntiles >> 3, rem = ntiles & 7u;
+    return x * per + (x < rem ? x : rem) + i;
+}
+
 // TH threads per 4096-element tile (256: 16 items per thread; 512: 8 items, half the registers
 // per thread and twice the waves per CU for the same LDS).
 template <int kMode, int TH>
@@ -339,12 +348,13 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     __shared__ uint32_t wsum[2][4];
 
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
     for (int i = tid; i < NW * 256; i += TH)
         (&cnt[0][0])[i] = 0;
     __syncthreads();
 
     // Warp-striped: wave w owns tile elements [w*IT*64, (w+1)*IT*64), item j covers 64 of them.
-    const size_t base = (size_t)blockIdx.x * kTile + (size_t)wave * (IT * 64);
+    const size_t base = (size_t)tile * kTile + (size_t)wave * (IT * 64);
     uint64_t k[IT];
     uint32_t v[IT];
     uint32_t lrank[IT];
@@ -355,7 +365,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     if (kMode == 3) {
         uint64_t *W = skey;
         constexpr uint32_t kWords = kTile / 8 + 3;
-        const size_t tb = (size_t)blockIdx.x * kTile;
+        const size_t tb = (size_t)tile * kTile;
         const size_t w0 = tb ? (tb - 7) >> 3 : 0;
         const size_t wmax = ((size_t)txt.g.npos + 64) >> 3;  // zero padding past the text
         for (uint32_t q = tid; q < kWords; q += TH) {
@@ -461,7 +471,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
             pt += wsum[0][w];
             pc += wsum[1][w];
         }
-        gbase[tid] = pt + xt - tt + offs[(size_t)tid * ntiles + blockIdx.x];
+        gbase[tid] = pt + xt - tt + offs[(size_t)tid * ntiles + tile];
         const uint32_t ds = pc + xc - tot;
         dstart[tid] = ds;
         uint32_t run = 0;
@@ -487,7 +497,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
                 sval[pos[j]] = v[j];
         }
         __syncthreads();
-        const size_t tbase = (size_t)blockIdx.x * kTile;
+        const size_t tbase = (size_t)tile * kTile;
         const uint32_t tcount = (uint32_t)((m - tbase) < (size_t)kTile ? (m - tbase) : (size_t)kTile);
         uint32_t gdst[IT];
 #pragma unroll
@@ -527,7 +537,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     }
     __syncthreads();
 
-    size_t tbase = (size_t)blockIdx.x * kTile;
+    size_t tbase = (size_t)tile * kTile;
     uint32_t tcount = (uint32_t)((m - tbase) < (size_t)kTile ? (m - tbase) : (size_t)kTile);
     uint32_t gdst[IT];  // global destination of staged slot tid + j * TH
 #pragma unroll

@@ -29,10 +29,11 @@
 //               index and new group id are prefix + popcount (large groups take their ids and
 //               extraction ranges with one atomic per group in k_commit)
 //   k_commit    rank update for every active suffix (in large rounds staged by text range
-//               and applied window by window: k_rank_stage / k_rank_apply), SA write for
+//               and applied window by window: scatter_staged), SA write for
 //               singletons, compaction
 //   k_keys      next round's keys: gid << kb | rank[i + h]
 #include "internal.hpp"
+#include "scatter.hpp"
 
 #include <chrono>
 #include <cstdlib>
@@ -319,7 +320,7 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
     const uint32_t slot = c + o, rpos = hp + o;  // SA slot (singletons); rank = group head's + 1
     // rank[i] is a random 4-byte scatter (a read-modify-write of a whole HBM burst). Large
     // rounds write only the ranks of i < ihi here and leave every update in list order in
-    // `later` for the split passes (k_rank_upper) or the staged scatter (k_rank_apply); small
+    // `later` for the split passes (k_rank_upper) or the staged scatter (scatter_staged); small
     // ones write rank directly (ihi = ~0, no `later`). The entry that keeps its old head's
     // place keeps its rank.
     const bool keep = (same && rpos == hp + o) || (!surv_rank && size > 1);
@@ -470,68 +471,18 @@ __global__ void k_dead_ranks(Blocks bl, uint32_t *__restrict__ rank)
     rank[b * bl.bs + bl.bs - 8u + (x & 7u)] = 0u;
 }
 
-// Staged rank scatter. k_commit leaves the new ranks in list order (later[c], 0xffffffff when
-// unchanged); the list's suffixes are in random text order, so writing rank[i] directly is a
-// 4-byte scatter over the whole rank array (n * 4 bytes, beyond the 256 MB Infinity Cache on
-// large blocks). Instead k_rank_stage bins the updates by text range (2^rlog positions = 4 MB
-// of rank per range) into per-range runs (LDS counts, one global atomic per range and tile),
-// and k_rank_apply writes them range by range, XCD-aware, so the writes in flight on one XCD
-// fall in one L2-sized window of the rank array (the ANSV staging of ansv.hip, for ranks).
-constexpr uint32_t kStageTile = 4096;
-constexpr uint32_t kStageRanges = 1024;
-
-__global__ __launch_bounds__(kT) void k_rank_stage(const uint32_t *__restrict__ val,
-                                                   const uint32_t *__restrict__ later, uint32_t m,
-                                                   uint32_t rlog, uint32_t *__restrict__ rfill,
-                                                   uint2 *__restrict__ stage)
-{
-    __shared__ uint32_t cnt[kStageRanges];
-    constexpr uint32_t kItems = kStageTile / kT;
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t r = tid; r < kStageRanges; r += kT)
-        cnt[r] = 0;
-    __syncthreads();
-    const size_t base = (size_t)blockIdx.x * kStageTile;
-    uint32_t iv[kItems], rv[kItems], loc[kItems];
-#pragma unroll
-    for (uint32_t j = 0; j < kItems; j++) {  // unconditional loads (clamped entry)
-        const size_t c = base + (size_t)j * kT + tid;
-        const size_t cc = c < m ? c : 0;
-        iv[j] = val[cc];
-        rv[j] = later[cc];
-        if (c >= m)
-            rv[j] = 0xffffffffu;
+// Staged rank scatter (scatter.hpp): k_commit leaves the new ranks in list order (later[c],
+// 0xffffffff when unchanged); scatter_staged bins them by text window and applies them window by
+// window, XCD-aware.
+struct LaterSrc {
+    const uint32_t *val, *later;
+    __device__ __forceinline__ bool operator()(size_t c, uint32_t &idx, uint32_t &v) const
+    {
+        idx = val[c];
+        v = later[c];
+        return v != 0xffffffffu;
     }
-#pragma unroll
-    for (uint32_t j = 0; j < kItems; j++)
-        loc[j] = rv[j] != 0xffffffffu ? atomicAdd(&cnt[iv[j] >> rlog], 1u) : 0u;
-    __syncthreads();
-    for (uint32_t r = tid; r < kStageRanges; r += kT)
-        if (cnt[r])
-            cnt[r] = (r << rlog) + atomicAdd(&rfill[r], cnt[r]);
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < kItems; j++)
-        if (rv[j] != 0xffffffffu)
-            stage[cnt[iv[j] >> rlog] + loc[j]] = make_uint2(iv[j], rv[j]);
-}
-
-// Workgroup g runs on XCD g mod 8 (round-robin dispatch, a speed assumption only): XCD x takes
-// text ranges x, x + 8, ... in turn, 256 staged updates per workgroup.
-__global__ __launch_bounds__(kT) void k_rank_apply(const uint2 *__restrict__ stage,
-                                                   const uint32_t *__restrict__ rfill, uint32_t rlog,
-                                                   uint32_t nranges, uint32_t *__restrict__ rank)
-{
-    const uint32_t g = blockIdx.x, tiles = 1u << (rlog - 8);
-    const uint32_t k = g >> 3, r = (g & 7u) + 8u * (k >> (rlog - 8));
-    if (r >= nranges)
-        return;
-    const uint32_t x = (k & (tiles - 1u)) * kT + threadIdx.x;
-    if (x >= rfill[r])
-        return;
-    const uint2 e = stage[((size_t)r << rlog) + x];
-    rank[e.x] = e.y;
-}
+};
 
 // Later passes of a split rank scatter: ranks of suffixes in [ilo, ihi), from k_commit's list.
 __global__ void k_rank_upper(const uint32_t *__restrict__ val, const uint32_t *__restrict__ later,
@@ -1471,8 +1422,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         //   direct  k_commit writes rank[i] (small rounds);
         //   split   k_commit writes the lower text part, k_rank_upper passes the rest, parts of
         //           at most ~200 MB of rank array each (Infinity-Cache-sized windows);
-        //   stage   every update binned by text range (k_rank_stage) and applied window by
-        //           window (k_rank_apply, XCD-aware), for rank arrays far past the cache.
+        //   stage   every update binned by text window and applied window by window
+        //           (scatter_staged, XCD-aware), for rank arrays far past the cache.
         // Default: up to 512 MB of ranks split from 32M updates, above it stage from 4M, 1 MB
         // windows (Fibonacci 256 MiB: SA 554 -> 505 ms; text 100 MB: SA 24.8 ms split, 25.3
         // staged; profiles/r02l_*).
@@ -1496,21 +1447,10 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                                q * span, q + 1 == parts ? 0xffffffffu : (q + 1) * span, ws.rank);
             SALZ_LAUNCH_CHECK();
         }
-        if (mode == 2) {
-            uint32_t rlog = 18;
-            while ((((uint64_t)n - 1) >> rlog) + 1 > kStageRanges)
-                rlog++;
-            const uint32_t nranges = (uint32_t)((((uint64_t)n - 1) >> rlog) + 1);
-            uint32_t *rfill = ws.radix_counts;  // free outside the radix sorts
-            uint2 *stage = reinterpret_cast<uint2 *>(ws.pst);  // free after this round's sort
-            SALZ_HIP(hipMemsetAsync(rfill, 0, kStageRanges * sizeof(uint32_t), st));
-            hipLaunchKernelGGL(k_rank_stage, dim3(grid_for(m, kStageTile)), dim3(kT), 0, st, V, later, m,
-                               rlog, rfill, stage);
-            SALZ_LAUNCH_CHECK();
-            const uint32_t agrid = 8u * ((nranges + 7u) / 8u) << (rlog - 8);
-            hipLaunchKernelGGL(k_rank_apply, dim3(agrid), dim3(kT), 0, st, stage, rfill, rlog, nranges,
-                               ws.rank);
-            SALZ_LAUNCH_CHECK();
+        if (mode == 2) {  // (pst is free after this round's sort)
+            if (scatter_staged(LaterSrc{V, later}, m, n, ws.rank, 1u, 0u, reinterpret_cast<uint2 *>(ws.pst),
+                               ws.cap_s, ws.radix_counts, st) != 0)
+                return -1;
         }
         // A split block's ranks leave together: a local failure is folded into the round's
         // allreduce (bit 48 and up count failed ranks) instead of leaving the others blocked.

@@ -72,8 +72,8 @@ __global__ __launch_bounds__(kScThreads) void k_sc_apply(const uint2 *__restrict
     dst[(size_t)e.x * stride + field] = e.y;
 }
 
-// Scatter m pairs from src into dst (indices < nidx), staged through `stage` (room for
-// nidx + 2^rlog pairs) with window counters rfill (one word per window of 2^rlog indices).
+// Scatter m pairs from src into dst (indices < nidx, each at most once), staged through `stage`
+// (room for nidx pairs) with window counters rfill (one word per window of 2^rlog indices).
 template <class Src>
 int scatter_staged(Src src, uint32_t m, uint32_t nidx, uint32_t *dst, uint32_t stride, uint32_t field,
                    uint2 *stage, size_t stage_cap, uint32_t *rfill, hipStream_t st)
@@ -84,7 +84,8 @@ int scatter_staged(Src src, uint32_t m, uint32_t nidx, uint32_t *dst, uint32_t s
     while ((((uint64_t)nidx - 1) >> rlog) + 1 > kScWindows)
         rlog++;
     const uint32_t nwin = (uint32_t)((((uint64_t)nidx - 1) >> rlog) + 1);
-    if (((size_t)nwin << rlog) > stage_cap) {
+    // window r's run starts at r << rlog and holds its indices (< nidx): every slot is below nidx
+    if ((size_t)nidx > stage_cap) {
         set_error("staged scatter: %u windows of 2^%u exceed the staging buffer (%zu)", nwin, rlog, stage_cap);
         return -1;
     }
