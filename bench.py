@@ -202,6 +202,11 @@ def measure_traffic(args):
     import subprocess
     import tempfile
 
+    # Under a profiler already (this bench is the program of an outer rocprofv3 run), its library
+    # is preloaded into every child: a nested rocprofv3 would start with the GPU initialised and
+    # then exec the program, which is never done. Those runs measure the counters themselves.
+    if any(k.startswith("ROCPROF") for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None, "not measured: this run is itself under rocprofv3"
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
         return None, "rocprofv3 not found"

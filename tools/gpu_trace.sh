@@ -5,5 +5,5 @@
 set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out/${TAG:-trace}; mkdir -p $out
-SALZ_DEBUG=parse timeout -k 10 200 rocprofv3 --kernel-trace -d $out/mixed -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-e2e --kind mixed --steps 1 --warmup 0 > $out/mixed.json 2> $out/mixed.err &&
-SALZ_DEBUG=parse timeout -k 10 200 rocprofv3 --kernel-trace -d $out/sil -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-e2e --workload silesia --steps 1 --warmup 0 > $out/sil.json 2> $out/sil.err
+SALZ_DEBUG=parse timeout -k 10 200 rocprofv3 --kernel-trace -d $out/mixed -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-pmc --no-e2e --kind mixed --steps 1 --warmup 0 > $out/mixed.json 2> $out/mixed.err &&
+SALZ_DEBUG=parse timeout -k 10 200 rocprofv3 --kernel-trace -d $out/sil -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-pmc --no-e2e --workload silesia --steps 1 --warmup 0 > $out/sil.json 2> $out/sil.err
