@@ -675,9 +675,20 @@ __global__ __launch_bounds__(kT) void k_compact_exits(ExitBits eb, const uint64_
     }
 }
 
-// The same, one thread per node of E (its word by a binary search over the word prefixes, its slot
-// by selecting the set bit): |E| threads instead of one per 8 slots, where E is sparse.
-__global__ __launch_bounds__(kT) void k_compact_nodes(ExitBits eb, size_t nw, uint32_t steps, uint32_t ne,
+// Node -> mask word of a sparse E: a thread per word writes its index at its nodes' numbers.
+__global__ __launch_bounds__(kT) void k_node_words(ExitBits eb, size_t nw, uint32_t *__restrict__ nword)
+{
+    const size_t w = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (w >= nw)
+        return;
+    const uint32_t c = eb.wcnt[w], b = eb.wpre[w];
+    for (uint32_t k = 0; k < c; k++)
+        nword[b + k] = (uint32_t)w;
+}
+
+// The same, one thread per node of E (its word from k_node_words, its slot by selecting the set
+// bit): |E| threads instead of one per 8 slots, where E is sparse.
+__global__ __launch_bounds__(kT) void k_compact_nodes(ExitBits eb, const uint32_t *__restrict__ nword, uint32_t ne,
                                                       const uint64_t *__restrict__ pst,
                                                       const uint32_t *__restrict__ cin, uint32_t n, uint32_t klog,
                                                       uint32_t *__restrict__ elist, uint32_t *__restrict__ jt0,
@@ -687,14 +698,7 @@ __global__ __launch_bounds__(kT) void k_compact_nodes(ExitBits eb, size_t nw, ui
     const uint32_t xi = blockIdx.x * kT + threadIdx.x;
     if (xi >= ne)
         return;
-    // the last word whose prefix is <= xi (a fixed number of steps, every load unconditional)
-    size_t lo = 0, hi = nw;
-    for (uint32_t i = 0; i < steps; i++) {
-        const size_t mid = (lo + hi) >> 1;
-        const bool le = eb.wpre[mid] <= xi;
-        lo = le ? mid : lo;
-        hi = le ? hi : mid;
-    }
+    const uint32_t lo = nword[xi];
     uint64_t m = eb.mask[lo];
     uint32_t k = xi - eb.wpre[lo], p = 0;
 #pragma unroll
@@ -705,7 +709,7 @@ __global__ __launch_bounds__(kT) void k_compact_nodes(ExitBits eb, size_t nw, ui
         m = up ? m >> w : m;
         p += up ? w : 0u;
     }
-    const size_t s = lo * 64 + p;
+    const size_t s = (size_t)lo * 64 + p;
     const uint32_t q = (uint32_t)spos(s, klog);
     const uint64_t v = pst[s];
     const uint32_t ev = q >= n ? n : (uint32_t)v;
@@ -1166,9 +1170,12 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         }
         if (node_compact == 2 || (node_compact == 1 && (uint64_t)ne * 64 < S)) {  // sparse E: a thread per node
             const size_t nw = S / 64;
-            hipLaunchKernelGGL(k_compact_nodes, dim3(grid_for(ne, kT)), dim3(kT), 0, st, eb, nw,
-                               (uint32_t)bit_width(nw) + 1u, ne, ws.pst, cin, n, klog, elist, snap, js[0], dsum,
-                               lz_pass ? Lv[lc] : nullptr, lz_pass ? ce : nullptr);
+            uint32_t *nword = ws.lcps;  // (the LCP array: read by the candidates stage only)
+            hipLaunchKernelGGL(k_node_words, dim3(grid_for(nw, kT)), dim3(kT), 0, st, eb, nw, nword);
+            SALZ_LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_compact_nodes, dim3(grid_for(ne, kT)), dim3(kT), 0, st, eb, nword, ne, ws.pst,
+                               cin, n, klog, elist, snap, js[0], dsum, lz_pass ? Lv[lc] : nullptr,
+                               lz_pass ? ce : nullptr);
         } else {
             hipLaunchKernelGGL(k_compact_exits, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st, eb, ws.pst, cin, n, klog,
                                S / 8, elist, snap, js[0], dsum, lz_pass ? Lv[lc] : nullptr, lz_pass ? ce : nullptr);
