@@ -603,7 +603,7 @@ __device__ __forceinline__ void seg_lsd(uint64_t *sk, uint32_t (*cnt)[256], uint
 //     binary search: the groups stay contiguous in the sorted array).
 // Rank rounds (TEXT = 0): key = group << kb | rank; the LSD passes take the kb rank bits. The
 // text round (TEXT = 1, keys = kb text bits, groups in gin): the LSD passes take the top bits of
-// the key that keep the sort at 40 bits (5 passes); the runs of equal (group, top bits) they leave
+// the key that keep the sort at 48 bits (6 passes); the runs of equal (group, top bits) they leave
 // are marked (rb, need) and ordered by the whole key in k_seg_text_fix.
 constexpr uint32_t kPer = kSegCap / kSegThreads;
 
@@ -612,7 +612,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_sort(uint64_t *__restrict__
                                                           const uint32_t *__restrict__ gin, SegPlan plan,
                                                           const uint64_t *__restrict__ ginfo, uint32_t m, int kb,
                                                           uint32_t tiny, uint64_t *__restrict__ rb,
-                                                          uint32_t *__restrict__ need, uint32_t *err)
+                                                          uint32_t *__restrict__ need, uint32_t *err, int lsd_bits)
 {
     __shared__ uint64_t sk[kSegCap];  // the window's keys, then the larger groups' LSD keys
     __shared__ uint32_t sv[kSegCap];  // the window's values (by window index)
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_sort(uint64_t *__restrict__
     const uint32_t count = hi - lo;
     const uint64_t mask = kb >= 64 ? ~0ull : (1ull << kb) - 1ull;
     const int gbits = 32 - __builtin_clz((g1 - g0) | 1u);
-    const int kr = TEXT ? (kb < 40 - gbits ? kb : 40 - gbits) : kb;  // key bits in the LSD key
+    const int kr = TEXT ? (kb < lsd_bits - gbits ? kb : lsd_bits - gbits) : kb;  // key bits in the LSD key
     if (tid == 0)
         nbig = 0;
     for (uint32_t i = tid; i < count; i += kSegThreads) {
@@ -1250,6 +1250,10 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // 0 / 8 / 16 / 32 / 64 / 128 / 256 / 2048; mixed 100 MB 27.2 (0) -> 25.7 ms (64-256)
     // (profiles/r04n_tiny_sweep.txt)
     const uint32_t seg_tiny = (uint32_t)env_num("SALZ_SA", "tiny", 128);
+    // The text round's LDS passes sort (group, top key bits) to 48 bits (6 passes) and leave the
+    // rarer ties to k_seg_text_fix: C2 SA 20.29 -> 20.18 ms against 40 bits (5 passes), 52 bits
+    // (7 passes) 20.28 (profiles/r04w_c3_ab.txt).
+    constexpr int lsd_bits = 48;
     // Round 1 keyed by text (see k_keys_text): one block or a batch, the block's own sort (not a
     // split block's bucket), an alphabet of at most 127 bytes (symbols >= 1, so zero padding
     // is unambiguous). SALZ_SA=rank1 keeps round 1 on ranks.
@@ -1284,7 +1288,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             uint32_t *need = reinterpret_cast<uint32_t *>(ws.pst + (size_t)nwin * (kSegCap / 64));
             SALZ_HIP(hipMemsetAsync(need, 0, sizeof(uint32_t) * nwin, st));
             hipLaunchKernelGGL(k_seg_sort<true>, dim3(nwin), dim3(kSegThreads), 0, st, K, V, gin, plan, tab.ginfo,
-                               m, tbits, seg_tiny, rb, need, derr);
+                               m, tbits, seg_tiny, rb, need, derr, lsd_bits);
             SALZ_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_seg_text_fix, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, rb, need);
             SALZ_LAUNCH_CHECK();
@@ -1346,7 +1350,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                                    G_act, plan);
                 SALZ_LAUNCH_CHECK();
                 hipLaunchKernelGGL(k_seg_sort<false>, dim3(nwin), dim3(kSegThreads), 0, st, K, V, nullptr, plan,
-                                   tab.ginfo, m, kb, seg_tiny, nullptr, nullptr, derr);
+                                   tab.ginfo, m, kb, seg_tiny, nullptr, nullptr, derr, 0);
                 SALZ_LAUNCH_CHECK();
                 if (mL) {
                     uint32_t *tmap = pw + 4 * nwin;  // (lsc, after the window plan)
