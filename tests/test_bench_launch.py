@@ -59,3 +59,21 @@ def test_bench_rejects_world_mismatch():
                         "--no-cpu-baseline"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                        timeout=120, env=env)
     assert p.returncode != 0 and "launcher started 1 ranks" in (p.stderr + p.stdout)
+
+
+def test_bench_skips_its_pmc_passes_under_a_profiler(monkeypatch):
+    """Under an outer rocprofv3 (its library preloaded, ROCPROF_* set) bench.py must not start its
+    own rocprofv3 children: the preloaded profiler would initialise the GPU in the nested
+    wrapper, which then execs the program."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    monkeypatch.setenv("ROCPROF_COUNTERS", "FETCH_SIZE")
+    traffic, why = bench.measure_traffic(None)
+    assert traffic is None and "under rocprofv3" in why
+    monkeypatch.delenv("ROCPROF_COUNTERS")
+    monkeypatch.setenv("LD_PRELOAD", "/opt/rocm/lib/librocprofiler-sdk-tool.so")
+    traffic, why = bench.measure_traffic(None)
+    assert traffic is None and "under rocprofv3" in why
