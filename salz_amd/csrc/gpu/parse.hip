@@ -788,20 +788,60 @@ __global__ __launch_bounds__(kT) void k_cost_rest(ExitBits eb, const uint32_t *_
         v[r] = pst[sr[r]];
         mw[r] = eb.mask[sr[r] >> 6];
     }
-    uint32_t xe[kRows], se[kRows];
+    uint32_t se[kRows];
     bool isx[kRows];
 #pragma unroll
     for (uint32_t r = 0; r < kRows; r++) {
         isx[r] = (mw[r] >> lane) & 1u;  // an exit node: its own path sum
         se[r] = isx[r] ? (uint32_t)sr[r] : (uint32_t)sidx((uint32_t)v[r], klog);
-        const uint64_t m2 = eb.mask[se[r] >> 6];
-        xe[r] = eb.wpre[se[r] >> 6] + (uint32_t)__popcll(m2 & ((1ull << (se[r] & 63u)) - 1ull));
     }
-    uint32_t out[kRows];
+    // The rows of a thread are consecutive positions of one chunk, whose paths mostly leave it
+    // through the same exit: when every lane's rows have at most two distinct exits and at most
+    // one row that is an exit node itself (a wave-uniform test), the exits' index and cost loads
+    // are issued once per distinct exit (5 scattered loads and one per exit row) instead of per
+    // row (the kernel's time was the address processing of 32 scattered loads per thread).
+    uint32_t eA = se[kRows - 1], eB = eA, xr = kRows;  // (row kRows - 1 when every row is an exit)
+    uint32_t nx = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < kRows; r++) {
-        const uint32_t jv = js[xe[r]], cv = cin[se[r]];
-        out[r] = jv + (((uint32_t)(v[r] >> 32) + shift - cv) & (isx[r] ? 0u : 0xffffffffu));
+    for (uint32_t r = kRows; r-- > 0;) {
+        eA = isx[r] ? eA : se[r];  // the first non-exit row's exit
+        xr = isx[r] ? r : xr;
+        nx += isx[r] ? 1u : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = kRows; r-- > 0;)
+        eB = !isx[r] && se[r] != eA ? se[r] : eB;
+    bool few = nx <= 1u;
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; r++)
+        few = few && (isx[r] || se[r] == eA || se[r] == eB);
+    uint32_t out[kRows];
+    if (wave_ballot(!few) == 0) {
+        const uint32_t xs = (uint32_t)sr[xr < kRows ? xr : 0u];
+        const uint64_t mA = eb.mask[eA >> 6], mB = eb.mask[eB >> 6], mX = eb.mask[xs >> 6];
+        const uint32_t pA = eb.wpre[eA >> 6], pB = eb.wpre[eB >> 6], pX = eb.wpre[xs >> 6];
+        const uint32_t xA = pA + (uint32_t)__popcll(mA & ((1ull << (eA & 63u)) - 1ull));
+        const uint32_t xB = pB + (uint32_t)__popcll(mB & ((1ull << (eB & 63u)) - 1ull));
+        const uint32_t xX = pX + (uint32_t)__popcll(mX & ((1ull << (xs & 63u)) - 1ull));
+        const uint32_t jA = js[xA], jB = js[xB], jX = js[xX], cA = cin[eA], cB = cin[eB];
+#pragma unroll
+        for (uint32_t r = 0; r < kRows; r++) {
+            const bool a = se[r] == eA;
+            const uint32_t part = (uint32_t)(v[r] >> 32) + shift - (a ? cA : cB);
+            out[r] = isx[r] ? jX : (a ? jA : jB) + part;
+        }
+    } else {
+        uint32_t xe[kRows];
+#pragma unroll
+        for (uint32_t r = 0; r < kRows; r++) {
+            const uint64_t m2 = eb.mask[se[r] >> 6];
+            xe[r] = eb.wpre[se[r] >> 6] + (uint32_t)__popcll(m2 & ((1ull << (se[r] & 63u)) - 1ull));
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < kRows; r++) {
+            const uint32_t jv = js[xe[r]], cv = cin[se[r]];
+            out[r] = jv + (((uint32_t)(v[r] >> 32) + shift - cv) & (isx[r] ? 0u : 0xffffffffu));
+        }
     }
 #pragma unroll
     for (uint32_t r = 0; r < kRows; r++)
