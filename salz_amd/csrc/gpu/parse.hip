@@ -902,21 +902,71 @@ __global__ __launch_bounds__(kT) void k_lazy_rewrite(ExitBits eb, const uint32_t
     const uint32_t shift = dsum[cc], lc = Lcur[cc];
     if (c >= nchunks || uni[cc])
         return;
+    const size_t s0 = (t << (klog + 6)) | ((size_t)(g * kRows) << 6) | lane;
+    if (spos(s0, klog) > n)
+        return;
+    // k_cost_rest's shape: every row's loads first (rows past n repeat row 0), an exit node's own
+    // slot standing in for its exit, and one index / pre-pass cost load per distinct exit when the
+    // wave's rows have few
+    size_t sr[kRows];
+    uint64_t v[kRows], mw[kRows];
+    uint32_t old[kRows];
+#pragma unroll
     for (uint32_t r = 0; r < kRows; r++) {
-        const size_t s = (t << (klog + 6)) | ((size_t)(g * kRows + r) << 6) | lane;
-        if (spos(s, klog) > n)
-            break;
-        // Branch-free, every load of the row unconditional (an exit node's own slot stands in for
-        // its exit, and its in-chunk part is masked off arithmetically).
-        const uint32_t old = C[s] + lc;
-        const uint64_t v = pst[s];
-        const uint32_t xm = (uint32_t)(eb.mask[s >> 6] >> lane) & 1u;  // an exit node: its path sum
-        const size_t se = xm ? s : sidx((uint32_t)v, klog);
-        const uint32_t xe = bits_index(eb.mask, eb.wpre, se);
-        const uint32_t jv = js[xe], cv = ce[xe];
-        const uint32_t cost = jv + (((uint32_t)(v >> 32) + shift - cv) & (xm - 1u));
-        D[s] = cost - old;
-        C[s] = cost;
+        const size_t sq = s0 | ((size_t)r << 6);
+        sr[r] = spos(sq, klog) <= n ? sq : s0;
+        old[r] = C[sr[r]] + lc;
+        v[r] = pst[sr[r]];
+        mw[r] = eb.mask[sr[r] >> 6];
+    }
+    uint32_t se[kRows];
+    bool isx[kRows];
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; r++) {
+        isx[r] = (mw[r] >> lane) & 1u;
+        se[r] = isx[r] ? (uint32_t)sr[r] : (uint32_t)sidx((uint32_t)v[r], klog);
+    }
+    uint32_t eA = se[kRows - 1], eB = eA, xr = kRows, nx = 0;
+#pragma unroll
+    for (uint32_t r = kRows; r-- > 0;) {
+        eA = isx[r] ? eA : se[r];
+        xr = isx[r] ? r : xr;
+        nx += isx[r] ? 1u : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = kRows; r-- > 0;)
+        eB = !isx[r] && se[r] != eA ? se[r] : eB;
+    bool few = nx <= 1u;
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; r++)
+        few = few && (isx[r] || se[r] == eA || se[r] == eB);
+    uint32_t out[kRows];
+    if (wave_ballot(!few) == 0) {
+        const uint32_t xs = (uint32_t)sr[xr < kRows ? xr : 0u];
+        const uint32_t xA = bits_index(eb.mask, eb.wpre, eA), xB = bits_index(eb.mask, eb.wpre, eB);
+        const uint32_t xX = bits_index(eb.mask, eb.wpre, xs);
+        const uint32_t jA = js[xA], jB = js[xB], jX = js[xX], cA = ce[xA], cB = ce[xB];
+#pragma unroll
+        for (uint32_t r = 0; r < kRows; r++) {
+            const bool a = se[r] == eA;
+            const uint32_t part = (uint32_t)(v[r] >> 32) + shift - (a ? cA : cB);
+            out[r] = isx[r] ? jX : (a ? jA : jB) + part;
+        }
+    } else {
+        uint32_t xe[kRows];
+#pragma unroll
+        for (uint32_t r = 0; r < kRows; r++)
+            xe[r] = bits_index(eb.mask, eb.wpre, se[r]);
+#pragma unroll
+        for (uint32_t r = 0; r < kRows; r++) {
+            const uint32_t jv = js[xe[r]], cv = ce[xe[r]];
+            out[r] = jv + (((uint32_t)(v[r] >> 32) + shift - cv) & (isx[r] ? 0u : 0xffffffffu));
+        }
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kRows; r++) {
+        D[sr[r]] = out[r] - old[r];
+        C[sr[r]] = out[r];
     }
 }
 
