@@ -89,6 +89,8 @@ lib.salz_gpu_encode_batch_device.argtypes = [ctypes.c_void_p, _u8p, _sz, _sz, _u
 lib.salz_gpu_encode_batch_device.restype = ctypes.c_int
 lib.salz_debug_init_order.argtypes = [_sz, _sz, ctypes.c_void_p]
 lib.salz_debug_init_order.restype = ctypes.c_int
+lib.salz_debug_radix_selftest.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_uint64]
+lib.salz_debug_radix_selftest.restype = ctypes.c_long
 lib.salz_encode_blocks.argtypes = [_u8p, _sz, _sz, _u8p, _szp, ctypes.c_int]
 lib.salz_encode_blocks.restype = ctypes.c_int
 lib.salz_blocks_len_max.argtypes = [_sz, _sz]
@@ -159,6 +161,13 @@ def _ptr(a: np.ndarray) -> int:
 
 def last_error() -> str:
     return lib.salz_gpu_last_error().decode(errors="replace")
+
+
+def radix_selftest(m: int, bits: int, iters: int = 2, seed: int = 1, device: int = 0) -> int:
+    """Test hook: the suffix sorter's LSD radix sort on m random (key, index) pairs of `bits` key
+    bits, on the device; returns the number of runs whose output was out of order, unstable or
+    not a permutation of the input (-1: allocation failed)."""
+    return lib.salz_debug_radix_selftest(device, m, bits, iters, seed)
 
 
 def encoded_len_max(plain_len: int) -> int:

@@ -538,3 +538,14 @@ def test_cli_multi_batch_ring_and_exact_multiple(salz, tmp_path):
     r = subprocess.run([cli, "-5", "-k", "-q", str(g)], timeout=300)
     assert r.returncode != 0
     assert not (tmp_path / "exact.txt.salz").exists()
+
+
+@pytest.mark.parametrize("m,bits", [(1, 64), (4095, 17), (4097, 64), (13 * 4096 + 5, 40), (100_003, 63),
+                                    (4096 * 4096, 24), (4096 * 4096 + 1, 64), (8192 * 4096 + 3000, 33),
+                                    (24576 * 4096 + 4097, 40)])
+def test_radix_sort_selftest(salz, m, bits):
+    """The LSD radix sort (radix.hip) on random keys, and on keys with few distinct values for
+    stability: sorted, stable and a permutation of its input, at tile counts that are and are not
+    multiples of the 8 XCDs (the scatter's XCD-contiguous tile order) and across the row scan's
+    shapes (256-thread rows up to 4096 tiles, 512 up to 8192, 1024 beyond, looping past 24576)."""
+    assert salz.radix_selftest(m, bits, iters=2, seed=7) == 0
