@@ -1125,8 +1125,9 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         (void)cur;
         uint8_t *chold = choice[0], *chnew = choice[0];
         // From the third pass on, waves of chunks whose decisions would repeat skip the pass,
-        // and a pass with no dirty wave left is not run at all: the previous decisions are the
-        // fixed point and cin their exact costs (k_parse_mark, DESIGN.md "Parse"). The test
+        // and a pass with no dirty wave left walks no chunk (every wave clean) and ends the loop
+        // at its host read: the previous decisions are the fixed point and cin their exact costs
+        // (k_parse_mark, DESIGN.md "Parse"). The test
         // costs about a third of a pass. A large block's pass is latency-bound (its duration is
         // one lane's walk, however few waves run), so there it pays only as the stopping test:
         // before the third pass when the second changed few decisions (text stops there), later
