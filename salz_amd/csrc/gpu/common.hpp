@@ -296,7 +296,11 @@ __device__ __forceinline__ uint64_t round0_key_mapped(const uint8_t *Tm, uint32_
     const uint32_t left = e - i;
     uint64_t key = 0;
     if (a.k == 8 || a.k == 9) {  // the usual text cases: straight-line, so the loads of a thread's items batch
-        uint64_t w = load_u64_any(Tm, i);
+        // the two aligned words holding Tm[i, i + 8): the second also holds Tm[i + 8]
+        const uint64_t *wp = reinterpret_cast<const uint64_t *>(Tm + ((size_t)i & ~(size_t)7));
+        const unsigned sh = (unsigned)(i & 7u) * 8u;
+        const uint64_t w0 = wp[0], w1 = wp[1];
+        uint64_t w = (w0 >> sh) | ((w1 << 1) << (63u - sh));
         if (left < 8)
             w &= (1ull << (8u * left)) - 1ull;
         // 8 symbols of `bits` bits (first symbol most significant), packed pairwise: byte pairs,
@@ -307,7 +311,7 @@ __device__ __forceinline__ uint64_t round0_key_mapped(const uint8_t *Tm, uint32_
         x = (x & 0x0000FFFF0000FFFFull) | (((x >> 16) & 0x0000FFFF0000FFFFull) << (2 * b));
         x = (x & 0xFFFFFFFFull) | ((x >> 32) << (4 * b));
         if (a.k == 9) {  // a ninth symbol (7-bit alphabets: 63 bits), zero past the end
-            const uint32_t s9 = Tm[(size_t)i + 8];  // (unconditional: the buffer is padded)
+            const uint32_t s9 = (uint32_t)(w1 >> sh) & 255u;  // Tm[i + 8]
             x = (x << b) | (left > 8 ? s9 : 0u);
         }
         return x;
