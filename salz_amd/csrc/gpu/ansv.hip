@@ -34,6 +34,7 @@ constexpr int kT = 256;
 constexpr uint32_t kB = 2048;  // leaves per workgroup block
 constexpr uint32_t kInf = 0xffffffffu;
 constexpr uint32_t kNear = 16;  // linear neighbour scan before the tree walk
+constexpr uint32_t kScan = 8;   // leaves under the deepest global tree node (scanned by the global walk)
 constexpr uint32_t kWQ = 1408;  // LDS walk-queue entries per block
 constexpr uint32_t kShards = 16;      // global-queue shards (blockIdx mod kShards)
 constexpr size_t kQCountWord = 800;   // u32 index into Workspace::dscal: 2 * kShards counters
@@ -189,13 +190,18 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     // wave, the top two by one thread: two barriers instead of one per level.
     static_assert(kB == 8 * kT, "8 leaves per thread");
     const uint32_t root = np2 / kB + blockIdx.x;
+    // Only the nodes over >= kScan leaves go to the global heap (k < 2 kB / kScan): the global
+    // walks scan a node's kScan leaves from the suffix array and LCP arrays instead of descending
+    // the last levels, so three quarters of the tree writes are saved.
     auto put = [&](uint32_t k, uint32_t a, uint32_t c) {
         vsa[k] = a;
         vlc[k] = c;
-        const uint32_t lev = 31u - __builtin_clz(k);
-        const uint32_t g = (root << lev) + (k - (1u << lev));
-        tsa[g] = a;
-        tlcp[g] = c;
+        if (k < 2 * kB / kScan) {
+            const uint32_t lev = 31u - __builtin_clz(k);
+            const uint32_t g = (root << lev) + (k - (1u << lev));
+            tsa[g] = a;
+            tlcp[g] = c;
+        }
     };
     uint32_t a[8], c[8];
     {
@@ -443,12 +449,13 @@ __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
     uint32_t lm = qlen[e];
     const uint32_t v = t.sa[r];
     uint32_t node = t.np2 / kB + r / kB, hit = kInf;
+    const uint32_t low = t.np2 / kScan;  // nodes over kScan leaves: [low, 2 low)
     while (node > 1) {
         bool side = nsv ? !(node & 1u) : (node & 1u);
         if (side) {
             uint32_t s = nsv ? node + 1 : node - 1;
             if (t.vmin(s) < v) {
-                while (s < t.np2) {
+                while (s < low) {
                     uint32_t near = nsv ? 2 * s : 2 * s + 1;  // child adjacent to the query
                     if (t.vmin(near) < v) {
                         s = near;
@@ -457,9 +464,31 @@ __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
                         s = nsv ? 2 * s + 1 : 2 * s;
                     }
                 }
-                if (nsv)
-                    lm = umin(lm, t.lmin(s));
-                hit = s - t.np2;
+                // the node's kScan leaves, from the query's side: PSV takes the last leaf with a
+                // smaller suffix (LCP minimum over the leaves after it), NSV the first (the
+                // minimum up to and including it)
+                const uint32_t r0 = (s - low) * kScan;
+                uint32_t sv[kScan], lv[kScan];
+#pragma unroll
+                for (uint32_t k = 0; k < kScan; k++) {  // (leaves past n: +inf, like vmin / lmin)
+                    const uint32_t rk = r0 + k, rc = rk < t.n ? rk : 0u;
+                    const uint32_t a = t.sa[rc], c = t.lcp[rc];
+                    sv[k] = rk < t.n ? a : kInf;
+                    lv[k] = rk < t.n ? c : kInf;
+                }
+                uint32_t h = kInf, m = lm;
+#pragma unroll
+                for (uint32_t k = 0; k < kScan; k++) {
+                    const uint32_t q = nsv ? k : kScan - 1u - k;
+                    const bool live = h == kInf;
+                    if (nsv)
+                        m = live ? umin(m, lv[q]) : m;
+                    h = live && sv[q] < v ? r0 + q : h;
+                    if (!nsv)
+                        m = h == kInf ? umin(m, lv[q]) : m;
+                }
+                lm = m;
+                hit = h;
                 break;
             }
             lm = umin(lm, t.lmin(s));
