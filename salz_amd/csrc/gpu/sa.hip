@@ -1250,6 +1250,9 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // 0 / 8 / 16 / 32 / 64 / 128 / 256 / 2048; mixed 100 MB 27.2 (0) -> 25.7 ms (64-256)
     // (profiles/r04n_tiny_sweep.txt)
     const uint32_t seg_tiny = (uint32_t)env_num("SALZ_SA", "tiny", 128);
+    // the text round counts groups of up to 256 (C2 SA 20.02 -> 19.89 ms, enwik9-sized blocks
+    // 12.2 -> 12.0 ms; the rank rounds of mixed data are faster at 128: profiles/r04w_c3_ab.txt)
+    const uint32_t seg_tiny_text = (uint32_t)env_num("SALZ_SA", "tiny", 256);
     // The text round's LDS passes sort (group, top key bits) to 48 bits (6 passes) and leave the
     // rarer ties to k_seg_text_fix: C2 SA 20.29 -> 20.18 ms against 40 bits (5 passes), 52 bits
     // (7 passes) 20.28 (profiles/r04w_c3_ab.txt).
@@ -1288,7 +1291,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             uint32_t *need = reinterpret_cast<uint32_t *>(ws.pst + (size_t)nwin * (kSegCap / 64));
             SALZ_HIP(hipMemsetAsync(need, 0, sizeof(uint32_t) * nwin, st));
             hipLaunchKernelGGL(k_seg_sort<true>, dim3(nwin), dim3(kSegThreads), 0, st, K, V, gin, plan, tab.ginfo,
-                               m, tbits, seg_tiny, rb, need, derr, lsd_bits);
+                               m, tbits, seg_tiny_text, rb, need, derr, lsd_bits);
             SALZ_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_seg_text_fix, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, rb, need);
             SALZ_LAUNCH_CHECK();
