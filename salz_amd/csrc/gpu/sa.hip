@@ -636,9 +636,25 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_sort(uint64_t *__restrict__
     const int kr = TEXT ? (kb < lsd_bits - gbits ? kb : lsd_bits - gbits) : kb;  // key bits in the LSD key
     if (tid == 0)
         nbig = 0;
-    for (uint32_t i = tid; i < count; i += kSegThreads) {
-        sk[i] = K[lo + i];
-        sv[i] = V[lo + i];
+    // the window into LDS: every load issued before the first is used (clamped, unconditional),
+    // one memory latency instead of one per 256 entries
+    {
+        uint64_t wk[kPer];
+        uint32_t wv[kPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j++) {
+            const uint32_t i = tid + j * kSegThreads, ii = i < count ? i : 0u;
+            wk[j] = K[lo + ii];
+            wv[j] = V[lo + ii];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j++) {
+            const uint32_t i = tid + j * kSegThreads;
+            if (i < count) {
+                sk[i] = wk[j];
+                sv[i] = wv[j];
+            }
+        }
     }
     __syncthreads();
     // counted groups: placed now; the larger groups' members: their LSD keys, collected
@@ -980,9 +996,23 @@ __global__ __launch_bounds__(kSegThreads) void k_seg_text_fix(uint64_t *__restri
     const uint32_t nwords = (count + 63u) >> 6;
     if (tid == 0)
         nlong = 0;
-    for (uint32_t i = tid; i < count; i += kSegThreads) {
-        sk[i] = K[lo + i];
-        sv[i] = V[lo + i];
+    {  // (every load issued before the first is used, as in k_seg_sort)
+        uint64_t wk[kPer];
+        uint32_t wv[kPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j++) {
+            const uint32_t i = tid + j * kSegThreads, ii = i < count ? i : 0u;
+            wk[j] = K[lo + ii];
+            wv[j] = V[lo + ii];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; j++) {
+            const uint32_t i = tid + j * kSegThreads;
+            if (i < count) {
+                sk[i] = wk[j];
+                sv[i] = wv[j];
+            }
+        }
     }
     for (uint32_t q = tid; q < nwords; q += kSegThreads)
         runb[q] = rb[(size_t)w * (kSegCap / 64) + q];
