@@ -132,46 +132,60 @@ __global__ void k_alpha_presence(const uint8_t *__restrict__ T, size_t P, uint32
 }
 
 // Repetition probe (one workgroup): fingerprints of the 32 bytes at 4096 evenly spaced
-// positions, sorted in LDS; out = how many samples share their fingerprint with another. A
-// Fibonacci or periodic block repeats every 32-gram (all samples collide), text almost never.
+// positions, counted in an LDS hash table; out = how many samples share their fingerprint with
+// another. A Fibonacci or periodic block repeats every 32-gram (all samples collide), text almost
+// never. (A bitonic sort of the 4096 fingerprints took 78 barriers: ~70 us per block; the table
+// takes one insert per sample.)
 constexpr uint32_t kProbe = 4096;
 constexpr uint32_t kProbeThreads = 1024;
+constexpr uint32_t kProbeSlots = 16384;  // open addressing, 1/4 full
 __global__ __launch_bounds__(kProbeThreads) void k_repeat_probe(const uint8_t *__restrict__ T, uint32_t n,
                                                                 uint32_t *__restrict__ out)
 {
-    __shared__ uint64_t k[kProbe];
+    __shared__ uint32_t key[kProbeSlots];  // the upper half of a fingerprint, | 1 (0 = empty)
+    __shared__ uint32_t cnt[kProbeSlots];
     __shared__ uint32_t dups;
+    constexpr uint32_t kPerT = kProbe / kProbeThreads;
     const uint32_t tid = threadIdx.x;
     if (tid == 0)
         dups = 0;
-    for (uint32_t s = tid; s < kProbe; s += kProbeThreads) {
-        const size_t p = (size_t)s * (n - 32u) / kProbe;
+    for (uint32_t i = tid; i < kProbeSlots; i += kProbeThreads) {
+        key[i] = 0;
+        cnt[i] = 0;
+    }
+    uint64_t w[kPerT][4];  // every sample's loads issued first
+#pragma unroll
+    for (uint32_t j = 0; j < kPerT; j++) {
+        const size_t p = (size_t)(tid + j * kProbeThreads) * (n - 32u) / kProbe;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            w[j][q] = load_u64_any(T, p + 8u * q);
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kPerT; j++) {
         uint64_t h = 0x9E3779B97F4A7C15ull;
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
-            h ^= load_u64_any(T, p + 8u * w);
+        for (int q = 0; q < 4; q++) {
+            h ^= w[j][q];
             h *= 0xBF58476D1CE4E5B9ull;
             h ^= h >> 31;
         }
-        k[s] = h;
+        const uint32_t fp = (uint32_t)(h >> 32) | 1u;
+        uint32_t slot = (uint32_t)h & (kProbeSlots - 1u);
+        for (uint32_t probe = 0; probe < kProbeSlots; probe++) {  // (the table never fills)
+            const uint32_t old = atomicCAS(&key[slot], 0u, fp);
+            if (old == 0u || old == fp) {
+                atomicAdd(&cnt[slot], 1u);
+                break;
+            }
+            slot = (slot + 1u) & (kProbeSlots - 1u);
+        }
     }
     __syncthreads();
-    for (uint32_t size = 2; size <= kProbe; size <<= 1)  // bitonic sort
-        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-            for (uint32_t t = tid; t < kProbe / 2; t += kProbeThreads) {
-                const uint32_t i = 2 * t - (t & (stride - 1)), j = i + stride;
-                const bool up = (i & size) == 0;
-                const uint64_t a = k[i], b = k[j];
-                if ((a > b) == up) {
-                    k[i] = b;
-                    k[j] = a;
-                }
-            }
-            __syncthreads();
-        }
     uint32_t d = 0;
-    for (uint32_t s = tid; s < kProbe; s += kProbeThreads)
-        d += (s > 0 && k[s - 1] == k[s]) || (s + 1 < kProbe && k[s + 1] == k[s]);
+    for (uint32_t i = tid; i < kProbeSlots; i += kProbeThreads)
+        d += cnt[i] >= 2u ? cnt[i] : 0u;
     atomicAdd(&dups, d);
     __syncthreads();
     if (tid == 0)
