@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
     const uint8_t *chold, uint8_t *chnew, uint32_t n, Blocks bl, uint32_t klog,
     uint32_t *__restrict__ changed, uint32_t *err, uint8_t *__restrict__ eflag,
     const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum, uint32_t *__restrict__ reach,
-    uint32_t *__restrict__ rlo, Lazy lz)
+    uint32_t *__restrict__ rlo, Lazy lz, int first)
 {
     constexpr uint32_t kDepth = DEP, kCDepth = CDEP;
     static_assert(kDepth <= kWin && kCDepth >= kDepth && ((kCDepth + 1) % kDepth) == 0, "ring depths");
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             const uint64_t stp = live ? ((uint64_t)best << 32) | ex : (uint64_t)n;
             pst[slot(j)] = stp;
             chnew[slot(j)] = ch;
-            diff += live && ch != orr[0];
+            diff += live && (first || ch != orr[0]);  // (the first pass has no old choices)
             // Exit set E (every position's exit; consecutive positions mostly share one). The
             // store is issued every step, as a store under a narrower EXEC mask would leave
             // partial vmcnt waits depending on whether it ran (tests/test_codegen.py); a lane
@@ -1106,7 +1106,8 @@ int stage_parse(Workspace &ws, const Blocks &bl)
 
     hipLaunchKernelGGL(k_cost_seed, dim3(grid_for(S, kT)), dim3(kT), 0, st, cost[0], bl, klog, S);
     SALZ_LAUNCH_CHECK();
-    SALZ_HIP(hipMemsetAsync(choice[0], 0xff, S, st));
+    // (no choice array init: the first pass writes every slot's choice and counts every live
+    // position as changed)
     // counters changed (48), ndirty (50), listed chunks (51): zeroed here, then by the scalar reads
     // that consume them
     SALZ_HIP(hipMemsetAsync(changed, 0, 16, st));
@@ -1205,11 +1206,11 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         if (pack && it > 0)
             hipLaunchKernelGGL(k_parse_chunk<CandPacked>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, cand8,
                                nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr, eflag, wd, dsum, rch,
-                               rlo, lzw);
+                               rlo, lzw, it == 0 ? 1 : 0);
         else
             hipLaunchKernelGGL(k_parse_chunk<CandFull>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
                                it == 0 ? cand8 : nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr,
-                               eflag, wd, dsum, rch, rlo, lzw);
+                               eflag, wd, dsum, rch, rlo, lzw, it == 0 ? 1 : 0);
         SALZ_LAUNCH_CHECK();
         // The exit set of the new decisions (E was marked by the chunk pass) as bits and word
         // counts, numbered by the scan, before the pass's one host read: that read then returns
