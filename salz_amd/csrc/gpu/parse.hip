@@ -796,39 +796,31 @@ __global__ __launch_bounds__(kT) void k_cost_rest(ExitBits eb, const uint32_t *_
         se[r] = isx[r] ? (uint32_t)sr[r] : (uint32_t)sidx((uint32_t)v[r], klog);
     }
     // The rows of a thread are consecutive positions of one chunk, whose paths mostly leave it
-    // through the same exit: when every lane's rows have at most two distinct exits and at most
-    // one row that is an exit node itself (a wave-uniform test), the exits' index and cost loads
-    // are issued once per distinct exit (5 scattered loads and one per exit row) instead of per
-    // row (the kernel's time was the address processing of 32 scattered loads per thread).
-    uint32_t eA = se[kRows - 1], eB = eA, xr = kRows;  // (row kRows - 1 when every row is an exit)
-    uint32_t nx = 0;
+    // through the same exit: a row's cost comes from the node at its key slot se (its exit, or
+    // itself when it is an exit node), and when every lane's rows have at most three distinct key
+    // slots (a wave-uniform test) their index and cost loads are issued once per distinct slot
+    // (12 scattered loads instead of 32: the kernel's time was the address processing of the
+    // scattered loads).
+    uint32_t kA = se[0], kB = kA, kC = kA;
 #pragma unroll
-    for (uint32_t r = kRows; r-- > 0;) {
-        eA = isx[r] ? eA : se[r];  // the first non-exit row's exit
-        xr = isx[r] ? r : xr;
-        nx += isx[r] ? 1u : 0u;
+    for (uint32_t r = 1; r < kRows; r++) {
+        kB = kB == kA && se[r] != kA ? se[r] : kB;
+        kC = kC == kA && se[r] != kA && se[r] != kB ? se[r] : kC;
     }
-#pragma unroll
-    for (uint32_t r = kRows; r-- > 0;)
-        eB = !isx[r] && se[r] != eA ? se[r] : eB;
-    bool few = nx <= 1u;
+    bool few = true;
 #pragma unroll
     for (uint32_t r = 0; r < kRows; r++)
-        few = few && (isx[r] || se[r] == eA || se[r] == eB);
+        few = few && (se[r] == kA || se[r] == kB || se[r] == kC);
     uint32_t out[kRows];
     if (wave_ballot(!few) == 0) {
-        const uint32_t xs = (uint32_t)sr[xr < kRows ? xr : 0u];
-        const uint64_t mA = eb.mask[eA >> 6], mB = eb.mask[eB >> 6], mX = eb.mask[xs >> 6];
-        const uint32_t pA = eb.wpre[eA >> 6], pB = eb.wpre[eB >> 6], pX = eb.wpre[xs >> 6];
-        const uint32_t xA = pA + (uint32_t)__popcll(mA & ((1ull << (eA & 63u)) - 1ull));
-        const uint32_t xB = pB + (uint32_t)__popcll(mB & ((1ull << (eB & 63u)) - 1ull));
-        const uint32_t xX = pX + (uint32_t)__popcll(mX & ((1ull << (xs & 63u)) - 1ull));
-        const uint32_t jA = js[xA], jB = js[xB], jX = js[xX], cA = cin[eA], cB = cin[eB];
+        const uint32_t xA = bits_index(eb.mask, eb.wpre, kA), xB = bits_index(eb.mask, eb.wpre, kB);
+        const uint32_t xC = bits_index(eb.mask, eb.wpre, kC);
+        const uint32_t jA = js[xA], jB = js[xB], jC = js[xC], cA = cin[kA], cB = cin[kB], cC = cin[kC];
 #pragma unroll
         for (uint32_t r = 0; r < kRows; r++) {
-            const bool a = se[r] == eA;
-            const uint32_t part = (uint32_t)(v[r] >> 32) + shift - (a ? cA : cB);
-            out[r] = isx[r] ? jX : (a ? jA : jB) + part;
+            const bool a = se[r] == kA, b = se[r] == kB;
+            const uint32_t jv = a ? jA : b ? jB : jC, cv = a ? cA : b ? cB : cC;
+            out[r] = jv + (((uint32_t)(v[r] >> 32) + shift - cv) & (isx[r] ? 0u : 0xffffffffu));
         }
     } else {
         uint32_t xe[kRows];
@@ -926,31 +918,26 @@ __global__ __launch_bounds__(kT) void k_lazy_rewrite(ExitBits eb, const uint32_t
         isx[r] = (mw[r] >> lane) & 1u;
         se[r] = isx[r] ? (uint32_t)sr[r] : (uint32_t)sidx((uint32_t)v[r], klog);
     }
-    uint32_t eA = se[kRows - 1], eB = eA, xr = kRows, nx = 0;
+    uint32_t kA = se[0], kB = kA, kC = kA;  // (k_cost_rest's distinct key slots)
 #pragma unroll
-    for (uint32_t r = kRows; r-- > 0;) {
-        eA = isx[r] ? eA : se[r];
-        xr = isx[r] ? r : xr;
-        nx += isx[r] ? 1u : 0u;
+    for (uint32_t r = 1; r < kRows; r++) {
+        kB = kB == kA && se[r] != kA ? se[r] : kB;
+        kC = kC == kA && se[r] != kA && se[r] != kB ? se[r] : kC;
     }
-#pragma unroll
-    for (uint32_t r = kRows; r-- > 0;)
-        eB = !isx[r] && se[r] != eA ? se[r] : eB;
-    bool few = nx <= 1u;
+    bool few = true;
 #pragma unroll
     for (uint32_t r = 0; r < kRows; r++)
-        few = few && (isx[r] || se[r] == eA || se[r] == eB);
+        few = few && (se[r] == kA || se[r] == kB || se[r] == kC);
     uint32_t out[kRows];
     if (wave_ballot(!few) == 0) {
-        const uint32_t xs = (uint32_t)sr[xr < kRows ? xr : 0u];
-        const uint32_t xA = bits_index(eb.mask, eb.wpre, eA), xB = bits_index(eb.mask, eb.wpre, eB);
-        const uint32_t xX = bits_index(eb.mask, eb.wpre, xs);
-        const uint32_t jA = js[xA], jB = js[xB], jX = js[xX], cA = ce[xA], cB = ce[xB];
+        const uint32_t xA = bits_index(eb.mask, eb.wpre, kA), xB = bits_index(eb.mask, eb.wpre, kB);
+        const uint32_t xC = bits_index(eb.mask, eb.wpre, kC);
+        const uint32_t jA = js[xA], jB = js[xB], jC = js[xC], cA = ce[xA], cB = ce[xB], cC = ce[xC];
 #pragma unroll
         for (uint32_t r = 0; r < kRows; r++) {
-            const bool a = se[r] == eA;
-            const uint32_t part = (uint32_t)(v[r] >> 32) + shift - (a ? cA : cB);
-            out[r] = isx[r] ? jX : (a ? jA : jB) + part;
+            const bool a = se[r] == kA, b = se[r] == kB;
+            const uint32_t jv = a ? jA : b ? jB : jC, cv = a ? cA : b ? cB : cC;
+            out[r] = jv + (((uint32_t)(v[r] >> 32) + shift - cv) & (isx[r] ? 0u : 0xffffffffu));
         }
     } else {
         uint32_t xe[kRows];
