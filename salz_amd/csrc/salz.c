@@ -53,7 +53,9 @@ size_t vnibble_size(uint32_t val)
 size_t encode_vnibble_le(uint32_t val, uint64_t *res)
 {
     /* k octal digits of val - S_{k-1}, most significant in the highest nibble, terminator
-     * bit 0x8 on the lowest nibble. Bytes beyond the k nibbles are left zero. */
+     * bit 0x8 on the lowest nibble. Like the reference, only the ceil(k / 2) bytes that hold
+     * the k nibbles are stored (the last one's high nibble zero when k is odd); the bytes of
+     * *res beyond them are left as the caller had them. */
     size_t k = vnibble_size(val);
     uint64_t s = 0, p = 8;
     for (size_t j = 1; j < k; j++) {
@@ -63,7 +65,7 @@ size_t encode_vnibble_le(uint32_t val, uint64_t *res)
     uint64_t d = (uint64_t)val - s, r = 0;
     for (size_t j = 0; j < k; j++)
         r |= (((d >> (3 * j)) & 7u) | (j == 0 ? 8u : 0u)) << (4 * j);
-    *res = r;
+    memcpy(res, &r, (k + 1) / 2); /* little-endian: nibble j in byte j / 2 */
     return k;
 }
 

@@ -55,7 +55,9 @@ def test_encoded_len_max_formula():
 
 def test_vnibble_closed_form_matches_reference_restatement():
     """encode_vnibble_le / vnibble_size (lib/salz.c:352-445, :565-588): the product's
-    closed form equals the oracle's byte-packing restatement (low 4k bits)."""
+    closed form equals the oracle's byte-packing restatement (low 4k bits), and like the
+    reference it stores only the ceil(k / 2) bytes that hold the nibbles (:354-444): the bytes
+    of *res beyond them keep what the caller had there."""
     import salz_amd
 
     o = oracle()
@@ -64,8 +66,12 @@ def test_vnibble_closed_form_matches_reference_restatement():
     vals = list(range(0, 70000)) + [int(x) for x in rng.integers(0, 2**32, 20000, dtype=np.uint64)]
     vals += [8, 72, 584, 4680, 37448, 299592, 2396744, 19173960, 153391688, 1227133512]
     vals += [v - 1 for v in vals[-10:]] + [0xFFFFFFFF]
+    fill = 0xA5A5A5A5A5A5A5A5
     for v in vals:
+        a.value = fill
         k1 = salz_amd.lib.encode_vnibble_le(v, ctypes.byref(a))
+        nb = (k1 + 1) // 2
+        assert a.value >> (8 * nb) == fill >> (8 * nb), v
         k2 = o.oracle_encode_vnibble_le(v, ctypes.byref(b))
         assert k1 == k2 == salz_amd.lib.vnibble_size(v) == o.oracle_vnibble_size(v)
         m = (1 << (4 * k1)) - 1
