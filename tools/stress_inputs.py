@@ -24,6 +24,10 @@ cases = {
     "random": lambda: gen("smx", n, 3, 256),
     "binary2": lambda: gen("smx", n, 5, 2),
     "fib": lambda: gen("fib", n),
+    "sawtooth": lambda: np.resize(np.arange(256, dtype=np.uint8), n),
+    "halves": lambda: np.resize(gen("text", n // 2 + 1, 11), n),  # one repeat at distance n/2
+    "runs": lambda: np.repeat(gen("smx", n // 64 + 1, 13, 256), 64)[:n],
+    "mixed": lambda: gen("mixed", n, 17),
 }
 ctx = salz_amd.Context(0, n)
 for name, make in cases.items():
