@@ -6,6 +6,9 @@
 //
 // Every kernel: one query per thread, indices from a precomputed random array (read
 // coalesced), results written coalesced, so the random side is the only random traffic.
+// The "xcd" lines draw each workgroup's indices from the eighth of the table that belongs to
+// its XCD (workgroups are dealt to the 8 XCDs round-robin), so a table of up to 32 MiB keeps
+// every XCD's part inside its own 4 MB L2.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -32,6 +35,30 @@ __global__ void k_init_idx(uint32_t *idx, size_t m, uint32_t n, uint64_t seed)
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     z ^= z >> 31;
     idx[i] = (uint32_t)(z % n);
+}
+
+// indices in the XCD's eighth of the table: workgroup b runs on XCD b mod 8
+__global__ void k_init_idx_xcd(uint32_t *idx, size_t m, uint32_t n, uint64_t seed)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m)
+        return;
+    uint64_t z = seed + i * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    const uint32_t part = n / 8u;
+    idx[i] = (uint32_t)(blockIdx.x & 7u) * part + (uint32_t)(z % part);
+}
+
+// 16-byte records (the candidate array's entries) at 16-byte slots of the table
+__global__ void k_scatter16(uint4 *__restrict__ tab, const uint32_t *__restrict__ idx, size_t m)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= m)
+        return;
+    const uint32_t v = (uint32_t)i;
+    tab[idx[i]] = make_uint4(v, v + 1u, v + 2u, v + 3u);
 }
 
 template <int F>
@@ -132,6 +159,13 @@ int main(int argc, char **argv)
     k_init_idx<<<g, b>>>(idx, m, n4, 777);
     timeit("gather8 bytes plain", [&] { k_gather8<0><<<g, b>>>(reinterpret_cast<uint8_t *>(tab), idx, m, out8); });
     timeit("gather8 bytes nontemporal", [&] { k_gather8<1><<<g, b>>>(reinterpret_cast<uint8_t *>(tab), idx, m, out8); });
+    k_init_idx_xcd<<<g, b>>>(idx, m, n4, 4242);
+    timeit("gather4 plain xcd", [&] { k_gather4<0><<<g, b>>>(tab, idx, m, out); });
+    timeit("scatter4 plain xcd", [&] { k_scatter4<0><<<g, b>>>(tab, idx, m); });
+    k_init_idx<<<g, b>>>(idx, m, n4 / 4u, 99);
+    timeit("scatter16 plain", [&] { k_scatter16<<<g, b>>>(reinterpret_cast<uint4 *>(tab), idx, m); });
+    k_init_idx_xcd<<<g, b>>>(idx, m, n4 / 4u, 98);
+    timeit("scatter16 plain xcd", [&] { k_scatter16<<<g, b>>>(reinterpret_cast<uint4 *>(tab), idx, m); });
     CK(hipDeviceSynchronize());
     return 0;
 }
