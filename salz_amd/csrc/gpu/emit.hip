@@ -266,7 +266,7 @@ struct BlockOut {
 // count), and the whole batch has arrived before any is used, so the stores of one batch (under
 // the branches' masks) are never separated by a partial vmcnt wait from the next batch's loads
 // ("Concurrent encodes and the unaligned text load"; tests/test_codegen.py).
-constexpr uint32_t kBatch = 8;
+constexpr uint32_t kBatch = 16;
 
 __global__ void k_emit_write(const uint8_t *__restrict__ T, const uint64_t *__restrict__ tok,
                              const uint32_t *__restrict__ ntok, Blocks bl, uint32_t N_last, uint32_t chunk,
@@ -316,9 +316,10 @@ __global__ void k_emit_write(const uint8_t *__restrict__ T, const uint64_t *__re
             r[q] = tok[tok_slot(g, k < nt ? k : 0u, klog)];
         }
         // every record of the batch is an operand: one full wait after the batch's loads
-        static_assert(kBatch == 8, "operand list");
-        asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
-#pragma unroll
+        static_assert(kBatch == 16, "operand list");
+        asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]),
+                     "v"(r[8]), "v"(r[9]), "v"(r[10]), "v"(r[11]), "v"(r[12]), "v"(r[13]), "v"(r[14]), "v"(r[15]));
+        // (consumed in a loop: the unroller declines 16 bodies; the records stay in registers)
         for (uint32_t q = 0; q < kBatch; q++) {
             if (k0 + q >= nt)
                 break;
