@@ -1191,16 +1191,18 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         uint8_t *wd = skipping && skip_on ? wdirty : nullptr;
         uint32_t *rch = it == 0 && range_on ? reach : nullptr;
         const Lazy lzw{lazy ? Lv[lc] : nullptr, lazy_on ? summ : nullptr, lazy_on ? chg : nullptr};
-        // Chunks of K <= 128 (non-text and mid-size blocks) prefetch far targets 2 steps ahead
-        // instead of 4: mixed 100 MB parse 8.22 -> 8.0 ms; text at K = 512 is 0.03 ms slower so
+        // Chunks of K <= 128 (non-text and mid-size blocks) prefetch far targets 1 step and
+        // candidates 3 steps ahead instead of 4 and 7: mixed 100 MB parse 8.22 -> 7.9 ms, Silesia
+        // blocks 3.1 -> 2.9 ms (profiles/r04zi_parse_near_prefetch_ab.txt); text at K = 512 is
+        // 0.03 ms slower so
         const bool near = klog <= 7;
         if (pack && it > 0)
-            hipLaunchKernelGGL((near ? k_parse_chunk<CandPacked, 2, 7> : k_parse_chunk<CandPacked, 4, 7>),
+            hipLaunchKernelGGL((near ? k_parse_chunk<CandPacked, 1, 3> : k_parse_chunk<CandPacked, 4, 7>),
                                dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, cand8,
                                nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr, eflag, wd, dsum, rch,
                                rlo, lzw, it == 0 ? 1 : 0);
         else
-            hipLaunchKernelGGL((near ? k_parse_chunk<CandFull, 2, 7> : k_parse_chunk<CandFull, 4, 7>),
+            hipLaunchKernelGGL((near ? k_parse_chunk<CandFull, 1, 3> : k_parse_chunk<CandFull, 4, 7>),
                                dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
                                it == 0 ? cand8 : nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr,
                                eflag, wd, dsum, rch, rlo, lzw, it == 0 ? 1 : 0);
