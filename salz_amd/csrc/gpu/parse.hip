@@ -135,7 +135,7 @@ constexpr uint32_t kSummW = kSumm + 1;  // words per chunk
 // would repeat their decisions (k_parse_mark), so they only carry their choices over, and
 // their states stay valid through dsum (the uniform cost shift added since their last pass).
 // DEP / CDEP: far-target and candidate prefetch distances (8, 15 measured no faster in the late
-// passes either).
+// passes either); chunks of K <= 128 run 1 / 3 (the launch below).
 template <class C, uint32_t DEP = 4, uint32_t CDEP = 7>
 __global__ __launch_bounds__(kT) void k_parse_chunk(
     const typename C::T *__restrict__ cand, uint2 *__restrict__ pack_out, const uint32_t *__restrict__ cin,
