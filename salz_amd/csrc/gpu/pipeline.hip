@@ -590,6 +590,7 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P
     }
     if (mark(ws, EV_UP)) return -1;
     ws.sigma = 0;
+    ws.stats.sa_dc3_levels = 0;  // (a suffix array handed in says nothing about repeats)
     if (ext) {
         SALZ_HIP(hipMemcpyAsync(ws.sa, ext->sa, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
         ws.lcps_ok = ext->lcp != nullptr;
@@ -615,7 +616,13 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P
     // 3224 / 3191 -> 3570 / 3567 MB/s (profiles/r03zzz_c3text_klog_ab.txt), though one block alone
     // parses 0.4 ms slower than at K = 64: fewer chunks and exits cost less GPU time in total
     // while other slots keep the GPU busy.
-    if (nbz == 1 && !env_flag("SALZ_PARSE", "klog") && ((ws.sigma > 127 && ws.klog > 7) || (ws.klog < 7 && n > (8u << 20))))
+    // A block the suffix sort sent to DC3 (long repeats everywhere: its factors are long, so its
+    // pass count barely depends on K) parses at K = 128 as well: Fibonacci 256 MiB 5 -> 6 passes,
+    // parse 9.9 -> 7.9 ms (profiles/r04zd_klog_probe.txt; random small alphabets, which stay on
+    // prefix doubling, need twice the passes at K = 128).
+    const bool repetitive = ws.stats.sa_dc3_levels > 0;
+    if (nbz == 1 && !env_flag("SALZ_PARSE", "klog") &&
+        (((ws.sigma > 127 || repetitive) && ws.klog > 7) || (ws.klog < 7 && n > (8u << 20))))
         ws.klog = 7;
     if (guard_check(ws, "sa") || (nbz == 1 && check_stage(ws, n, 2))) return -1;
     if (mark(ws, EV_SA)) return -1;
