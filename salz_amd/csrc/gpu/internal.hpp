@@ -150,6 +150,7 @@ int scan_sum_u64(const uint64_t *in, uint64_t *out, size_t n, bool inclusive,
 // radix sort of (u64 key, u32 value) pairs on key bits [bit_lo, bit_hi) (radix.hip).
 // On return *keys / *vals point at whichever buffer holds the sorted result.
 constexpr int kRadixTile = 4096;
+constexpr int kMaxDigits = 512;  // 9-bit radix digits (radix.hip)
 // With `text` set, the first pass builds the round-0 suffix keys from the text itself (m =
 // every live suffix of `blocks`; *keys / *vals are not read); a batch of several blocks then
 // gets extra passes on the block of each value, so the result is ordered by (block, key).

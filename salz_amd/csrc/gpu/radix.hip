@@ -71,18 +71,18 @@ __device__ __forceinline__ uint64_t window_key(uint64_t w, uint32_t w9, uint32_t
 }
 
 // digit source of a pass: 0 = key bits, 1 / 3 = key bits of text-built pairs, 2 = block of value,
-// 4 = large group of value
+// 4 = large group of value (value digits are 8-bit; the caller masks key digits to its width)
 __device__ __forceinline__ unsigned digit_of(int mode, uint64_t k, uint32_t v, int shift, const TextSrc &t)
 {
     return mode == 2 ? (t.g.blk(v) >> shift) & 255u
            : mode == 4 ? (group_of(t, v) >> shift) & 255u
-                       : (unsigned)(k >> shift) & 255u;
+                       : (unsigned)(k >> shift);
 }
 constexpr int kItems = 16;
 constexpr int kTile = kThreads * kItems;
 static_assert(kTile == kRadixTile, "tile size mismatch");
 
-template <int kMode>
+template <int kMode, int DB>
 __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restrict__ keys,
                                                          const uint32_t *__restrict__ vals,
                                                          uint32_t m, int shift,
@@ -90,16 +90,20 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
                                                          uint32_t ntiles, TextSrc txt,
                                                          const uint8_t *__restrict__ dig)
 {
-    // 32 sub-histograms (8 per wave, by lane & 7), 257 words apart so the copies of one digit
-    // sit in different banks: lanes of a wave adding to a hot digit (text keys' leading bytes
-    // are skewed) spread over 8 addresses instead of serialising on one.
-    constexpr int kCopies = 32, kStride = 257;
+    (void)dig;  // (digit arrays are counted by k_radix_hist_dig)
+    // Sub-histograms (8 per wave by lane & 7 for 8-bit digits, 4 per wave by lane & 3 for 9-bit
+    // ones), ND + 1 words apart so the copies of one digit sit in different banks: lanes of a wave
+    // adding to a hot digit (text keys' leading bytes are skewed) spread over several addresses
+    // instead of serialising on one.
+    constexpr int ND = 1 << DB, kCopies = DB == 8 ? 32 : 16, kPerWave = kCopies / 4, kStride = ND + 1;
+    constexpr uint32_t kMask = ND - 1;
+    static_assert(kMode == 0 || kMode == 1 || DB == 8, "value-digit passes are 8-bit");
     __shared__ uint32_t h[kCopies * kStride];
     unsigned tid = threadIdx.x, wave = tid >> 6;
     for (int i = tid; i < kCopies * kStride; i += kThreads)
         h[i] = 0;
     __syncthreads();
-    uint32_t *mine = h + (wave * 8 + (tid & 7u)) * kStride;
+    uint32_t *mine = h + (wave * kPerWave + (tid & (kPerWave - 1u))) * kStride;
     // Two keys per 16-byte load: pair j of thread t is keys 2 (j * kThreads + t) and + 1.
     const size_t base = (size_t)blockIdx.x * kTile;
     const uint4 *kp = reinterpret_cast<const uint4 *>(keys + base);
@@ -111,11 +115,12 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
                 atomicAdd(&mine[digit_of(kMode, 0, vals[base + i], shift, txt)], 1u);
         }
     } else if (kMode == 1 && shift == 0 && (txt.a.bits == 0 || ((txt.a.k == 8 || txt.a.k == 9) && txt.a.bits >= 4))) {
-        // Round 0's first digit is its key's low byte: the 8th byte (raw keys), or the last
-        // symbol with the low bits of the one before (8 or 9 symbols of >= 4 bits): two byte
-        // loads per suffix instead of the whole key. Loads unconditional (the text is padded),
-        // past the suffix's end masked to 0 like the key's bytes.
-        const uint32_t b = txt.a.bits, kl = txt.a.bits ? txt.a.k - 1u : 7u;
+        // Round 0's first digit is its key's low 8 or 9 bits: the 8th byte (raw keys; 9-bit digits
+        // add the 7th byte's low bit), or the last symbol with the low bits of the one before (8
+        // or 9 symbols of >= 4 bits): two byte loads per suffix instead of the whole key. Loads
+        // unconditional (the text is padded), past the suffix's end masked to 0 like the key's bytes.
+        const uint32_t b = txt.a.bits ? txt.a.bits : 8u, kl = txt.a.bits ? txt.a.k - 1u : 7u;
+        const bool prev = txt.a.bits || DB > 8;  // (whether the digit takes bits of the byte before)
         uint32_t d[kItems];
         if (txt.g.nb == 1 && base >= 7 && left >= (size_t)kTile) {  // (tile-uniform)
             // One block, a whole tile past the short suffixes: entry c is suffix c - 7, so a
@@ -133,8 +138,8 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
             for (int j = 0; j < kItems; j++) {
                 const uint32_t i = i0 + (uint32_t)j;
                 const uint32_t s7 = i + kl < e ? byte_at((uint32_t)j + 1u) : 0u;
-                const uint32_t s6 = b && i + kl - 1u < e ? byte_at((uint32_t)j) : 0u;
-                d[j] = (s7 | (s6 << b)) & 255u;
+                const uint32_t s6 = prev && i + kl - 1u < e ? byte_at((uint32_t)j) : 0u;
+                d[j] = (s7 | (s6 << b)) & kMask;
             }
 #pragma unroll
             for (int j = 0; j < kItems; j++)
@@ -145,8 +150,8 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
             const size_t idx = (size_t)j * kThreads + tid;
             const uint32_t i = init_suffix(idx < left ? base + idx : 0, txt.g), e = txt.g.end(i);
             const uint32_t t7 = txt.T[(size_t)i + kl], t6 = txt.T[(size_t)i + kl - 1u];
-            const uint32_t s7 = i + kl < e ? t7 : 0u, s6 = b && i + kl - 1u < e ? t6 : 0u;
-            d[j] = (s7 | (s6 << b)) & 255u;
+            const uint32_t s7 = i + kl < e ? t7 : 0u, s6 = prev && i + kl - 1u < e ? t6 : 0u;
+            d[j] = (s7 | (s6 << b)) & kMask;
         }
 #pragma unroll
         for (int j = 0; j < kItems; j++)
@@ -164,22 +169,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
 #pragma unroll
         for (int j = 0; j < kItems; j++)
             if ((size_t)j * kThreads + tid < left)
-                atomicAdd(&mine[(unsigned)(kk[j] >> shift) & 255u], 1u);
-    } else if (dig) {
-        // this pass's digits as bytes (written by the previous scatter): 16 per thread, one
-        // 16-byte load, instead of 16 keys of 8 bytes
-        const uint8_t *d = dig + base + (size_t)tid * kItems;
-        if (left >= (size_t)kTile) {
-            const uint4 x = *reinterpret_cast<const uint4 *>(d);
-            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-            for (int j = 0; j < kItems; j++)
-                atomicAdd(&mine[(w[j >> 2] >> (8 * (j & 3))) & 255u], 1u);
-        } else {
-            for (int j = 0; j < kItems; j++)
-                if ((size_t)tid * kItems + j < left)
-                    atomicAdd(&mine[d[j]], 1u);
-        }
+                atomicAdd(&mine[(unsigned)(kk[j] >> shift) & kMask], 1u);
     } else if (left >= (size_t)kTile) {
         uint4 x[kItems / 2];
 #pragma unroll
@@ -188,55 +178,71 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
 #pragma unroll
         for (int j = 0; j < kItems / 2; j++) {
             const uint64_t k0 = (uint64_t)x[j].y << 32 | x[j].x, k1 = (uint64_t)x[j].w << 32 | x[j].z;
-            atomicAdd(&mine[(unsigned)(k0 >> shift) & 255u], 1u);
-            atomicAdd(&mine[(unsigned)(k1 >> shift) & 255u], 1u);
+            atomicAdd(&mine[(unsigned)(k0 >> shift) & kMask], 1u);
+            atomicAdd(&mine[(unsigned)(k1 >> shift) & kMask], 1u);
         }
     } else {
 #pragma unroll
         for (int j = 0; j < kItems; j++) {
             const size_t i = (size_t)j * kThreads + tid;
             if (i < left)
-                atomicAdd(&mine[(unsigned)(keys[base + i] >> shift) & 255u], 1u);
+                atomicAdd(&mine[(unsigned)(keys[base + i] >> shift) & kMask], 1u);
         }
     }
     __syncthreads();
-    uint32_t sum = 0;
+    for (uint32_t d = tid; d < (uint32_t)ND; d += kThreads) {
+        uint32_t sum = 0;
 #pragma unroll
-    for (int c = 0; c < kCopies; c++)
-        sum += h[c * kStride + tid];
-    counts[(size_t)tid * ntiles + blockIdx.x] = sum;
+        for (int c = 0; c < kCopies; c++)
+            sum += h[c * kStride + d];
+        counts[(size_t)d * ntiles + blockIdx.x] = sum;
+    }
 }
 
-// Per-tile digit counts from the digit bytes the previous scatter wrote (16 per thread, one
-// 16-byte load). The load is issued before the counters are cleared, and 16 sub-histograms
-// (4 per wave, by lane & 3; 257 words apart so one digit's copies sit in different banks) keep
-// the LDS at 16 KB: 8 workgroups per CU instead of 4 with 32 copies, and half the clearing and
-// summing per tile (k_radix_hist with 32 copies: 98 us per 100 M digits, latency-bound).
-constexpr int kDigCopies = 16, kDigStride = 257;
-__global__ __launch_bounds__(kThreads) void k_radix_hist_dig(const uint8_t *__restrict__ dig, uint32_t m,
+// Per-tile digit counts from the digits the previous scatter wrote (16 per thread: one 16-byte
+// load of bytes, or two of 16-bit digits). The loads are issued before the counters are cleared,
+// and 16 sub-histograms (4 per wave, by lane & 3; ND + 1 words apart so one digit's copies sit in
+// different banks) keep the LDS at 16 KB (8-bit digits): 8 workgroups per CU instead of 4 with 32
+// copies, and half the clearing and summing per tile (k_radix_hist with 32 copies: 98 us per
+// 100 M digits, latency-bound).
+template <typename DT, int DB>
+__global__ __launch_bounds__(kThreads) void k_radix_hist_dig(const DT *__restrict__ dig, uint32_t m,
                                                              uint32_t *__restrict__ counts, uint32_t ntiles)
 {
-    __shared__ uint32_t h[kDigCopies * kDigStride];
+    // (9-bit digits: 8 copies, 2 per wave, so that the LDS stays at 16 KB: 8 workgroups per CU)
+    constexpr int ND = 1 << DB, kStride = ND + 1, kDigCopies = DB == 8 ? 16 : 8, kPerWave = kDigCopies / 4;
+    constexpr int kPerLoad = 16 / sizeof(DT), kLoads = kItems / kPerLoad, kBits = 8 * sizeof(DT);
+    constexpr uint32_t kMask = ND - 1;
+    __shared__ uint32_t h[kDigCopies * kStride];
     const unsigned tid = threadIdx.x, wave = tid >> 6;
     const size_t base = (size_t)blockIdx.x * kTile;
     const size_t left = m - base;
-    // (the digit buffer has room past m: the load is unconditional)
-    const uint4 x = *reinterpret_cast<const uint4 *>(dig + base + (size_t)tid * kItems);
-    for (int i = tid; i < kDigCopies * kDigStride; i += kThreads)
+    // (the digit buffer has room past m: the loads are unconditional)
+    const uint4 *src = reinterpret_cast<const uint4 *>(dig + base + (size_t)tid * kItems);
+    uint4 x[kLoads];
+#pragma unroll
+    for (int q = 0; q < kLoads; q++)
+        x[q] = src[q];
+    for (int i = tid; i < kDigCopies * kStride; i += kThreads)
         h[i] = 0;
     __syncthreads();
-    uint32_t *mine = h + (wave * 4 + (tid & 3u)) * kDigStride;
-    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    uint32_t *mine = h + (wave * kPerWave + (tid & (kPerWave - 1u))) * kStride;
 #pragma unroll
-    for (int j = 0; j < kItems; j++)
-        if ((size_t)tid * kItems + j < left)
-            atomicAdd(&mine[(w[j >> 2] >> (8 * (j & 3))) & 255u], 1u);
+    for (int q = 0; q < kLoads; q++) {
+        const uint32_t w[4] = {x[q].x, x[q].y, x[q].z, x[q].w};
+#pragma unroll
+        for (int j = 0; j < kPerLoad; j++)
+            if ((size_t)tid * kItems + q * kPerLoad + j < left)
+                atomicAdd(&mine[(w[j * kBits / 32] >> (kBits * j % 32)) & kMask], 1u);
+    }
     __syncthreads();
-    uint32_t sum = 0;
+    for (uint32_t d = tid; d < (uint32_t)ND; d += kThreads) {
+        uint32_t sum = 0;
 #pragma unroll
-    for (int c = 0; c < kDigCopies; c++)
-        sum += h[c * kDigStride + tid];
-    counts[(size_t)tid * ntiles + blockIdx.x] = sum;
+        for (int c = 0; c < kDigCopies; c++)
+            sum += h[c * kStride + d];
+        counts[(size_t)d * ntiles + blockIdx.x] = sum;
+    }
 }
 
 // Digit-major tile counts -> per-digit exclusive prefixes over the tiles (in place), one
@@ -309,14 +315,16 @@ __global__ __launch_bounds__(TH) void k_radix_rowscan(uint32_t *__restrict__ cou
         totals[blockIdx.x] = carry;
 }
 
-void radix_rowscan(uint32_t *counts, uint32_t ntiles, uint32_t *totals, hipStream_t st)
+void radix_rowscan(uint32_t *counts, uint32_t ntiles, uint32_t *totals, hipStream_t st, uint32_t ndig)
 {
     if (ntiles <= 256 * 16)
-        hipLaunchKernelGGL((k_radix_rowscan<256, 16>), dim3(256), dim3(256), 0, st, counts, ntiles, totals);
+        hipLaunchKernelGGL((k_radix_rowscan<256, 16>), dim3(ndig), dim3(256), 0, st, counts, ntiles, totals);
     else if (ntiles <= 512 * 16)
-        hipLaunchKernelGGL((k_radix_rowscan<512, 16>), dim3(256), dim3(512), 0, st, counts, ntiles, totals);
+        hipLaunchKernelGGL((k_radix_rowscan<512, 16>), dim3(ndig), dim3(512), 0, st, counts, ntiles, totals);
+    else if (ndig > 256)  // (512 rows: three 50 KB workgroups per CU hold them all at once)
+        hipLaunchKernelGGL((k_radix_rowscan<512, 24>), dim3(ndig), dim3(512), 0, st, counts, ntiles, totals);
     else
-        hipLaunchKernelGGL((k_radix_rowscan<1024, 24>), dim3(256), dim3(1024), 0, st, counts, ntiles, totals);
+        hipLaunchKernelGGL((k_radix_rowscan<1024, 24>), dim3(ndig), dim3(1024), 0, st, counts, ntiles, totals);
 }
 
 // Tile of scatter workgroup b: workgroups are dealt round-robin to the 8 XCDs (b mod 8), so XCD x
@@ -329,27 +337,31 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t ntiles)
 }
 
 // TH threads per 4096-element tile (256: 16 items per thread; 512: 8 items, half the registers
-// per thread and twice the waves per CU for the same LDS).
-template <int kMode, int TH>
+// per thread and twice the waves per CU for the same LDS). DB: digit bits (8, or 9 with 512
+// threads: thread = digit in the digit scans); DT: type of the next pass's digit array.
+template <int kMode, int TH, int DB, typename DT>
 __global__ __launch_bounds__(TH) void k_radix_scatter(
     const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
     uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t m, int shift,
     const uint32_t *__restrict__ offs, uint32_t ntiles, const uint32_t *__restrict__ totals,
-    TextSrc txt, uint8_t *__restrict__ dout, int nshift)
+    TextSrc txt, DT *__restrict__ dout, int nshift, uint32_t nmask)
 {
-    constexpr int IT = kTile / TH, NW = TH / 64;
-    // Keys and values are staged one after the other in the same 32 KB (4 workgroups per CU
-    // instead of 2 with a 48 KB key + value stage).
+    constexpr int IT = kTile / TH, NW = TH / 64, ND = 1 << DB, DW = ND / 64;
+    constexpr uint32_t kMask = ND - 1;
+    static_assert(ND <= TH, "one thread per digit");
+    static_assert(kMode == 0 || kMode == 1 || kMode == 3 || DB == 8, "value-digit passes are 8-bit");
+    // Keys and values are staged one after the other in the same 32 KB (3 workgroups per CU
+    // with the counters of 512 threads, instead of 2 with a 48 KB key + value stage).
     __shared__ uint64_t skey[kTile];
     uint32_t *sval = reinterpret_cast<uint32_t *>(skey);
-    __shared__ uint32_t cnt[NW][256];
-    __shared__ uint32_t dstart[256];
-    __shared__ uint32_t gbase[256];
-    __shared__ uint32_t wsum[2][4];
+    __shared__ uint32_t cnt[NW][ND];
+    __shared__ uint32_t dstart[ND];
+    __shared__ uint32_t gbase[ND];
+    __shared__ uint32_t wsum[2][DW];
 
     const unsigned tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
-    for (int i = tid; i < NW * 256; i += TH)
+    for (int i = tid; i < NW * ND; i += TH)
         (&cnt[0][0])[i] = 0;
     __syncthreads();
 
@@ -416,10 +428,10 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     for (int j = 0; j < IT; j++) {
         size_t i = base + (size_t)j * 64 + lane;
         bool ok = i < m;
-        unsigned d = digit_of(kMode, k[j], v[j], shift, txt);
+        unsigned d = digit_of(kMode, k[j], v[j], shift, txt) & kMask;
         uint64_t peers = wave_ballot(ok);
 #pragma unroll
-        for (int b = 0; b < 8; b++) {
+        for (int b = 0; b < DB; b++) {
             bool bit = (d >> b) & 1u;
             uint64_t bb = wave_ballot(bit);
             peers &= bit ? bb : ~bb;
@@ -439,10 +451,10 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     }
     __syncthreads();
 
-    // Digit bases (exclusive scan of the 256 digit totals) and the tile-local digit starts
+    // Digit bases (exclusive scan of the ND digit totals) and the tile-local digit starts
     // (exclusive scan of the per-digit tile counts), thread = digit; the per-wave counts become
     // per-wave starts.
-    const bool dg = tid < 256;
+    const bool dg = tid < ND;
     uint32_t xt = 0, xc = 0, tt = 0, tot = 0;
     if (dg) {
         tt = totals[tid];
@@ -530,7 +542,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
 #pragma unroll
     for (int j = 0; j < IT; j++) {
         size_t i = base + (size_t)j * 64 + lane;
-        unsigned d = (unsigned)(k[j] >> shift) & 255u;
+        unsigned d = (unsigned)(k[j] >> shift) & kMask;
         pos[j] = dstart[d] + cnt[wave][d] + lrank[j];
         if (i < m)
             skey[pos[j]] = k[j];
@@ -545,11 +557,11 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
         const uint32_t s = tid + (uint32_t)j * TH;
         if (s < tcount) {
             uint64_t key = skey[s];
-            unsigned d = (unsigned)(key >> shift) & 255u;
+            unsigned d = (unsigned)(key >> shift) & kMask;
             gdst[j] = gbase[d] + (s - dstart[d]);
             kout[gdst[j]] = key;
             if (dout)  // the next pass's digit, for its histogram
-                dout[gdst[j]] = (uint8_t)(key >> nshift);
+                dout[gdst[j]] = (DT)((key >> nshift) & nmask);
         }
     }
     __syncthreads();  // keys out of LDS; the same bytes now stage the values
@@ -570,6 +582,39 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
 
 }  // namespace
 
+// Digit widths of a sort over `bits` key bits: 8-bit digits, or with SALZ_SA=d9 9-bit digits
+// wherever they save a pass (63-bit text keys: 7 passes instead of 8), the 9-bit ones first.
+// Measured on one box (round 5, tools/ab_env.sh): a 9-bit pass costs 575 us + 120 us of
+// histogram + 30 us of row scan on C2 against 515 + 84 + 17 for an 8-bit one, so the pass it
+// saves is spent again: C2 SA 19.79 (8-bit) vs 19.95 ms, mixed 100 MB 24.82 vs 24.72 ms.
+static int digit_plan(int bits, bool allow9, int *width)
+{
+    const bool nine = env_flag("SALZ_SA", "d9");
+    const int p8 = (bits + 7) / 8, p9 = (bits + 8) / 9;
+    if (!allow9 || !nine || p9 >= p8) {
+        for (int p = 0; p < p8; p++)
+            width[p] = 8;
+        return p8;
+    }
+    const int n9 = bits - 8 * p9;  // (p9 passes: n9 of 9 bits, the rest of 8; 0 < n9 <= p9)
+    for (int p = 0; p < p9; p++)
+        width[p] = p < n9 ? 9 : 8;
+    return p9;
+}
+
+template <int DB, typename DT>
+static void launch_key_scatter(int mode, uint32_t ntiles, hipStream_t st, const uint64_t *kin, const uint32_t *vin,
+                               uint64_t *kout, uint32_t *vout, uint32_t m, int shift, const uint32_t *counts,
+                               const uint32_t *totals, const TextSrc &txt, DT *dout, int nshift, uint32_t nmask)
+{
+    if (mode == 3)
+        hipLaunchKernelGGL((k_radix_scatter<3, 512, DB, DT>), dim3(ntiles), dim3(512), 0, st, kin, vin, kout, vout,
+                           m, shift, counts, ntiles, totals, txt, dout, nshift, nmask);
+    else
+        hipLaunchKernelGGL((k_radix_scatter<0, 512, DB, DT>), dim3(ntiles), dim3(512), 0, st, kin, vin, kout, vout,
+                           m, shift, counts, ntiles, totals, txt, dout, nshift, nmask);
+}
+
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
                      const uint8_t *text, const Blocks *blocks, const Alpha *alpha, uint8_t *digits,
@@ -578,8 +623,8 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     if (m <= 1 || bit_hi <= bit_lo)
         return 0;
     uint32_t ntiles = (m + kTile - 1) / kTile;
-    size_t ncounts = (size_t)ntiles * 256;
-    if (ncounts + 256 > ws.radix_counts_elems) {  // + the digit totals
+    const size_t ncounts = (size_t)ntiles * kMaxDigits;
+    if (ncounts + kMaxDigits > ws.radix_counts_elems) {  // + the digit totals
         set_error("radix: count buffer too small");
         return -1;
     }
@@ -589,62 +634,93 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     // A batch's round 0: after the key passes, passes on the digits of the value's block
     // (stable), so the list is ordered by (block, key).
     const int blk_bits = blocks && g.nb > 1 ? bit_width(g.nb - 1u) : 0;
-    const int passes_key = (bit_hi - bit_lo + 7) / 8, passes = passes_key + (blk_bits + 7) / 8;
-    // key passes with 512-thread workgroups (8 items per thread; 256 threads with 16 items measured
-    // ~0.5% slower on C2, profiles/r03h_tm_radix_ab.txt)
     // one block with raw-byte or 8/9-symbol keys: the text pass builds keys from an LDS window
     const bool text_win = g.nb == 1 && g.npos >= 7 && (!alpha || alpha->bits == 0 || alpha->k == 8 || alpha->k == 9);
+    // 9-bit digits: key passes of 512 threads only (the generic text pass of a batch and the
+    // materialised round-0 list's byte digits keep 8 bits)
+    int width[64];
+    const int passes_key = digit_plan(bit_hi - bit_lo, !(text && !text_win) && !digits_ready, width);
+    const int passes = passes_key + (blk_bits + 7) / 8;
+    bool wide = false;  // a 9-bit pass: every digit array of this sort is 16-bit
+    for (int p = 0; p < passes_key; p++)
+        wide |= width[p] > 8;
+    // key passes with 512-thread workgroups (8 items per thread; 256 threads with 16 items measured
+    // ~0.5% slower on C2, profiles/r03h_tm_radix_ab.txt)
+    int shift_key = bit_lo;
     for (int pass = 0; pass < passes; pass++) {
         const int mode = pass >= passes_key ? 2 : (text && pass == 0) ? (text_win ? 3 : 1) : 0;
-        const int shift = mode == 2 ? 8 * (pass - passes_key) : bit_lo + 8 * pass;
+        const int db = mode == 2 ? 8 : width[pass];
+        const int shift = mode == 2 ? 8 * (pass - passes_key) : shift_key;
         TextSrc txt{text, g, Alpha{}, nullptr, nullptr, 0u};
-        // digit bytes: written by a key pass for the next key pass, read by that pass's histogram
+        // digits: written by a key pass for the next key pass, read by that pass's histogram
         const uint8_t *dig_in = digits && (pass > 0 || digits_ready) && mode == 0 ? digits : nullptr;
         uint8_t *dig_out = digits && pass + 1 < passes_key ? digits : nullptr;
-        const int nshift = bit_lo + 8 * (pass + 1);
+        const int nshift = shift + db;
+        const uint32_t nmask = pass + 1 < passes_key ? (1u << width[pass + 1]) - 1u : 255u;
         if (alpha)
             txt.a = *alpha;
-        if (mode == 1 || mode == 3)
-            hipLaunchKernelGGL(k_radix_hist<1>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
-                               shift, ws.radix_counts, ntiles, txt, dig_in);
-        else if (mode == 2)
-            hipLaunchKernelGGL(k_radix_hist<2>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
-                               shift, ws.radix_counts, ntiles, txt, dig_in);
-        else if (dig_in)
-            hipLaunchKernelGGL(k_radix_hist_dig, dim3(ntiles), dim3(kThreads), 0, st, dig_in, m, ws.radix_counts,
-                               ntiles);
-        else
-            hipLaunchKernelGGL(k_radix_hist<0>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m,
-                               shift, ws.radix_counts, ntiles, txt, dig_in);
+        if (mode == 1 || mode == 3) {
+            if (db == 9)
+                hipLaunchKernelGGL((k_radix_hist<1, 9>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, shift,
+                                   ws.radix_counts, ntiles, txt, nullptr);
+            else
+                hipLaunchKernelGGL((k_radix_hist<1, 8>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, shift,
+                                   ws.radix_counts, ntiles, txt, nullptr);
+        } else if (mode == 2) {
+            hipLaunchKernelGGL((k_radix_hist<2, 8>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, shift,
+                               ws.radix_counts, ntiles, txt, nullptr);
+        } else if (dig_in && wide) {
+            const uint16_t *d16 = reinterpret_cast<const uint16_t *>(dig_in);
+            if (db == 9)
+                hipLaunchKernelGGL((k_radix_hist_dig<uint16_t, 9>), dim3(ntiles), dim3(kThreads), 0, st, d16, m,
+                                   ws.radix_counts, ntiles);
+            else
+                hipLaunchKernelGGL((k_radix_hist_dig<uint16_t, 8>), dim3(ntiles), dim3(kThreads), 0, st, d16, m,
+                                   ws.radix_counts, ntiles);
+        } else if (dig_in) {
+            hipLaunchKernelGGL((k_radix_hist_dig<uint8_t, 8>), dim3(ntiles), dim3(kThreads), 0, st, dig_in, m,
+                               ws.radix_counts, ntiles);
+        } else if (db == 9) {
+            hipLaunchKernelGGL((k_radix_hist<0, 9>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, shift,
+                               ws.radix_counts, ntiles, txt, nullptr);
+        } else {
+            hipLaunchKernelGGL((k_radix_hist<0, 8>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, shift,
+                               ws.radix_counts, ntiles, txt, nullptr);
+        }
         SALZ_LAUNCH_CHECK();
         uint32_t *totals = ws.radix_counts + ncounts;
-        radix_rowscan(ws.radix_counts, ntiles, totals, st);
+        radix_rowscan(ws.radix_counts, ntiles, totals, st, 1u << db);
         SALZ_LAUNCH_CHECK();
-        // bench.py prices the timed launches at 24 B per element (key + value in and out);
-        // the text-sourced and block passes are left out of that roofline
+        // bench.py prices the timed launches at 24 B per element (key + value in and out) + the
+        // next pass's digit; the text-sourced and block passes are left out of that roofline
         bool timed = ws.timing && mode == 0 && ws.rx_used + 2 <= ws.rx_pool.size();
         if (timed)
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used], st));
-        if (mode == 3)
-            hipLaunchKernelGGL((k_radix_scatter<3, 512>), dim3(ntiles), dim3(512), 0, st, kin,
-                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
-        else if (mode == 1)
-            hipLaunchKernelGGL((k_radix_scatter<1, kThreads>), dim3(ntiles), dim3(kThreads), 0, st, kin,
-                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
+        if (mode == 1)
+            hipLaunchKernelGGL((k_radix_scatter<1, kThreads, 8, uint8_t>), dim3(ntiles), dim3(kThreads), 0, st, kin,
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift, nmask);
         else if (mode == 2)
-            hipLaunchKernelGGL((k_radix_scatter<2, kThreads>), dim3(ntiles), dim3(kThreads), 0, st, kin,
-                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
+            hipLaunchKernelGGL((k_radix_scatter<2, kThreads, 8, uint8_t>), dim3(ntiles), dim3(kThreads), 0, st, kin,
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, nullptr, 0, 0u);
+        else if (wide && db == 9)
+            launch_key_scatter<9, uint16_t>(mode, ntiles, st, kin, vin, kout, vout, m, shift, ws.radix_counts, totals,
+                                            txt, reinterpret_cast<uint16_t *>(dig_out), nshift, nmask);
+        else if (wide)
+            launch_key_scatter<8, uint16_t>(mode, ntiles, st, kin, vin, kout, vout, m, shift, ws.radix_counts, totals,
+                                            txt, reinterpret_cast<uint16_t *>(dig_out), nshift, nmask);
         else
-            hipLaunchKernelGGL((k_radix_scatter<0, 512>), dim3(ntiles), dim3(512), 0, st, kin,
-                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift);
+            launch_key_scatter<8, uint8_t>(mode, ntiles, st, kin, vin, kout, vout, m, shift, ws.radix_counts, totals,
+                                           txt, dig_out, nshift, nmask);
         SALZ_LAUNCH_CHECK();
         if (timed) {
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used + 1], st));
             ws.rx_used += 2;
             ws.stats.radix_scatter_launches++;
             ws.stats.radix_scatter_elems += m;
-            ws.stats.radix_scatter_bytes += (uint64_t)m * (dig_out ? 25u : 24u);
+            ws.stats.radix_scatter_bytes += (uint64_t)m * (dig_out ? (wide ? 26u : 25u) : 24u);
         }
+        if (mode != 2)
+            shift_key += db;
         uint64_t *tk = kin;
         kin = kout;
         kout = tk;
@@ -663,8 +739,8 @@ int radix_sort_by_group(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, ui
     if (m <= 1 || GL <= 1)
         return 0;
     const uint32_t ntiles = (m + kTile - 1) / kTile;
-    const size_t ncounts = (size_t)ntiles * 256;
-    if (ncounts + 256 > ws.radix_counts_elems) {
+    const size_t ncounts = (size_t)ntiles * kMaxDigits;
+    if (ncounts + kMaxDigits > ws.radix_counts_elems) {
         set_error("radix: count buffer too small");
         return -1;
     }
@@ -674,13 +750,13 @@ int radix_sort_by_group(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, ui
     const int passes = (bit_width(GL - 1u) + 7) / 8;
     uint32_t *totals = ws.radix_counts + ncounts;
     for (int pass = 0; pass < passes; pass++) {
-        hipLaunchKernelGGL(k_radix_hist<4>, dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, 8 * pass,
+        hipLaunchKernelGGL((k_radix_hist<4, 8>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, 8 * pass,
                            ws.radix_counts, ntiles, txt, nullptr);
         SALZ_LAUNCH_CHECK();
-        radix_rowscan(ws.radix_counts, ntiles, totals, st);
+        radix_rowscan(ws.radix_counts, ntiles, totals, st, 256);
         SALZ_LAUNCH_CHECK();
-        hipLaunchKernelGGL((k_radix_scatter<4, kThreads>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, kout, vout,
-                           m, 8 * pass, ws.radix_counts, ntiles, totals, txt, nullptr, 0);
+        hipLaunchKernelGGL((k_radix_scatter<4, kThreads, 8, uint8_t>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin,
+                           kout, vout, m, 8 * pass, ws.radix_counts, ntiles, totals, txt, nullptr, 0, 0u);
         SALZ_LAUNCH_CHECK();
         uint64_t *tk = kin;
         kin = kout;

@@ -252,7 +252,8 @@ def test_encode_batch_grows_workspace(salz, cap, block, size):
         assert rc == 0 and got[k] == s, k
 
 
-@pytest.mark.parametrize("keys", ["", "noalpha", "tiny=2048", "rank1", "rank1,tiny=2048", "noalpha,tiny=2048"])
+@pytest.mark.parametrize("keys", ["", "noalpha", "tiny=2048", "rank1", "rank1,tiny=2048", "noalpha,tiny=2048",
+                                  "d9", "rank1,d9"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
                                                ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
@@ -265,7 +266,8 @@ def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
     bytes ("noalpha"), give the unique suffix array; round 1 keyed by the text at i + h0 (the
     default for such alphabets) or by ranks ("rank1"); groups of up to 64 members placed by
     counting and larger ones by LSD passes in LDS (the default), or every group by counting
-    ("tiny=2048")."""
+    ("tiny=2048"); radix passes of 8-bit digits (the default) or of 9-bit digits where they save a
+    pass ("d9": 63-bit text keys in 7 passes)."""
     monkeypatch.setenv("SALZ_SA", ",".join(x for x in (mode, keys) if x))
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
@@ -542,10 +544,15 @@ def test_cli_multi_batch_ring_and_exact_multiple(salz, tmp_path):
 
 @pytest.mark.parametrize("m,bits", [(1, 64), (4095, 17), (4097, 64), (13 * 4096 + 5, 40), (100_003, 63),
                                     (4096 * 4096, 24), (4096 * 4096 + 1, 64), (8192 * 4096 + 3000, 33),
-                                    (24576 * 4096 + 4097, 40)])
-def test_radix_sort_selftest(salz, m, bits):
+                                    (24576 * 4096 + 4097, 40), (100_003, 9), (200_001, 45),
+                                    (24576 * 4096 + 4097, 63)])
+@pytest.mark.parametrize("digits", ["", "d9"])
+def test_radix_sort_selftest(salz, monkeypatch, m, bits, digits):
     """The LSD radix sort (radix.hip) on random keys, and on keys with few distinct values for
     stability: sorted, stable and a permutation of its input, at tile counts that are and are not
     multiples of the 8 XCDs (the scatter's XCD-contiguous tile order) and across the row scan's
-    shapes (256-thread rows up to 4096 tiles, 512 up to 8192, 1024 beyond, looping past 24576)."""
+    shapes (256-thread rows up to 4096 tiles, 512 up to 8192, 1024 beyond, looping past 24576);
+    digit plans of 8-bit passes (the default; 24, 40, 64 bits), 9-bit passes (9, 45, 63 bits: one pass fewer)
+    and both (17, 33 bits) under SALZ_SA=d9."""
+    monkeypatch.setenv("SALZ_SA", digits)
     assert salz.radix_selftest(m, bits, iters=2, seed=7) == 0

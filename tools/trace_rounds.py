@@ -19,7 +19,7 @@ def kname(full):
 def main(path, which=0):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "k_radix_hist<1>" in r["Kernel_Name"] or "k_radix_hist<3>" in r["Kernel_Name"] or
+    starts = [i for i, r in enumerate(rows) if "k_radix_hist<1" in r["Kernel_Name"] or "k_radix_hist<3>" in r["Kernel_Name"] or
               "k_radix_hist<true>" in r["Kernel_Name"]]
     if not starts:
         sys.exit("no encode found")
