@@ -147,6 +147,9 @@ typedef struct {
 void salz_gpu_pool_config(int slots_per_device, size_t cache_bytes, int any_device);
 /* Device memory held by the pool's workspaces on `device`. */
 size_t salz_gpu_pool_bytes(int device);
+/* Device workspaces allocated by this process so far (every context, every device): a pool whose
+   workspaces are reused across calls keeps this flat. */
+size_t salz_gpu_workspace_allocs(void);
 
 /* Per-stage HIP-event timing of subsequent calls (small overhead when on). */
 void salz_gpu_set_timing(salz_gpu_ctx *ctx, int on);

@@ -1211,8 +1211,10 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         // counts, numbered by the scan, before the pass's one host read: that read then returns
         // the changed count, |E| (etotal), the dirty waves and the chunks the test listed
         // together. A pass that changed nothing leaves E as it was, so these are unchanged then.
+        // Packing is skipped on "no dirty wave" only when the walk itself skipped the clean waves
+        // (wd): under SALZ_PARSE=noskip every chunk is walked and E is packed every pass.
         hipLaunchKernelGGL(k_exit_pack, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st,
-                           reinterpret_cast<const uint64_t *>(eflag), S / 8, eb, skipping ? ndirty : nullptr);
+                           reinterpret_cast<const uint64_t *>(eflag), S / 8, eb, wd ? ndirty : nullptr);
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u32(eb.wcnt, eb.wpre, S / 64, false, etotal, ws, st) != 0)
             return -1;

@@ -239,8 +239,11 @@ int copy_d2h(Workspace &ws, uint8_t *dst, const uint8_t *src, size_t bytes)
 static size_t batch_stride(size_t bs) { return ((size_t)salz_encoded_len_max(bs) + bs / 4 + 64 + 63) & ~(size_t)63; }
 static size_t out_bound(size_t N) { return (size_t)salz_encoded_len_max(N) + N / 4 + 4096 + 128 * (size_t)kMaxBatchBlocks; }
 
+static std::atomic<size_t> g_ws_allocs{0};
+
 int workspace_alloc(Workspace &ws, int device, size_t max_block)
 {
+    g_ws_allocs.fetch_add(1);
     workspace_free(ws);
     SALZ_HIP(hipSetDevice(device));
     ws.device = device;
@@ -1250,22 +1253,29 @@ static salz_gpu_ctx *pool_try_acquire(int cur, size_t need, bool *create_failed,
     return c;
 }
 
-// After a call on `dev`: release idle workspaces (the largest first, `mine` included: its
-// caller still holds it) until the device's cached bytes are under the cap.
+// After a call on `dev`: while the device's IDLE workspaces (`mine`, whose caller still holds it
+// and is about to let it go, and every other context not busy right now) hold more than the cap,
+// release the largest. Busy contexts neither count nor get released: their callers trim after
+// their own calls. (Counting them let two concurrent 256 MiB callers, ~30 GB each against the
+// 32 GiB default, free their own workspace after every call and reallocate it on the next.)
 static void pool_trim(int dev, salz_gpu_ctx *mine)
 {
     const size_t cap = pool_cap_bytes();
     std::vector<salz_gpu_ctx *> snap;
     {
         std::lock_guard<std::mutex> lk(g_default_mu);
+        if ((size_t)(dev + 1) * kMaxSlots > g_default.size())
+            return;
         snap.assign(g_default.begin() + (size_t)dev * kMaxSlots, g_default.begin() + (size_t)(dev + 1) * kMaxSlots);
     }
+    std::vector<salz_gpu_ctx *> idle;  // locked here (all but `mine`)
+    for (salz_gpu_ctx *c : snap)
+        if (c && c != kCreating && (c == mine || c->mu.try_lock()))
+            idle.push_back(c);
     for (;;) {
         size_t total = 0, big = 0;
         salz_gpu_ctx *victim = nullptr;
-        for (salz_gpu_ctx *c : snap) {
-            if (!c || c == kCreating)
-                continue;
+        for (salz_gpu_ctx *c : idle) {
             const size_t b = c->held.load();
             total += b;
             if (b > big) {
@@ -1274,19 +1284,13 @@ static void pool_trim(int dev, salz_gpu_ctx *mine)
             }
         }
         if (total <= cap || !victim)
-            return;
-        if (victim != mine && !victim->mu.try_lock()) {
-            // busy: its own caller trims after its call; drop it from this pass
-            for (salz_gpu_ctx *&c : snap)
-                if (c == victim)
-                    c = nullptr;
-            continue;
-        }
+            break;
         workspace_release(victim->ws);
         victim->held.store(0);
-        if (victim != mine)
-            victim->mu.unlock();
     }
+    for (salz_gpu_ctx *c : idle)
+        if (c != mine)
+            c->mu.unlock();
 }
 
 // Restores the calling thread's current HIP device (the pool may create or run a context on
@@ -1338,6 +1342,8 @@ void salz_gpu_pool_config(int slots_per_device, size_t cache_bytes, int any_devi
     if (any_device >= 0)
         g_pool_any_dev.store(any_device ? 1 : 0);
 }
+
+size_t salz_gpu_workspace_allocs(void) { return g_ws_allocs.load(); }
 
 size_t salz_gpu_pool_bytes(int device)
 {
@@ -1471,6 +1477,8 @@ int salz_encode_blocks(const uint8_t *src, size_t src_len, size_t block_size, ui
             th.emplace_back(worker, d, k);
     for (auto &t : th)
         t.join();
+    for (int d = 0; d < ndev; d++)  // the pool's per-device cache cap holds here too
+        pool_trim(d, nullptr);
     size_t need = 8;
     for (size_t t = 0; t < nbatches; t++) {
         if (rcs[t] != 0) {
@@ -1693,6 +1701,8 @@ int salz_encode_stream(salz_read_fn rd, void *rd_user, salz_write_fn wr, void *w
     rth.join();
     for (auto &t : th)
         t.join();
+    for (int d = 0; d < ndev; d++)  // the pool's per-device cache cap holds here too
+        pool_trim(d, nullptr);
     free_ring();
     if (!err.empty()) {
         set_error("%s", err.c_str());

@@ -131,18 +131,45 @@ __global__ void k_alpha_presence(const uint8_t *__restrict__ T, size_t P, uint32
         atomicOr(&words[threadIdx.x], w[threadIdx.x]);
 }
 
-// Repetition probe (one workgroup): fingerprints of the 32 bytes at 4096 evenly spaced
-// positions, counted in an LDS hash table; out = how many samples share their fingerprint with
-// another. A Fibonacci or periodic block repeats every 32-gram (all samples collide), text almost
-// never. (A bitonic sort of the 4096 fingerprints took 78 barriers: ~70 us per block; the table
-// takes one insert per sample.)
+// Repetition probe. A suffix is still unfinished at depth 32 iff its first 32 bytes occur at
+// another position too, so the share of sampled 32-grams that occur twice anywhere in the block
+// estimates the share of suffixes that doubling would still carry at depth 32, which is what
+// the depth-32 switch to DC3 tests (stage_suffix_array). Two steps:
+//   k_repeat_probe (one workgroup) fingerprints the 32-grams at 4096 evenly spaced positions into
+//     an open-addressing table (8192 slots: a 30-bit tag << 2 per slot, and how many samples share
+//     it). Samples that collide with each other (Fibonacci, periodic blocks: every 32-gram repeats
+//     within a few samples) decide at once; the table is copied out for the scan.
+//   k_repeat_scan fingerprints the 32-gram at EVERY position and marks the table slots it hits
+//     (bit 0: once, bit 1: twice, per workgroup); k_repeat_count sums the samples of the slots hit
+//     twice overall. This catches repeats at any distance: a text repeated once at distance n / 2,
+//     or runs of one byte, where the evenly spaced samples never meet (round 4 sent those to DC3
+//     only at depth 32, after three full-width rounds).
+// The fingerprint of the 32 bytes at p, from their four little-endian words.
+__device__ __forceinline__ uint64_t gram_fp(uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3)
+{
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    const uint64_t w[4] = {w0, w1, w2, w3};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        h ^= w[q];
+        h *= 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 31;
+    }
+    return h;
+}
 constexpr uint32_t kProbe = 4096;
 constexpr uint32_t kProbeThreads = 1024;
-constexpr uint32_t kProbeSlots = 16384;  // open addressing, 1/4 full
+constexpr uint32_t kProbeSlots = 8192;  // open addressing, at most half full
+__device__ __forceinline__ uint32_t gram_slot(uint64_t h) { return (uint32_t)h & (kProbeSlots - 1u); }
+__device__ __forceinline__ uint32_t gram_tag(uint64_t h) { return (((uint32_t)(h >> 34)) | 1u) << 2; }
+
+// ptab: the table's tags (0 = empty), pmul: samples per slot, gcnt: occurrences (zeroed here for the
+// scan). out[0]: samples that share their fingerprint with another sample.
 __global__ __launch_bounds__(kProbeThreads) void k_repeat_probe(const uint8_t *__restrict__ T, uint32_t n,
-                                                                uint32_t *__restrict__ out)
+                                                                uint32_t *__restrict__ out, uint32_t *__restrict__ ptab,
+                                                                uint32_t *__restrict__ pmul, uint32_t *__restrict__ gcnt)
 {
-    __shared__ uint32_t key[kProbeSlots];  // the upper half of a fingerprint, | 1 (0 = empty)
+    __shared__ uint32_t key[kProbeSlots];
     __shared__ uint32_t cnt[kProbeSlots];
     __shared__ uint32_t dups;
     constexpr uint32_t kPerT = kProbe / kProbeThreads;
@@ -164,18 +191,12 @@ __global__ __launch_bounds__(kProbeThreads) void k_repeat_probe(const uint8_t *_
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kPerT; j++) {
-        uint64_t h = 0x9E3779B97F4A7C15ull;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            h ^= w[j][q];
-            h *= 0xBF58476D1CE4E5B9ull;
-            h ^= h >> 31;
-        }
-        const uint32_t fp = (uint32_t)(h >> 32) | 1u;
-        uint32_t slot = (uint32_t)h & (kProbeSlots - 1u);
+        const uint64_t h = gram_fp(w[j][0], w[j][1], w[j][2], w[j][3]);
+        const uint32_t tag = gram_tag(h);
+        uint32_t slot = gram_slot(h);
         for (uint32_t probe = 0; probe < kProbeSlots; probe++) {  // (the table never fills)
-            const uint32_t old = atomicCAS(&key[slot], 0u, fp);
-            if (old == 0u || old == fp) {
+            const uint32_t old = atomicCAS(&key[slot], 0u, tag);
+            if (old == 0u || old == tag) {
                 atomicAdd(&cnt[slot], 1u);
                 break;
             }
@@ -184,12 +205,94 @@ __global__ __launch_bounds__(kProbeThreads) void k_repeat_probe(const uint8_t *_
     }
     __syncthreads();
     uint32_t d = 0;
-    for (uint32_t i = tid; i < kProbeSlots; i += kProbeThreads)
+    for (uint32_t i = tid; i < kProbeSlots; i += kProbeThreads) {
         d += cnt[i] >= 2u ? cnt[i] : 0u;
+        if (ptab) {
+            ptab[i] = key[i];
+            pmul[i] = cnt[i];
+            gcnt[i] = 0u;
+        }
+    }
     atomicAdd(&dups, d);
     __syncthreads();
     if (tid == 0)
         *out = dups;
+}
+
+// Every position's 32-gram against the sample table (skipped when the samples decided already:
+// dups[0] * 2 >= kProbe). A thread takes 8 consecutive positions from 5 aligned text words.
+constexpr uint32_t kScanThreads = 256;
+__global__ __launch_bounds__(kScanThreads) void k_repeat_scan(const uint8_t *__restrict__ T, uint32_t n,
+                                                              const uint32_t *__restrict__ dups,
+                                                              const uint32_t *__restrict__ ptab,
+                                                              uint32_t *__restrict__ gcnt)
+{
+    __shared__ uint32_t tab[kProbeSlots];  // tag | bit 0: hit once | bit 1: hit twice (this workgroup)
+    if (dups[0] * 2u >= kProbe)
+        return;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < kProbeSlots; i += kScanThreads)
+        tab[i] = ptab[i];
+    __syncthreads();
+    const uint32_t last = n - 32u;  // positions 0..last hold a whole 32-gram
+    const uint64_t *W = reinterpret_cast<const uint64_t *>(T);
+    for (size_t g = (size_t)blockIdx.x * kScanThreads + tid; g * 8 <= last; g += (size_t)gridDim.x * kScanThreads) {
+        uint64_t x[5];  // (the text buffer is padded past N + 64)
+#pragma unroll
+        for (int q = 0; q < 5; q++)
+            x[q] = W[g + q];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t sh = 8u * j;
+            uint64_t v[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                v[q] = (x[q] >> sh) | ((x[q + 1] << 1) << (63u - sh));
+            const uint64_t h = gram_fp(v[0], v[1], v[2], v[3]);
+            const uint32_t tag = gram_tag(h);
+            uint32_t slot = gram_slot(h);
+            if (g * 8 + j > last)
+                break;
+            for (;;) {
+                const uint32_t e = tab[slot];
+                if (e == 0u)
+                    break;
+                if ((e & ~3u) == tag) {
+                    if (!(e & 2u) && (atomicOr(&tab[slot], 1u) & 1u))
+                        atomicOr(&tab[slot], 2u);
+                    break;
+                }
+                slot = (slot + 1u) & (kProbeSlots - 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < kProbeSlots; i += kScanThreads) {
+        const uint32_t c = (tab[i] & 1u) + ((tab[i] >> 1) & 1u);
+        if (c)
+            atomicAdd(&gcnt[i], c);
+    }
+}
+
+// out[0]: the samples whose 32-gram occurs at least twice in the block.
+__global__ __launch_bounds__(kProbeThreads) void k_repeat_count(const uint32_t *__restrict__ dups,
+                                                                const uint32_t *__restrict__ ptab,
+                                                                const uint32_t *__restrict__ pmul,
+                                                                const uint32_t *__restrict__ gcnt,
+                                                                uint32_t *__restrict__ out)
+{
+    __shared__ uint32_t tot;
+    if (threadIdx.x == 0)
+        tot = 0;
+    __syncthreads();
+    uint32_t r = 0;
+    if (dups[0] * 2u < kProbe)
+        for (uint32_t i = threadIdx.x; i < kProbeSlots; i += kProbeThreads)
+            r += ptab[i] && gcnt[i] >= 2u ? pmul[i] : 0u;
+    atomicAdd(&tot, r);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        *out = tot;
 }
 
 // Group-head flags travel as one 64-bit ballot per wave of the sorted list (hmask) plus its
@@ -850,6 +953,22 @@ __global__ void k_dbg_pairs(const uint64_t *__restrict__ K, const uint32_t *__re
     }
 }
 
+// The text round's list (SALZ_CHECK=rounds): every key is the round-0 key at i + h0 of its suffix,
+// and the list is sorted by (group, key).
+__global__ void k_dbg_text(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
+                           const uint32_t *__restrict__ gin, const uint8_t *__restrict__ Tm, uint32_t m, Blocks bl,
+                           Alpha a, uint32_t h0, uint32_t *err)
+{
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (c >= m)
+        return;
+    const uint32_t i = V[c];
+    if (i >= bl.npos || bl.end(i) - i <= h0 || K[c] != round0_key_mapped(Tm, i + h0, bl.end(i), a))
+        atomicOr(err, 0x80000u);
+    else if (c > 0 && (gin[c - 1] > gin[c] || (gin[c - 1] == gin[c] && K[c - 1] > K[c])))
+        atomicOr(err, 0x100000u);
+}
+
 __global__ void k_dbg_heads(HeadBits hb, const uint32_t *__restrict__ headpos, uint32_t m,
                             uint32_t *err)
 {
@@ -1193,8 +1312,10 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // that wide; text keeps ~17% at depth 32, Fibonacci and periodic blocks all of them).
     const bool dc3_force = env_flag("SALZ_SA", "dc3") && bl.nb == 1 && n >= 2 && !dist;
     const bool dc3_auto = !env_flag("SALZ_SA", "doubling") && bl.nb == 1 && n >= (1u << 20) && !dist;
-    // SALZ_SA=noprobe: no repetition probe (only the depth-32 switch)
+    // SALZ_SA=noprobe: no repetition probe (only the depth-32 switch); noscan: the evenly spaced
+    // samples only (round 4's probe), no scan of every position
     const bool dc3_probe_off = env_flag("SALZ_SA", "noprobe");
+    const bool dc3_scan = !env_flag("SALZ_SA", "noscan") && n >= 64;
     bool dc3_now = false;
     Alpha codes{};  // the block's byte codes 1..sigma for DC3 (raw bytes + 1 when not known)
     int codes_raw = 1;
@@ -1206,13 +1327,29 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                            dim3(kT), 0, st, ws.text, P, words);
         SALZ_LAUNCH_CHECK();
         if (dc3_auto && !dc3_probe_off) {
-            hipLaunchKernelGGL(k_repeat_probe, dim3(1), dim3(kProbeThreads), 0, st, ws.text, n, words + 8);
+            // sample table, scan and count in u1 (free until round 0's survivor counts)
+            uint32_t *ptab = ws.u1, *pmul = ws.u1 + kProbeSlots, *gcnt = ws.u1 + 2 * kProbeSlots;
+            hipLaunchKernelGGL(k_repeat_probe, dim3(1), dim3(kProbeThreads), 0, st, ws.text, n, words + 8,
+                               dc3_scan ? ptab : nullptr, pmul, gcnt);
             SALZ_LAUNCH_CHECK();
+            if (dc3_scan) {
+                const uint32_t groups = (n - 32u) / 8u + 1u;
+                const uint32_t grid = grid_for(groups, kScanThreads) < 1024 ? grid_for(groups, kScanThreads) : 1024;
+                hipLaunchKernelGGL(k_repeat_scan, dim3(grid), dim3(kScanThreads), 0, st, ws.text, n, words + 8,
+                                   ptab, gcnt);
+                SALZ_LAUNCH_CHECK();
+                hipLaunchKernelGGL(k_repeat_count, dim3(1), dim3(kProbeThreads), 0, st, words + 8, ptab, pmul,
+                                   gcnt, words + 9);
+                SALZ_LAUNCH_CHECK();
+            }
         }
         if (read_scalars(ws, 960, 48, "sa.alpha") != 0)
             return -1;
-        // half the samples repeated: long repeats everywhere, DC3 from the start
-        dc3_now = dc3_auto && !dc3_probe_off && reinterpret_cast<const uint32_t *>(ws.hscal)[248] * 2 >= kProbe;
+        // half the samples repeated among themselves (long repeats everywhere), or three quarters
+        // of them anywhere in the block (what the depth-32 switch below tests): DC3 from the start
+        const uint32_t *hs = reinterpret_cast<const uint32_t *>(ws.hscal);
+        dc3_now = dc3_auto && !dc3_probe_off &&
+                  (hs[248] * 2 >= kProbe || (dc3_scan && (uint64_t)hs[249] * 4 >= 3ull * kProbe));
         const uint32_t *pw = reinterpret_cast<const uint32_t *>(ws.hscal) + 240;
         uint32_t sigma = 0;
         for (int c = 0; c < 256; c++)
@@ -1304,7 +1441,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // Round 1 keyed by text (see k_keys_text): one block or a batch, the block's own sort (not a
     // split block's bucket), an alphabet of at most 127 bytes (symbols >= 1, so zero padding
     // is unambiguous). SALZ_SA=rank1 keeps round 1 on ranks.
-    const bool text1 = !env_flag("SALZ_SA", "rank1") && !dist && !dbg_rounds && alpha.bits > 0;
+    const bool text1 = !env_flag("SALZ_SA", "rank1") && !dist && alpha.bits > 0;
     const int tbits = (int)(alpha.k * alpha.bits);
     // group ids of the text round's list (its keys are the text): the upper half of lsc, free
     // during every round (the window plan and tile map take its first entries)
@@ -1420,6 +1557,11 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         Kx = (K == ws.keyA) ? ws.keyB : ws.keyA;
         Vx = (V == ws.valA) ? ws.valB : ws.valA;
 
+        if (dbg_rounds && textr) {
+            hipLaunchKernelGGL(k_dbg_text, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, gin, tmapped, m, bl, alpha,
+                               h / 2, derr);
+            SALZ_LAUNCH_CHECK();
+        }
         if (dbg_rounds && !seg_round && bl.nb == 1) {
             hipLaunchKernelGGL(k_dbg_sorted, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, m, derr, 0x1000u);
             SALZ_LAUNCH_CHECK();

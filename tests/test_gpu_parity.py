@@ -42,6 +42,11 @@ def _special(kind, n):
     if kind == "runs":
         rng = np.random.default_rng(5)
         return np.repeat(rng.integers(0, 3, n // 50 + 1, dtype=np.uint8), 50)[:n].copy()
+    if kind == "runs40":  # runs of 40 equal bytes, 64 byte values
+        rng = np.random.default_rng(6)
+        return np.repeat(rng.integers(0, 64, n // 40 + 1, dtype=np.uint8), 40)[:n].copy()
+    if kind == "halves":  # a text repeated once at distance ~n / 2
+        return np.resize(gen("text", n // 2 + 1, 11), n)
     raise ValueError(kind)
 
 
@@ -59,7 +64,7 @@ STAGE_CASES = [
 
 
 def _make(kind, n, seed, alpha):
-    if kind in ("zeros", "period3", "runs"):
+    if kind in ("zeros", "period3", "runs", "runs40", "halves"):
         return _special(kind, n)
     return gen(kind, n, seed, alpha)
 
@@ -252,21 +257,24 @@ def test_encode_batch_grows_workspace(salz, cap, block, size):
         assert rc == 0 and got[k] == s, k
 
 
-@pytest.mark.parametrize("keys", ["", "noalpha", "tiny=2048", "rank1", "rank1,tiny=2048", "noalpha,tiny=2048",
-                                  "d9", "rank1,d9"])
+@pytest.mark.parametrize("keys", ["", "noalpha", "tiny=2048", "tiny=0", "rank1", "rank1,tiny=2048",
+                                  "noalpha,tiny=2048", "d9", "rank1,d9"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
                                                ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
                                                ("smx", 150000, 3, 20), ("runs", 120000, 0, 0),
-                                               ("zeros", 70000, 0, 0), ("smx", 300000, 4, 100)])
+                                               ("zeros", 70000, 0, 0), ("smx", 300000, 4, 100),
+                                               ("runs40", 700001, 0, 0)])
 def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
     """Both doubling-round sorts (global radix on (group, rank); LDS sort of small groups +
     extracted large groups; SALZ_SA=global / segmented), with round-0 keys from the compacted
     alphabet (the default for texts of <= 127 distinct bytes: 2 to 32 symbols per key) or raw
     bytes ("noalpha"), give the unique suffix array; round 1 keyed by the text at i + h0 (the
-    default for such alphabets) or by ranks ("rank1"); groups of up to 64 members placed by
-    counting and larger ones by LSD passes in LDS (the default), or every group by counting
-    ("tiny=2048"); radix passes of 8-bit digits (the default) or of 9-bit digits where they save a
+    default for such alphabets) or by ranks ("rank1"); groups of up to 128 members (rank rounds)
+    or 256 (the text round) placed by counting and larger ones by LSD passes in LDS (the
+    default), every group by counting ("tiny=2048"), or every group by the LSD passes ("tiny=0":
+    on the repetitive small-alphabet "runs40" block the text round's LSD leaves runs of equal top
+    key bits longer than 64 entries, which k_seg_text_fix orders with its bitonic network); radix passes of 8-bit digits (the default) or of 9-bit digits where they save a
     pass ("d9": 63-bit text keys in 7 passes)."""
     monkeypatch.setenv("SALZ_SA", ",".join(x for x in (mode, keys) if x))
     src = _make(kind, n, seed, alpha)
@@ -350,20 +358,47 @@ def test_dc3_edge_sizes(ctx, monkeypatch):
             assert rc == 0 and out == ref, (N, kind)
 
 
-@pytest.mark.parametrize("algo", ["", "noprobe", "doubling"])
+def test_suffix_sort_round_checks():
+    """SALZ_CHECK=rounds,sa (the suffix sorter's per-round invariants, the text round's keys and
+    order included, and the final permutation check) pass, and the streams equal the oracle's.
+    The switch is read once per process, so the encodes run in a child process."""
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import salz_amd\n"
+        "from tests.test_gpu_parity import _make\n"
+        "from tests.helpers import oracle_encode\n"
+        "ctx = salz_amd.Context(0, 1 << 21)\n"
+        "for kind, n, seed, alpha in (('text', 600000, 5, 0), ('mixed', 300000, 6, 0), ('smx', 200000, 2, 20),\n"
+        "                             ('fib', 100000, 0, 0), ('runs40', 400001, 0, 0)):\n"
+        "    src = _make(kind, n, seed, alpha)\n"
+        "    assert ctx.encode(src) == oracle_encode(src)[1], kind\n"
+        "print('round checks ok')\n" % ROOT)
+    env = dict(os.environ, SALZ_CHECK="rounds,sa")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0 and "round checks ok" in r.stdout, (r.stdout + r.stderr)[-3000:]
+
+
+@pytest.mark.parametrize("algo", ["", "noscan", "noprobe", "doubling"])
 def test_dc3_auto_switch(ctx, monkeypatch, algo):
-    """A repetitive block of >= 1 MiB goes to DC3 by default: before round 0 when the repetition
-    probe finds its sampled 32-grams repeated, else (SALZ_SA=noprobe) at depth 32; text does
-    not; SALZ_SA=doubling keeps prefix doubling. All give the reference stream."""
-    monkeypatch.setenv("SALZ_SA", algo if algo in ("noprobe", "doubling") else "")
-    for kind, n in (("fib", 3 << 20), ("period3", 2 << 20), ("text", 2 << 20)):
+    """A repetitive block of >= 1 MiB goes to DC3 by default. Before round 0 when the repetition
+    probe finds its evenly spaced 32-gram samples repeated among themselves (Fibonacci, period 3),
+    or finds three quarters of them occurring elsewhere in the block by scanning every position
+    (a text repeated once at distance n / 2, runs of 40 equal bytes: the samples rarely meet there;
+    SALZ_SA=noscan leaves those to the depth-32 switch); with SALZ_SA=noprobe at depth 32; text
+    does not go; SALZ_SA=doubling keeps prefix doubling. All give the reference stream."""
+    monkeypatch.setenv("SALZ_SA", algo)
+    for kind, n in (("fib", 3 << 20), ("period3", 2 << 20), ("text", 2 << 20), ("halves", (2 << 20) + 4321),
+                    ("runs40", (3 << 20) + 77)):
         src = _make(kind, n, 1, 0)
         out = ctx.encode(src)
         rep = kind != "text" and algo != "doubling"
         st = ctx.stats()
         assert (st["sa_dc3_levels"] > 0) == rep, kind
         if rep:  # the probe skips round 0 of doubling
-            assert st["sa_rounds"] == (1 if algo == "noprobe" else 0), kind
+            early = algo == "" or (algo == "noscan" and kind in ("fib", "period3"))
+            assert (st["sa_rounds"] == 0) == early, (kind, st["sa_rounds"])
         rc, ref = oracle_encode(src)
         assert rc == 0 and out == ref, kind
 

@@ -15,6 +15,7 @@ from tests.helpers import gen, oracle_encode  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--size", type=int, default=64 << 20)
 ap.add_argument("--parity", action="store_true")
+ap.add_argument("--cases", default="", help="comma-separated subset of the cases (default: all)")
 a = ap.parse_args()
 n = a.size
 cases = {
@@ -30,7 +31,10 @@ cases = {
     "mixed": lambda: gen("mixed", n, 17),
 }
 ctx = salz_amd.Context(0, n)
+want = [c for c in a.cases.split(",") if c]
 for name, make in cases.items():
+    if want and name not in want:
+        continue
     src = make()
     ctx.encode(src[: 1 << 20])  # warm
     t0 = time.perf_counter()
