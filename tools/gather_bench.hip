@@ -3,6 +3,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -o tools/gather_bench tools/gather_bench.hip
 //   tools/gather_bench [table_mib] [queries_m]
+//   tools/gather_bench calib     (one dispatch per access pattern, for the PMC calibration)
 //
 // Every kernel: one query per thread, indices from a precomputed random array (read
 // coalesced), results written coalesced, so the random side is the only random traffic.
@@ -117,8 +118,54 @@ __global__ void k_gather8(const uint8_t *__restrict__ tab, const uint32_t *__res
     out[i] = (a >> sh) | ((b << 1) << (63u - sh));
 }
 
+// Plain coalesced copy of 16-byte words (the calibration's streaming reference).
+__global__ void k_copy16(const uint4 *__restrict__ a, uint4 *__restrict__ b, size_t m)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < m)
+        b[i] = a[i];
+}
+
+// Calibration of the FETCH_SIZE / WRITE_SIZE counters (tools/pmc_traffic.py --calib): each kernel
+// runs exactly once on known byte counts, so that `rocprofv3 --pmc FETCH_SIZE` (then WRITE_SIZE)
+// of `gather_bench calib` gives the counter per access pattern:
+//   k_copy16               m16 16-byte reads + writes, coalesced (the guide's x2 fetch case)
+//   k_gather4<0> big/small m 4-byte random reads from a 1.6 GB table / a 64 MiB (L2 + MALL) table,
+//                          + the 4-byte index read and result write, coalesced
+//   k_gather8<0>           m unaligned 8-byte reads (two aligned words) from a 400 MB byte table
+//   k_scatter4<0>          m 4-byte random writes into 1.6 GB
+//   k_scatter16            m 16-byte random writes into 1.6 GB
+static int calib()
+{
+    const size_t m = 64u << 20, big = (size_t)1600 << 20, small = (size_t)64 << 20;
+    uint32_t *tab, *idx, *out;
+    CK(hipMalloc(&tab, big + 64));
+    CK(hipMalloc(&idx, m * 4));
+    CK(hipMalloc(&out, m * 16));
+    CK(hipMemset(tab, 1, big + 64));
+    const dim3 g((unsigned)((m + 255) / 256)), b(256);
+    printf("calib m=%zu accesses per kernel; useful bytes: copy16 %zu read + %zu write; gather4 %zu random + "
+           "%zu coalesced read, %zu write; gather8 %zu random read; scatter4 %zu random write; scatter16 %zu random "
+           "write\n", m, m * 16, m * 16, m * 4, m * 4, m * 4, m * 8, m * 4, m * 16);
+    k_copy16<<<g, b>>>(reinterpret_cast<const uint4 *>(tab), reinterpret_cast<uint4 *>(out), m);
+    k_init_idx<<<g, b>>>(idx, m, (uint32_t)(big / 4), 11);
+    k_gather4<0><<<g, b>>>(tab, idx, m, out);                              // dispatch: big table
+    k_init_idx<<<g, b>>>(idx, m, (uint32_t)(small / 4), 12);
+    k_gather4<0><<<g, b>>>(tab, idx, m, out);                              // dispatch: small table
+    k_init_idx<<<g, b>>>(idx, m, (uint32_t)(400u << 20), 13);
+    k_gather8<0><<<g, b>>>(reinterpret_cast<uint8_t *>(tab), idx, m, reinterpret_cast<uint64_t *>(out));
+    k_init_idx<<<g, b>>>(idx, m, (uint32_t)(big / 4), 14);
+    k_scatter4<0><<<g, b>>>(tab, idx, m);
+    k_init_idx<<<g, b>>>(idx, m, (uint32_t)(big / 16), 15);
+    k_scatter16<<<g, b>>>(reinterpret_cast<uint4 *>(tab), idx, m);
+    CK(hipDeviceSynchronize());
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
+    if (argc > 1 && argv[1][0] == 'c')
+        return calib();
     const size_t tab_mib = argc > 1 ? atol(argv[1]) : 400;
     const size_t m = (argc > 2 ? atol(argv[2]) : 64) << 20;
     const uint32_t n4 = (uint32_t)((tab_mib << 20) / 4);
