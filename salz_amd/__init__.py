@@ -81,8 +81,9 @@ lib.salz_gpu_pool_config.argtypes = [ctypes.c_int, _sz, ctypes.c_int]
 lib.salz_gpu_pool_config.restype = None
 lib.salz_gpu_pool_bytes.argtypes = [ctypes.c_int]
 lib.salz_gpu_pool_bytes.restype = _sz
-lib.salz_gpu_workspace_allocs.argtypes = []
-lib.salz_gpu_workspace_allocs.restype = _sz
+if hasattr(lib, "salz_gpu_workspace_allocs"):  # (absent from round-4 builds loaded for A/B timing)
+    lib.salz_gpu_workspace_allocs.argtypes = []
+    lib.salz_gpu_workspace_allocs.restype = _sz
 lib.salz_gpu_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
 lib.salz_gpu_set_timing.restype = None
 lib.salz_gpu_encode_batch.argtypes = [ctypes.c_void_p, _u8p, _sz, _sz, _u8p, _szp]

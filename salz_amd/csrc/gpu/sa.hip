@@ -135,42 +135,47 @@ __global__ void k_alpha_presence(const uint8_t *__restrict__ T, size_t P, uint32
 // another position too, so the share of sampled 32-grams that occur twice anywhere in the block
 // estimates the share of suffixes that doubling would still carry at depth 32, which is what
 // the depth-32 switch to DC3 tests (stage_suffix_array). Two steps:
-//   k_repeat_probe (one workgroup) fingerprints the 32-grams at 4096 evenly spaced positions into
-//     an open-addressing table (8192 slots: a 30-bit tag << 2 per slot, and how many samples share
-//     it). Samples that collide with each other (Fibonacci, periodic blocks: every 32-gram repeats
-//     within a few samples) decide at once; the table is copied out for the scan.
-//   k_repeat_scan fingerprints the 32-gram at EVERY position and marks the table slots it hits
-//     (bit 0: once, bit 1: twice, per workgroup); k_repeat_count sums the samples of the slots hit
-//     twice overall. This catches repeats at any distance: a text repeated once at distance n / 2,
-//     or runs of one byte, where the evenly spaced samples never meet (round 4 sent those to DC3
-//     only at depth 32, after three full-width rounds).
-// The fingerprint of the 32 bytes at p, from their four little-endian words.
+//   k_repeat_probe (one workgroup) fingerprints 512 evenly spaced sample points, each as the eight
+//     32-grams at q, q + 1, .., q + 7, into an open-addressing table (8192 slots: a 30-bit tag << 2
+//     per slot, and how many samples share it). Samples that collide with each other (Fibonacci,
+//     periodic blocks: every 32-gram repeats within a few samples) decide at once.
+//   k_repeat_scan fingerprints the 32-gram at every position p = 0 mod 8 (aligned words: no byte
+//     shifts) and counts the table slots it hits; k_repeat_count calls a point repeated when one of
+//     its eight grams occurs at an aligned position other than its own. A copy of the point at any
+//     distance d puts exactly one of its eight grams (q + i + d = 0 mod 8) on an aligned position,
+//     so this finds repeats at any distance: a text repeated once at distance n / 2, or runs of one
+//     byte, where the evenly spaced samples never meet (round 4 sent those to DC3 only at depth 32,
+//     after three full-width rounds).
+// The fingerprint of the 32 bytes from their four little-endian words: an xor of rotated words
+// (full-rate operations), then 32-bit multiplies for the table slot, the filter bit and the 30-bit
+// tag. A collision only makes a 32-gram look repeated.
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 __device__ __forceinline__ uint64_t gram_fp(uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3)
 {
-    uint64_t h = 0x9E3779B97F4A7C15ull;
-    const uint64_t w[4] = {w0, w1, w2, w3};
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        h ^= w[q];
-        h *= 0xBF58476D1CE4E5B9ull;
-        h ^= h >> 31;
-    }
-    return h;
+    const uint64_t f = w0 ^ rotl64(w1, 19) ^ rotl64(w2, 38) ^ rotl64(w3, 57);
+    return f ^ (f >> 29);
 }
-constexpr uint32_t kProbe = 4096;
+constexpr uint32_t kProbePoints = 512;
+constexpr uint32_t kProbe = 8 * kProbePoints;  // sampled grams
 constexpr uint32_t kProbeThreads = 1024;
-constexpr uint32_t kProbeSlots = 8192;  // open addressing, at most half full
-__device__ __forceinline__ uint32_t gram_slot(uint64_t h) { return (uint32_t)h & (kProbeSlots - 1u); }
-__device__ __forceinline__ uint32_t gram_tag(uint64_t h) { return (((uint32_t)(h >> 34)) | 1u) << 2; }
+constexpr uint32_t kProbeSlots = 8192;    // open addressing, at most half full
+constexpr uint32_t kFilterBits = 65536;  // one bit per 16-bit fingerprint prefix of a sample (6% set)
+__device__ __forceinline__ uint32_t gram_mix(uint64_t h) { return (uint32_t)h * 0x9E3779B1u; }
+__device__ __forceinline__ uint32_t gram_slot(uint32_t mx) { return mx >> 19; }
+__device__ __forceinline__ uint32_t gram_fbit(uint32_t mx) { return mx >> 16; }
+__device__ __forceinline__ uint32_t gram_tag(uint64_t h) { return (((uint32_t)(h >> 32) * 0x85EBCA77u) | 4u) & ~3u; }
 
-// ptab: the table's tags (0 = empty), pmul: samples per slot, gcnt: occurrences (zeroed here for the
-// scan). out[0]: samples that share their fingerprint with another sample.
+// ptab: the table's tags (0 = empty), pmul: samples per slot, gcnt: aligned occurrences (zeroed here
+// for the scan), pfilt: the samples' filter bits, pslot: every sample's slot (<< 1 | its own position
+// is aligned). out[0]: samples that share their fingerprint with another sample.
 __global__ __launch_bounds__(kProbeThreads) void k_repeat_probe(const uint8_t *__restrict__ T, uint32_t n,
                                                                 uint32_t *__restrict__ out, uint32_t *__restrict__ ptab,
-                                                                uint32_t *__restrict__ pmul, uint32_t *__restrict__ gcnt)
+                                                                uint32_t *__restrict__ pmul, uint32_t *__restrict__ gcnt,
+                                                                uint32_t *__restrict__ pfilt, uint32_t *__restrict__ pslot)
 {
     __shared__ uint32_t key[kProbeSlots];
     __shared__ uint32_t cnt[kProbeSlots];
+    __shared__ uint32_t filt[kFilterBits / 32];
     __shared__ uint32_t dups;
     constexpr uint32_t kPerT = kProbe / kProbeThreads;
     const uint32_t tid = threadIdx.x;
@@ -180,20 +185,25 @@ __global__ __launch_bounds__(kProbeThreads) void k_repeat_probe(const uint8_t *_
         key[i] = 0;
         cnt[i] = 0;
     }
+    for (uint32_t i = tid; i < kFilterBits / 32; i += kProbeThreads)
+        filt[i] = 0;
     uint64_t w[kPerT][4];  // every sample's loads issued first
+    size_t pos[kPerT];
 #pragma unroll
     for (uint32_t j = 0; j < kPerT; j++) {
-        const size_t p = (size_t)(tid + j * kProbeThreads) * (n - 32u) / kProbe;
+        const uint32_t s = tid + j * kProbeThreads;  // sample s: point s / 8, gram s % 8
+        pos[j] = (size_t)(s >> 3) * (n - 40u) / kProbePoints + (s & 7u);
 #pragma unroll
         for (int q = 0; q < 4; q++)
-            w[j][q] = load_u64_any(T, p + 8u * q);
+            w[j][q] = load_u64_any(T, pos[j] + 8u * q);
     }
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < kPerT; j++) {
         const uint64_t h = gram_fp(w[j][0], w[j][1], w[j][2], w[j][3]);
-        const uint32_t tag = gram_tag(h);
-        uint32_t slot = gram_slot(h);
+        const uint32_t tag = gram_tag(h), mx = gram_mix(h);
+        uint32_t slot = gram_slot(mx);
+        atomicOr(&filt[gram_fbit(mx) >> 5], 1u << (gram_fbit(mx) & 31u));
         for (uint32_t probe = 0; probe < kProbeSlots; probe++) {  // (the table never fills)
             const uint32_t old = atomicCAS(&key[slot], 0u, tag);
             if (old == 0u || old == tag) {
@@ -202,6 +212,8 @@ __global__ __launch_bounds__(kProbeThreads) void k_repeat_probe(const uint8_t *_
             }
             slot = (slot + 1u) & (kProbeSlots - 1u);
         }
+        if (ptab)
+            pslot[tid + j * kProbeThreads] = slot << 1 | ((pos[j] & 7u) == 0u ? 1u : 0u);
     }
     __syncthreads();
     uint32_t d = 0;
@@ -213,51 +225,64 @@ __global__ __launch_bounds__(kProbeThreads) void k_repeat_probe(const uint8_t *_
             gcnt[i] = 0u;
         }
     }
+    if (ptab)
+        for (uint32_t i = tid; i < kFilterBits / 32; i += kProbeThreads)
+            pfilt[i] = filt[i];
     atomicAdd(&dups, d);
     __syncthreads();
     if (tid == 0)
         *out = dups;
 }
 
-// Every position's 32-gram against the sample table (skipped when the samples decided already:
-// dups[0] * 2 >= kProbe). A thread takes 8 consecutive positions from 5 aligned text words.
+// The 32-gram at every position p = 0 mod 8 against the sample table (skipped when the samples
+// decided already: dups[0] * 2 >= kProbe). A thread takes 8 such positions from 11 aligned text
+// words; a gram whose filter bit is clear (94% of text) goes no further. Hits count per workgroup
+// in LDS (saturating at 2), then once per slot into gcnt.
 constexpr uint32_t kScanThreads = 256;
 __global__ __launch_bounds__(kScanThreads) void k_repeat_scan(const uint8_t *__restrict__ T, uint32_t n,
                                                               const uint32_t *__restrict__ dups,
                                                               const uint32_t *__restrict__ ptab,
+                                                              const uint32_t *__restrict__ pfilt,
                                                               uint32_t *__restrict__ gcnt)
 {
-    __shared__ uint32_t tab[kProbeSlots];  // tag | bit 0: hit once | bit 1: hit twice (this workgroup)
+    __shared__ uint32_t tab[kProbeSlots];  // tag | hits in this workgroup (2 bits, saturating)
+    __shared__ uint32_t filt[kFilterBits / 32];
     if (dups[0] * 2u >= kProbe)
         return;
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < kProbeSlots; i += kScanThreads)
         tab[i] = ptab[i];
+    for (uint32_t i = tid; i < kFilterBits / 32; i += kScanThreads)
+        filt[i] = pfilt[i];
     __syncthreads();
-    const uint32_t last = n - 32u;  // positions 0..last hold a whole 32-gram
+    const uint32_t lastw = (n - 32u) / 8u;  // aligned grams: word indices 0..lastw
     const uint64_t *W = reinterpret_cast<const uint64_t *>(T);
-    for (size_t g = (size_t)blockIdx.x * kScanThreads + tid; g * 8 <= last; g += (size_t)gridDim.x * kScanThreads) {
-        uint64_t x[5];  // (the text buffer is padded past N + 64)
+    for (size_t g = (size_t)blockIdx.x * kScanThreads + tid; g * 8 <= lastw; g += (size_t)gridDim.x * kScanThreads) {
+        uint64_t x[11];  // (the text buffer is padded past N + 64)
 #pragma unroll
-        for (int q = 0; q < 5; q++)
-            x[q] = W[g + q];
+        for (int q = 0; q < 11; q++)
+            x[q] = W[g * 8 + q];
+        uint32_t cand = 0;  // grams whose filter bit is set
+        uint64_t hs[8];
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++) {
-            const uint32_t sh = 8u * j;
-            uint64_t v[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                v[q] = (x[q] >> sh) | ((x[q + 1] << 1) << (63u - sh));
-            const uint64_t h = gram_fp(v[0], v[1], v[2], v[3]);
+            hs[j] = gram_fp(x[j], x[j + 1], x[j + 2], x[j + 3]);
+            const uint32_t fb = gram_fbit(gram_mix(hs[j]));
+            cand |= ((filt[fb >> 5] >> (fb & 31u)) & 1u) << j;
+        }
+        if (g * 8 + 7 > lastw)
+            cand &= (1u << (lastw - g * 8 + 1)) - 1u;
+        while (cand) {
+            const uint32_t j = __builtin_ctz(cand);
+            cand &= cand - 1u;
+            const uint64_t h = hs[j];
             const uint32_t tag = gram_tag(h);
-            uint32_t slot = gram_slot(h);
-            if (g * 8 + j > last)
-                break;
+            uint32_t slot = gram_slot(gram_mix(h));
             for (;;) {
                 const uint32_t e = tab[slot];
                 if (e == 0u)
                     break;
-                if ((e & ~3u) == tag) {
+                if ((e & ~3u) == tag) {  // bit 0: hit once, bit 1: hit twice (or-ed, so never past 3)
                     if (!(e & 2u) && (atomicOr(&tab[slot], 1u) & 1u))
                         atomicOr(&tab[slot], 2u);
                     break;
@@ -274,22 +299,27 @@ __global__ __launch_bounds__(kScanThreads) void k_repeat_scan(const uint8_t *__r
     }
 }
 
-// out[0]: the samples whose 32-gram occurs at least twice in the block.
-__global__ __launch_bounds__(kProbeThreads) void k_repeat_count(const uint32_t *__restrict__ dups,
-                                                                const uint32_t *__restrict__ ptab,
-                                                                const uint32_t *__restrict__ pmul,
-                                                                const uint32_t *__restrict__ gcnt,
-                                                                uint32_t *__restrict__ out)
+// out[0]: the sample points (of kProbePoints) one of whose grams occurs at an aligned position
+// other than its own, or is shared with another sample.
+__global__ __launch_bounds__(kProbePoints) void k_repeat_count(const uint32_t *__restrict__ dups,
+                                                               const uint32_t *__restrict__ pmul,
+                                                               const uint32_t *__restrict__ gcnt,
+                                                               const uint32_t *__restrict__ pslot,
+                                                               uint32_t *__restrict__ out)
 {
     __shared__ uint32_t tot;
     if (threadIdx.x == 0)
         tot = 0;
     __syncthreads();
-    uint32_t r = 0;
+    bool rep = false;
     if (dups[0] * 2u < kProbe)
-        for (uint32_t i = threadIdx.x; i < kProbeSlots; i += kProbeThreads)
-            r += ptab[i] && gcnt[i] >= 2u ? pmul[i] : 0u;
-    atomicAdd(&tot, r);
+        for (uint32_t i = 0; i < 8; i++) {
+            const uint32_t e = pslot[threadIdx.x * 8u + i], sl = e >> 1;
+            rep = rep || pmul[sl] >= 2u || gcnt[sl] >= 1u + (e & 1u);
+        }
+    const uint64_t b = wave_ballot(rep);
+    if (lane_id() == 0)
+        atomicAdd(&tot, (uint32_t)__popcll(b));
     __syncthreads();
     if (threadIdx.x == 0)
         *out = tot;
@@ -963,7 +993,7 @@ __global__ void k_dbg_text(const uint64_t *__restrict__ K, const uint32_t *__res
     if (c >= m)
         return;
     const uint32_t i = V[c];
-    if (i >= bl.npos || bl.end(i) - i <= h0 || K[c] != round0_key_mapped(Tm, i + h0, bl.end(i), a))
+    if (i >= bl.npos || bl.end(i) - i < h0 || K[c] != round0_key_mapped(Tm, i + h0, bl.end(i), a))
         atomicOr(err, 0x80000u);
     else if (c > 0 && (gin[c - 1] > gin[c] || (gin[c - 1] == gin[c] && K[c - 1] > K[c])))
         atomicOr(err, 0x100000u);
@@ -1329,17 +1359,18 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         if (dc3_auto && !dc3_probe_off) {
             // sample table, scan and count in u1 (free until round 0's survivor counts)
             uint32_t *ptab = ws.u1, *pmul = ws.u1 + kProbeSlots, *gcnt = ws.u1 + 2 * kProbeSlots;
+            uint32_t *pfilt = ws.u1 + 3 * kProbeSlots, *pslot = pfilt + kFilterBits / 32;
             hipLaunchKernelGGL(k_repeat_probe, dim3(1), dim3(kProbeThreads), 0, st, ws.text, n, words + 8,
-                               dc3_scan ? ptab : nullptr, pmul, gcnt);
+                               dc3_scan ? ptab : nullptr, pmul, gcnt, pfilt, pslot);
             SALZ_LAUNCH_CHECK();
             if (dc3_scan) {
-                const uint32_t groups = (n - 32u) / 8u + 1u;
+                const uint32_t groups = (n - 32u) / 64u + 1u;  // 8 aligned grams per thread
                 const uint32_t grid = grid_for(groups, kScanThreads) < 1024 ? grid_for(groups, kScanThreads) : 1024;
                 hipLaunchKernelGGL(k_repeat_scan, dim3(grid), dim3(kScanThreads), 0, st, ws.text, n, words + 8,
-                                   ptab, gcnt);
+                                   ptab, pfilt, gcnt);
                 SALZ_LAUNCH_CHECK();
-                hipLaunchKernelGGL(k_repeat_count, dim3(1), dim3(kProbeThreads), 0, st, words + 8, ptab, pmul,
-                                   gcnt, words + 9);
+                hipLaunchKernelGGL(k_repeat_count, dim3(1), dim3(kProbePoints), 0, st, words + 8, pmul, gcnt, pslot,
+                                   words + 9);
                 SALZ_LAUNCH_CHECK();
             }
         }
@@ -1349,7 +1380,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         // of them anywhere in the block (what the depth-32 switch below tests): DC3 from the start
         const uint32_t *hs = reinterpret_cast<const uint32_t *>(ws.hscal);
         dc3_now = dc3_auto && !dc3_probe_off &&
-                  (hs[248] * 2 >= kProbe || (dc3_scan && (uint64_t)hs[249] * 4 >= 3ull * kProbe));
+                  (hs[248] * 2 >= kProbe || (dc3_scan && (uint64_t)hs[249] * 4 >= 3ull * kProbePoints));
         const uint32_t *pw = reinterpret_cast<const uint32_t *>(ws.hscal) + 240;
         uint32_t sigma = 0;
         for (int c = 0; c < 256; c++)

@@ -41,7 +41,10 @@ for name, make in cases.items():
     out = ctx.encode(src)
     t1 = time.perf_counter()
     ok = salz_amd.decode_safe(out, n, frame=True) == src.tobytes()
-    line = f"{name:11s} {n} B -> {len(out)} B  {(t1 - t0) * 1e3:8.1f} ms  {n / (t1 - t0) / 1e6:8.1f} MB/s  roundtrip {ok}"
+    st = ctx.stats()
+    algo = f"dc3 {st['sa_dc3_levels']} levels" if st["sa_dc3_levels"] else f"doubling {st['sa_rounds']} rounds"
+    line = (f"{name:11s} {n} B -> {len(out)} B  {(t1 - t0) * 1e3:8.1f} ms  {n / (t1 - t0) / 1e6:8.1f} MB/s  "
+            f"roundtrip {ok}  sa: {algo}")
     if a.parity:
         rc, ref = oracle_encode(src)
         line += f"  parity {rc == 0 and ref == out}"
