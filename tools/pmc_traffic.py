@@ -6,9 +6,15 @@
 
 Correction (/opt/skills/guides/MI355X_MICROARCH.md, "HBM [CDNA4]"): FETCH_SIZE and WRITE_SIZE
 are in KiB; on gfx950 FETCH_SIZE counts half the bytes of wide streaming reads, so
-traffic = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 per dispatch. Reads narrower than
-16 B per lane are uncalibrated (the guide): treat the absolute as an estimate and the
-ratio to the algorithmic bytes as the signal.
+traffic = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 per dispatch.
+Calibrated for the other access widths in round 5 (profiles/r05i_pmc_calibration.txt,
+tools/gather_bench calib): every L2 -> fabric read request is a 128-B line whatever the width
+(TCC_EA0_RDREQ_128B_sum = TCC_EA0_RDREQ_sum for random 4- and 8-byte reads too) and FETCH_SIZE
+tallies 64 B per request, so the x2 holds for every read; a random 4-byte read costs 1.03 lines,
+an unaligned 8-byte one 1.08. Infinity Cache hits are counted as traffic: a kernel whose random
+side fits the 256 MiB cache can show more than the ~6.3 TB/s HBM delivers (a gather over a
+64 MiB table: 7.0 TB/s). WRITE_SIZE is exact for streaming stores; a random 4- or 16-byte store
+counts one 32-B sector.
 
 Algorithmic bytes of k_radix_scatter: 24 B per element (read 8 B key + 4 B value, write
 8 B key + 4 B value; passes followed by another key pass also write the next digit byte, 25 B,
