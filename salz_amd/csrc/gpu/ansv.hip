@@ -404,6 +404,91 @@ __global__ __launch_bounds__(kT) void k_cand_scatter(const uint32_t *__restrict_
     cand[sidx(p, klog)] = c;
 }
 
+// Second staging level (SALZ_SA=ansv2, large blocks): each text range's run is counting-sorted by
+// its 8 sub-ranges of 2^(rlog - 3) positions in LDS and appended to per-sub-range runs (structure
+// of arrays: positions, then the two halves), so the final scatter writes cand through windows of
+// 2 MB, which an XCD's 4 MB L2 holds whole (its 16-byte stores merge into full lines there instead
+// of leaving L2 as 32-byte partial-sector writes). Not the default: see stage_candidates.
+constexpr uint32_t kRsItems = 16, kRsTile = kT * kRsItems;
+__global__ __launch_bounds__(kT) void k_ansv_restage(const uint32_t *__restrict__ sp, const uint4 *__restrict__ stage,
+                                                     uint32_t rlog, const uint32_t *__restrict__ rfill,
+                                                     uint32_t *__restrict__ sfill, uint32_t *__restrict__ sp2,
+                                                     uint2 *__restrict__ lo2, uint2 *__restrict__ hi2)
+{
+    __shared__ uint32_t cnt[8], base[8];
+    const uint32_t tiles = 1u << (rlog - 12);  // kRsTile = 4096 entries per tile
+    const uint32_t r = blockIdx.x / tiles, k = blockIdx.x % tiles, tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t fill = rfill[r];
+    const size_t t0 = (size_t)k * kRsTile;
+    if (t0 >= fill)
+        return;
+    if (tid < 8)
+        cnt[tid] = 0;
+    __syncthreads();
+    const size_t run = (size_t)r << rlog;
+    const uint32_t sub = rlog - 3;
+    uint32_t pv[kRsItems], loc[kRsItems];
+    uint4 cv[kRsItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kRsItems; j++) {  // every load issued first (clamped, unconditional)
+        const size_t x = t0 + (size_t)j * kT + tid, xc = x < fill ? x : t0;
+        pv[j] = sp[run + xc];
+        cv[j] = stage[run + xc];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kRsItems; j++) {
+        const bool ok = t0 + (size_t)j * kT + tid < fill;
+        const uint32_t b = (pv[j] >> sub) & 7u;
+        uint64_t peers = wave_ballot(ok);
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            const bool bit = (b >> q) & 1u;
+            const uint64_t bb = wave_ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const int leader = peers ? (int)__ffsll((unsigned long long)peers) - 1 : (int)lane;
+        uint32_t old = 0;
+        if (ok && (int)lane == leader)
+            old = atomicAdd(&cnt[b], (uint32_t)__popcll(peers));
+        loc[j] = shfl_u32(old, leader) + count_below(peers);
+    }
+    __syncthreads();
+    if (tid < 8 && cnt[tid])
+        base[tid] = ((r * 8u + tid) << sub) + atomicAdd(&sfill[r * 8u + tid], cnt[tid]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kRsItems; j++) {
+        if (t0 + (size_t)j * kT + tid >= fill)
+            continue;
+        const uint32_t dst = base[(pv[j] >> sub) & 7u] + loc[j];
+        sp2[dst] = pv[j];
+        lo2[dst] = make_uint2(cv[j].x, cv[j].y);
+        hi2[dst] = make_uint2(cv[j].z, cv[j].w);
+    }
+}
+
+// The sub-range runs -> cand, XCD-aware like k_cand_scatter (XCD x takes sub-ranges x, x + 8, ..).
+__global__ __launch_bounds__(kT) void k_cand_scatter2(const uint32_t *__restrict__ sp2, const uint2 *__restrict__ lo2,
+                                                      const uint2 *__restrict__ hi2, uint32_t npos,
+                                                      uint4 *__restrict__ cand, uint32_t klog, uint32_t slog,
+                                                      uint32_t nsub, const uint32_t *__restrict__ sfill,
+                                                      uint32_t *__restrict__ err)
+{
+    const uint32_t g = blockIdx.x, tiles = 1u << (slog - 8);
+    const uint32_t k = g >> 3, r = (g & 7u) + 8u * (k >> (slog - 8));
+    if (r >= nsub)
+        return;
+    const size_t x = (size_t)(k & (tiles - 1u)) * kT + threadIdx.x;
+    if (x >= sfill[r])
+        return;
+    const size_t i = ((size_t)r << slog) + x;
+    const uint32_t p = sp2[i];
+    const uint2 a = lo2[i], b = hi2[i];
+    if (bad_index(p >= npos, err, kErrAnsv))
+        return;
+    cand[sidx(p, klog)] = make_uint4(a.x, a.y, b.x, b.y);
+}
+
 __global__ void k_tree_level(uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp,
                              uint32_t lo, uint32_t cnt)
 {
@@ -563,10 +648,31 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
                        tlcp, stage, sp, rfill, rlog, qp, qpl, qn, qnl, cnt, prof);
     SALZ_LAUNCH_CHECK();
     const uint32_t nranges = (uint32_t)((((uint64_t)npos - 1) >> rlog) + 1);
-    const uint32_t sgrid = 8u * ((nranges + 7u) / 8u) << (rlog - 8);
-    hipLaunchKernelGGL(k_cand_scatter, dim3(sgrid), dim3(kT), 0, st, sp, stage, npos, ws.cand,
-                       ws.klog, rlog, nranges, rfill, derr);
-    SALZ_LAUNCH_CHECK();
+    // SALZ_SA=ansv2: a second staging level for large blocks (cand past 64 MB). Measured slower on
+    // C2 (round 5, tools/ab_env.sh on one box): ANSV 3.65 -> 4.04 ms, the re-sort 0.86 ms and the
+    // 2 MB-window scatter still 1.20 ms against 1.71 ms for the one 16 MB-window scatter, since
+    // every window's lines are written back once it moves on. Kept as a tested option.
+    const bool two = npos > (1u << 22) && env_flag("SALZ_SA", "ansv2") &&
+                     ws.radix_counts_elems >= (size_t)kMaxRanges * 9;
+    if (two) {
+        uint32_t *sfill = rfill + kMaxRanges;  // per sub-range fill
+        SALZ_HIP(hipMemsetAsync(sfill, 0, (size_t)kMaxRanges * 8 * sizeof(uint32_t), st));
+        uint32_t *sp2 = ws.rank;  // (free after the suffix sort; the parse takes it later)
+        uint2 *lo2 = reinterpret_cast<uint2 *>(ws.g64), *hi2 = reinterpret_cast<uint2 *>(ws.pst);
+        hipLaunchKernelGGL(k_ansv_restage, dim3(nranges << (rlog - 12)), dim3(kT), 0, st, sp, stage, rlog, rfill, sfill,
+                           sp2, lo2, hi2);
+        SALZ_LAUNCH_CHECK();
+        const uint32_t slog = rlog - 3, nsub = nranges * 8u;
+        const uint32_t sgrid = 8u * ((nsub + 7u) / 8u) << (slog - 8);
+        hipLaunchKernelGGL(k_cand_scatter2, dim3(sgrid), dim3(kT), 0, st, sp2, lo2, hi2, npos, ws.cand, ws.klog, slog,
+                           nsub, sfill, derr);
+        SALZ_LAUNCH_CHECK();
+    } else {
+        const uint32_t sgrid = 8u * ((nranges + 7u) / 8u) << (rlog - 8);
+        hipLaunchKernelGGL(k_cand_scatter, dim3(sgrid), dim3(kT), 0, st, sp, stage, npos, ws.cand,
+                           ws.klog, rlog, nranges, rfill, derr);
+        SALZ_LAUNCH_CHECK();
+    }
     if (prof) {
         if (read_scalars(ws, 0, (kQCountWord + 2 * kShards) * sizeof(uint32_t), "ansv.prof") != 0)
             return -1;

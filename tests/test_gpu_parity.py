@@ -358,6 +358,22 @@ def test_dc3_edge_sizes(ctx, monkeypatch):
             assert rc == 0 and out == ref, (N, kind)
 
 
+@pytest.mark.parametrize("keys", ["", "ansv2"])
+@pytest.mark.parametrize("kind,n,seed", [("text", 6_000_007, 8), ("mixed", 5_000_001, 9)])
+def test_ansv_staging_levels(ctx, monkeypatch, keys, kind, n, seed):
+    """Candidates of blocks past 2^22 positions through one staging level (the default) or two
+    (SALZ_SA=ansv2: each 2^20-position run re-sorted into 2^17-position sub-runs before the scatter
+    into cand): psv/nsv and their lengths equal the oracle's either way."""
+    monkeypatch.setenv("SALZ_SA", keys)
+    src = gen(kind, n, seed)
+    out, d = ctx.encode_dump(src)
+    o = oracle_stages(src)
+    for k in ("psv", "nsv", "lp", "ln"):
+        i = _first_diff(d[k], o[k])
+        assert i < 0, f"{k} differs at {i}: gpu {d[k][i]} oracle {o[k][i]}"
+    assert out == oracle_encode(src)[1]
+
+
 def test_suffix_sort_round_checks():
     """SALZ_CHECK=rounds,sa (the suffix sorter's per-round invariants, the text round's keys and
     order included, and the final permutation check) pass, and the streams equal the oracle's.
