@@ -114,6 +114,19 @@ int salz_gpu_dist_suffix_array(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t 
                                size_t xcap, uint32_t *d_sa_piece, uint32_t *d_lcp_piece,
                                uint64_t *offsets, int *lcp_ok);
 
+/* The same with the collectives inside the library: RCCL over xGMI on the context's own stream
+ * (no host callback per round; librccl.so.1 is opened at run time). One communicator per rank:
+ * salz_gpu_dist_comm_id on one rank gives the 128-byte id that every rank passes, with its rank,
+ * to salz_gpu_dist_comm_create (collective: it returns once every rank has joined). The
+ * communicator's device must be the context's. */
+typedef struct salz_gpu_dist_comm salz_gpu_dist_comm;
+int salz_gpu_dist_comm_id(uint8_t *id128);
+salz_gpu_dist_comm *salz_gpu_dist_comm_create(int device, int nranks, int rank, const uint8_t *id128);
+void salz_gpu_dist_comm_destroy(salz_gpu_dist_comm *comm);
+int salz_gpu_dist_suffix_array_comm(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t N, salz_gpu_dist_comm *comm,
+                                    uint32_t *d_xsend, uint32_t *d_xrecv, size_t xcap, uint32_t *d_sa_piece,
+                                    uint32_t *d_lcp_piece, uint64_t *offsets, int *lcp_ok);
+
 /* Encode one block from its suffix array (device memory, N - 8 entries, e.g. gathered from the
  * pieces above) and, when d_lcp is not NULL, its LCP array: the LCPs at the nfix positions in
  * lcp_fix (a piece's first entry) are recomputed from the text. The stream goes to device buffer

@@ -117,6 +117,17 @@ lib.salz_gpu_dist_suffix_array.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _sz
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                            ctypes.POINTER(ctypes.c_int)]
 lib.salz_gpu_dist_suffix_array.restype = ctypes.c_int
+lib.salz_gpu_dist_comm_id.argtypes = [ctypes.c_void_p]
+lib.salz_gpu_dist_comm_id.restype = ctypes.c_int
+lib.salz_gpu_dist_comm_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+lib.salz_gpu_dist_comm_create.restype = ctypes.c_void_p
+lib.salz_gpu_dist_comm_destroy.argtypes = [ctypes.c_void_p]
+lib.salz_gpu_dist_comm_destroy.restype = None
+lib.salz_gpu_dist_suffix_array_comm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _sz, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p, _sz, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                                ctypes.POINTER(ctypes.c_int)]
+lib.salz_gpu_dist_suffix_array_comm.restype = ctypes.c_int
 lib.salz_gpu_encode_from_sa.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _sz, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.POINTER(ctypes.c_uint64), _sz, ctypes.c_void_p, _sz, _szp]
 lib.salz_gpu_encode_from_sa.restype = ctypes.c_int

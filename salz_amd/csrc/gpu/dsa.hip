@@ -14,7 +14,18 @@
 //   all-to-all     requests out, then k_dist_answer (rank[j] of the received j) and back
 //   k_dist_place   next round's key of each slot from its answer
 // Ranks whose bucket is sorted keep answering until an allreduce of the survivors is 0.
+// Round 1 of a text block (127 or fewer distinct bytes) is keyed by the text at i + h0, which every
+// rank holds, so it needs no exchange (sa.hip's text round). With one rank, rank[i + h] is local
+// and no collective runs at all (SALZ_SA=xchg forces the exchange there, for measurement).
+//
+// The collectives (DistXchg): the caller's callbacks (salz_dist_ops: torch.distributed from
+// Python, gloo in the tests) or RCCL called from the library on its own stream
+// (salz_gpu_dist_comm: no host callback per round; librccl is opened at run time, so the library
+// links no RCCL for callers that never split a block).
 #include "internal.hpp"
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
 
 #include <cstring>
 #include <vector>
@@ -24,30 +35,72 @@ namespace {
 
 constexpr int kT = 256;
 constexpr uint32_t kClasses = 65536;
-constexpr uint32_t kClassPart = 16384;  // classes counted per pass (64 KB of LDS counters)
 
 __device__ __forceinline__ uint32_t two_byte_class(const uint8_t *T, uint32_t i, uint32_t n)
 {
     return ((uint32_t)T[i] << 8) | (i + 1 < n ? (uint32_t)T[i + 1] : 0u);
 }
 
-// Histogram of the two-byte classes of suffixes 0..n-1 in [lo, lo + kClassPart), LDS-privatised.
-__global__ __launch_bounds__(kT) void k_class_hist(const uint8_t *__restrict__ T, uint32_t n, uint32_t lo,
-                                                   uint32_t *__restrict__ hist)
+// The bucket plan needs the two-byte class histogram only around the bucket boundaries: one pass
+// counts the first bytes; then only the suffixes whose first byte holds a boundary (at most
+// nranks - 1 byte values) count their second byte. Every other class of a byte has that byte's
+// owner. (Round 4 counted all 65536 classes in four passes over the text: 1.1 ms per 100 MB.)
+__global__ __launch_bounds__(kT) void k_byte_hist(const uint8_t *__restrict__ T, uint32_t n,
+                                                  uint32_t *__restrict__ hist)
 {
-    __shared__ uint32_t h[kClassPart];
-    for (uint32_t k = threadIdx.x; k < kClassPart; k += kT)
-        h[k] = 0;
+    __shared__ uint32_t h[4][256];  // one copy per wave
+    for (uint32_t k = threadIdx.x; k < 4 * 256; k += kT)
+        (&h[0][0])[k] = 0;
     __syncthreads();
-    for (size_t i = (size_t)blockIdx.x * kT + threadIdx.x; i < n; i += (size_t)gridDim.x * kT) {
-        const uint32_t c = two_byte_class(T, (uint32_t)i, n) - lo;
-        if (c < kClassPart)
-            atomicAdd(&h[c], 1u);
+    uint32_t *mine = h[threadIdx.x >> 6];
+    for (size_t i = ((size_t)blockIdx.x * kT + threadIdx.x) * 16; i < n; i += (size_t)gridDim.x * kT * 16) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(T + i);  // (padded buffer)
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int b = 0; b < 16; b++)
+            if (i + b < n)
+                atomicAdd(&mine[(w[b >> 2] >> (8 * (b & 3))) & 255u], 1u);
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < kClassPart; k += kT)
+    for (uint32_t k = threadIdx.x; k < 256; k += kT) {
+        const uint32_t v = h[0][k] + h[1][k] + h[2][k] + h[3][k];
+        if (v)
+            atomicAdd(&hist[k], v);
+    }
+}
+
+// Second-byte counts of the suffixes whose first byte is one of the nsplit boundary bytes
+// (slot[first byte] = its index, 0xff otherwise): hist2[slot * 256 + second byte].
+constexpr uint32_t kMaxSplitBytes = 32;  // per pass (32 KB of LDS counters)
+__global__ __launch_bounds__(kT) void k_pair_hist(const uint8_t *__restrict__ T, uint32_t n,
+                                                  const uint8_t *__restrict__ slot, uint32_t nsplit,
+                                                  uint32_t *__restrict__ hist2)
+{
+    __shared__ uint32_t h[kMaxSplitBytes * 256];
+    __shared__ uint8_t sl[256];
+    for (uint32_t k = threadIdx.x; k < nsplit * 256; k += kT)
+        h[k] = 0;
+    for (uint32_t k = threadIdx.x; k < 256; k += kT)
+        sl[k] = slot[k];
+    __syncthreads();
+    for (size_t i = ((size_t)blockIdx.x * kT + threadIdx.x) * 16; i < n; i += (size_t)gridDim.x * kT * 16) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(T + i);  // (padded: byte i + 16 is readable)
+        const uint32_t nx = T[i + 16];
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            const uint32_t c = (w[b >> 2] >> (8 * (b & 3))) & 255u;
+            const uint32_t s = sl[c];
+            if (s != 0xffu && i + b < n) {
+                const uint32_t c2 = b < 15 ? (w[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 255u : nx;
+                atomicAdd(&h[s * 256u + (i + b + 1 < n ? c2 : 0u)], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nsplit * 256; k += kT)
         if (h[k])
-            atomicAdd(&hist[lo + k], h[k]);
+            atomicAdd(&hist2[k], h[k]);
 }
 
 // Own long suffixes (8 or more bytes left), flagged for compaction in text order.
@@ -131,7 +184,7 @@ __global__ void k_dist_place(const uint32_t *__restrict__ slot, const uint32_t *
 int dist_answer_round(Workspace &ws, const DistSa &d, const uint64_t *send_counts)
 {
     std::vector<uint64_t> recv(d.nranks, 0), back(d.nranks, 0);
-    if (d.ops->alltoall(d.ops->user, send_counts, recv.data()) != 0) {
+    if (d.x->alltoall(send_counts, recv.data()) != 0) {
         set_error("split suffix sort: all-to-all of the rank requests failed");
         return -1;
     }
@@ -149,7 +202,7 @@ int dist_answer_round(Workspace &ws, const DistSa &d, const uint64_t *send_count
         SALZ_LAUNCH_CHECK();
     }
     SALZ_HIP(hipStreamSynchronize(ws.stream));
-    if (d.ops->alltoall(d.ops->user, recv.data(), back.data()) != 0) {
+    if (d.x->alltoall(recv.data(), back.data()) != 0) {
         set_error("split suffix sort: all-to-all of the rank answers failed");
         return -1;
     }
@@ -161,6 +214,117 @@ int dist_answer_round(Workspace &ws, const DistSa &d, const uint64_t *send_count
         }
     return 0;
 }
+
+// ---- collectives -------------------------------------------------------------------------------
+struct OpsXchg final : DistXchg {
+    const salz_dist_ops *ops;
+    explicit OpsXchg(const salz_dist_ops *o) : ops(o) {}
+    int alltoall(const uint64_t *sc, uint64_t *rc) override { return ops->alltoall(ops->user, sc, rc); }
+    int allreduce_sum(uint64_t *v) override { return ops->allreduce_sum(ops->user, v); }
+};
+
+// RCCL entry points, opened at run time (the copy already loaded in the process first: torch
+// brings its own; then the ROCm one).
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclAllToAll) all_to_all = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    bool ok = false;
+};
+
+const Rccl &rccl()
+{
+    static Rccl r = [] {
+        Rccl x;
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h)
+            h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h)
+            h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h)
+            return x;
+        auto sym = [&](auto &f, const char *name) {
+            f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));
+            return f != nullptr;
+        };
+        x.ok = sym(x.get_unique_id, "ncclGetUniqueId") && sym(x.comm_init_rank, "ncclCommInitRank") &&
+               sym(x.comm_destroy, "ncclCommDestroy") && sym(x.group_start, "ncclGroupStart") &&
+               sym(x.group_end, "ncclGroupEnd") && sym(x.send, "ncclSend") && sym(x.recv, "ncclRecv") &&
+               sym(x.all_reduce, "ncclAllReduce") && sym(x.all_to_all, "ncclAllToAll") &&
+               sym(x.error_string, "ncclGetErrorString");
+        return x;
+    }();
+    return r;
+}
+
+}  // namespace
+
+// A communicator of the split suffix sort: RCCL over xGMI between the ranks' GPUs, plus 2 * nranks
+// + 1 device words for the counts.
+struct DistComm {
+    ncclComm_t comm = nullptr;
+    int device = 0, nranks = 0, rank = 0;
+    uint64_t *dcnt = nullptr;
+};
+
+namespace {
+
+#define SALZ_NCCL(expr)                                                                             \
+    do {                                                                                            \
+        const ncclResult_t r_ = (expr);                                                             \
+        if (r_ != ncclSuccess) {                                                                    \
+            set_error("%s:%d: %s -> %s", __FILE__, __LINE__, #expr, rccl().error_string(r_));        \
+            return -1;                                                                              \
+        }                                                                                           \
+    } while (0)
+
+struct RcclXchg final : DistXchg {
+    DistComm *c;
+    hipStream_t st;
+    const uint32_t *xsend;
+    uint32_t *xrecv;
+    RcclXchg(DistComm *comm, hipStream_t s, const uint32_t *xs, uint32_t *xr) : c(comm), st(s), xsend(xs), xrecv(xr) {}
+    // counts through one all-to-all of u64 words (read back: they size the data exchange), then the
+    // data as grouped sends and receives on the library's stream
+    int alltoall(const uint64_t *sc, uint64_t *rc) override
+    {
+        const Rccl &R = rccl();
+        const int nr = c->nranks;
+        SALZ_HIP(hipMemcpyAsync(c->dcnt, sc, (size_t)nr * 8, hipMemcpyHostToDevice, st));
+        SALZ_NCCL(R.all_to_all(c->dcnt, c->dcnt + nr, 1, ncclUint64, c->comm, st));
+        SALZ_HIP(hipMemcpyAsync(rc, c->dcnt + nr, (size_t)nr * 8, hipMemcpyDeviceToHost, st));
+        SALZ_HIP(hipStreamSynchronize(st));
+        SALZ_NCCL(R.group_start());
+        size_t so = 0, ro = 0;
+        for (int r = 0; r < nr; r++) {
+            if (sc[r])
+                SALZ_NCCL(R.send(xsend + so, sc[r], ncclUint32, r, c->comm, st));
+            if (rc[r])
+                SALZ_NCCL(R.recv(xrecv + ro, rc[r], ncclUint32, r, c->comm, st));
+            so += sc[r];
+            ro += rc[r];
+        }
+        SALZ_NCCL(R.group_end());
+        return 0;
+    }
+    int allreduce_sum(uint64_t *v) override
+    {
+        const Rccl &R = rccl();
+        uint64_t *d = c->dcnt + 2 * c->nranks;
+        SALZ_HIP(hipMemcpyAsync(d, v, 8, hipMemcpyHostToDevice, st));
+        SALZ_NCCL(R.all_reduce(d, d, 1, ncclUint64, ncclSum, c->comm, st));
+        SALZ_HIP(hipMemcpyAsync(v, d, 8, hipMemcpyDeviceToHost, st));
+        SALZ_HIP(hipStreamSynchronize(st));
+        return 0;
+    }
+};
 
 }  // namespace
 
@@ -200,14 +364,15 @@ int dist_keys(Workspace &ws, const DistSa &d, const uint32_t *nval, const uint32
     return 0;
 }
 
-int dist_idle_rounds(Workspace &ws, const DistSa &d)
+int dist_idle_rounds(Workspace &ws, const DistSa &d, int round)
 {
     const std::vector<uint64_t> none(d.nranks, 0);
-    for (;;) {
-        if (dist_answer_round(ws, d, none.data()) != 0)
+    for (;; round++) {
+        // the keys of round + 1 (none to exchange when it is the text round), then its allreduce
+        if (!(d.text1 && round == 0) && dist_answer_round(ws, d, none.data()) != 0)
             return -1;
         uint64_t g = 0;
-        if (d.ops->allreduce_sum(d.ops->user, &g) != 0) {
+        if (d.x->allreduce_sum(&g) != 0) {
             set_error("split suffix sort: allreduce failed");
             return -1;
         }
@@ -217,7 +382,7 @@ int dist_idle_rounds(Workspace &ws, const DistSa &d)
 }
 
 // This rank's bucket and its suffix array piece (see the file comment). ws.text holds the block.
-int dist_suffix_array(Workspace &ws, uint32_t n, int nranks, int rank, const salz_dist_ops *ops, uint32_t *xsend,
+int dist_suffix_array(Workspace &ws, uint32_t n, int nranks, int rank, DistXchg *x, uint32_t *xsend,
                       uint32_t *xrecv, size_t xcap, uint64_t *offsets, uint32_t *m0_out)
 {
     hipStream_t st = ws.stream;
@@ -232,29 +397,71 @@ int dist_suffix_array(Workspace &ws, uint32_t n, int nranks, int rank, const sal
         SALZ_HIP(hipMalloc(&p, kClasses + kClasses * sizeof(uint32_t)));
         ws.dist_owner = static_cast<uint8_t *>(p);
     }
-    // class histogram, read back; the plan is computed identically on every rank
-    uint32_t *hist = reinterpret_cast<uint32_t *>(ws.dist_owner + kClasses);
-    SALZ_HIP(hipMemsetAsync(hist, 0, kClasses * sizeof(uint32_t), st));
+    // The plan, computed identically on every rank: classes in order, rank r + 1's bucket starts at
+    // the first class whose preceding count reaches n (r + 1) / nranks. First-byte counts, then the
+    // second-byte counts of the bytes a boundary falls strictly inside (the classes of any other
+    // byte all go to one rank).
+    uint32_t *hist = reinterpret_cast<uint32_t *>(ws.dist_owner + kClasses);  // 256 + 256 * splits
+    SALZ_HIP(hipMemsetAsync(hist, 0, 256 * sizeof(uint32_t), st));
     const unsigned g = grid_for(n, kT * 64) < 1024u ? grid_for(n, kT * 64) : 1024u;
-    for (uint32_t lo = 0; lo < kClasses; lo += kClassPart) {
-        hipLaunchKernelGGL(k_class_hist, dim3(g), dim3(kT), 0, st, ws.text, n, lo, hist);
-        SALZ_LAUNCH_CHECK();
-    }
-    std::vector<uint32_t> h(kClasses);
-    if (read_device(ws, hist, kClasses * sizeof(uint32_t), h.data()) != 0)
+    hipLaunchKernelGGL(k_byte_hist, dim3(g), dim3(kT), 0, st, ws.text, n, hist);
+    SALZ_LAUNCH_CHECK();
+    std::vector<uint32_t> h1(256);
+    if (read_device(ws, hist, 256 * sizeof(uint32_t), h1.data()) != 0)
         return -1;
+    std::vector<uint8_t> slot(256, 0xff);
+    std::vector<uint32_t> splits;
+    {
+        uint64_t before = 0;
+        for (uint32_t b = 0; b < 256; b++) {
+            const uint64_t after = before + h1[b];
+            for (int r = 1; r < nranks; r++) {
+                const uint64_t t = (uint64_t)n * r / nranks;
+                if (before < t && t < after && slot[b] == 0xff) {
+                    slot[b] = (uint8_t)splits.size();
+                    splits.push_back(b);
+                }
+            }
+            before = after;
+        }
+    }
+    std::vector<uint32_t> h2(splits.size() * 256, 0);
+    for (size_t s0 = 0; s0 < splits.size(); s0 += kMaxSplitBytes) {
+        const uint32_t ns = (uint32_t)(splits.size() - s0 < kMaxSplitBytes ? splits.size() - s0 : kMaxSplitBytes);
+        std::vector<uint8_t> sl(256, 0xff);
+        for (uint32_t k = 0; k < ns; k++)
+            sl[splits[s0 + k]] = (uint8_t)k;
+        uint8_t *dslot = ws.dist_owner;  // (the owner table is written after the plan)
+        uint32_t *hist2 = hist + 256;
+        SALZ_HIP(hipMemcpyAsync(dslot, sl.data(), 256, hipMemcpyHostToDevice, st));
+        SALZ_HIP(hipMemsetAsync(hist2, 0, (size_t)ns * 256 * sizeof(uint32_t), st));
+        hipLaunchKernelGGL(k_pair_hist, dim3(g), dim3(kT), 0, st, ws.text, n, dslot, ns, hist2);
+        SALZ_LAUNCH_CHECK();
+        if (read_device(ws, hist2, (size_t)ns * 256 * sizeof(uint32_t), h2.data() + s0 * 256) != 0)
+            return -1;
+    }
     std::vector<uint8_t> owner(kClasses);
     uint64_t cum = 0;
     int r = 0;
     offsets[0] = 0;
-    for (uint32_t c = 0; c < kClasses; c++) {
-        // class c starts rank r + 1's bucket once r's share is reached
+    auto advance = [&]() {  // boundaries at the current class start
         while (r + 1 < nranks && cum >= (uint64_t)n * (r + 1) / nranks) {
             r++;
             offsets[r] = cum;
         }
-        owner[c] = (uint8_t)r;
-        cum += h[c];
+    };
+    for (uint32_t b = 0; b < 256; b++) {
+        if (slot[b] == 0xff) {  // no boundary inside: the byte's classes go to one rank
+            advance();
+            memset(owner.data() + b * 256u, r, 256);
+            cum += h1[b];
+            continue;
+        }
+        for (uint32_t c2 = 0; c2 < 256; c2++) {
+            advance();
+            owner[b * 256u + c2] = (uint8_t)r;
+            cum += h2[(size_t)slot[b] * 256 + c2];
+        }
     }
     while (r + 1 < nranks)
         offsets[++r] = cum;
@@ -297,15 +504,23 @@ int dist_suffix_array(Workspace &ws, uint32_t n, int nranks, int rank, const sal
         set_error("split suffix sort: exchange buffers of %zu words for a bucket of %u", xcap, m0);
         return -1;
     }
-    const DistSa d{ops, rank, nranks, ws.dist_owner, list, m0, (uint32_t)offsets[rank], n, xsend, xrecv, xcap};
+    // Round 1 keyed by the text: decided here from the block's alphabet, the same on every rank
+    // (an empty bucket's rank too, whose idle rounds must skip that round's exchange with the rest)
+    const int abits = block_alpha_bits(ws, n);
+    if (abits < 0)
+        return -1;
+    const bool text1 = abits > 0 && !env_flag("SALZ_SA", "rank1");
+    const bool local = nranks == 1 && !env_flag("SALZ_SA", "xchg");
+    const DistSa d{x, rank, nranks, ws.dist_owner, list, m0, (uint32_t)offsets[rank], n, xsend, xrecv, xcap, text1,
+                   local};
     if (m0 == 0) {  // an empty bucket still answers the other ranks until they are done
         SALZ_HIP(hipMemsetAsync(ws.rank + n, 0, sizeof(uint32_t), st));
         uint64_t g = 0;
-        if (ops->allreduce_sum(ops->user, &g) != 0) {
+        if (x->allreduce_sum(&g) != 0) {
             set_error("split suffix sort: allreduce failed");
             return -1;
         }
-        if (g && dist_idle_rounds(ws, d) != 0)
+        if (g && dist_idle_rounds(ws, d, 0) != 0)
             return -1;
     } else {
         const Blocks bl{0xffffffffu, 1u, n};
@@ -316,4 +531,91 @@ int dist_suffix_array(Workspace &ws, uint32_t n, int nranks, int rank, const sal
     return 0;
 }
 
+// ---- C ABI --------------------------------------------------------------------------------------
+int dist_suffix_array_ops(Workspace &ws, uint32_t n, int nranks, int rank, const salz_dist_ops *ops, uint32_t *xsend,
+                          uint32_t *xrecv, size_t xcap, uint64_t *offsets, uint32_t *m0_out)
+{
+    OpsXchg x(ops);
+    return dist_suffix_array(ws, n, nranks, rank, &x, xsend, xrecv, xcap, offsets, m0_out);
+}
+
+int dist_suffix_array_comm(Workspace &ws, uint32_t n, DistComm *c, uint32_t *xsend, uint32_t *xrecv, size_t xcap,
+                           uint64_t *offsets, uint32_t *m0_out)
+{
+    if (c->device != ws.device) {
+        set_error("split suffix sort: communicator of device %d, context of device %d", c->device, ws.device);
+        return -1;
+    }
+    RcclXchg x(c, ws.stream, xsend, xrecv);
+    return dist_suffix_array(ws, n, c->nranks, c->rank, &x, xsend, xrecv, xcap, offsets, m0_out);
+}
+
 }  // namespace salz
+
+extern "C" {
+
+int salz_gpu_dist_comm_id(uint8_t *id)
+{
+    using namespace salz;
+    if (!id) {
+        set_error("NULL argument");
+        return -1;
+    }
+    if (!rccl().ok) {
+        set_error("librccl.so.1 not found (or lacks an entry point): no in-library collectives");
+        return -1;
+    }
+    ncclUniqueId u;
+    SALZ_NCCL(rccl().get_unique_id(&u));
+    memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return 0;
+}
+
+salz_gpu_dist_comm *salz_gpu_dist_comm_create(int device, int nranks, int rank, const uint8_t *id)
+{
+    using namespace salz;
+    if (!id || nranks < 1 || nranks > 255 || rank < 0 || rank >= nranks) {
+        set_error("invalid argument");
+        return nullptr;
+    }
+    if (!rccl().ok) {
+        set_error("librccl.so.1 not found (or lacks an entry point): no in-library collectives");
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        set_error("hipSetDevice(%d) failed", device);
+        return nullptr;
+    }
+    auto *c = new DistComm;
+    c->device = device;
+    c->nranks = nranks;
+    c->rank = rank;
+    ncclUniqueId u;
+    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    const ncclResult_t r = rccl().comm_init_rank(&c->comm, nranks, u, rank);
+    if (r != ncclSuccess || hipMalloc(reinterpret_cast<void **>(&c->dcnt), (2 * (size_t)nranks + 1) * 8) != hipSuccess) {
+        set_error("RCCL communicator (rank %d of %d): %s", rank, nranks,
+                  r != ncclSuccess ? rccl().error_string(r) : "hipMalloc failed");
+        if (c->comm)
+            rccl().comm_destroy(c->comm);
+        delete c;
+        return nullptr;
+    }
+    return reinterpret_cast<salz_gpu_dist_comm *>(c);
+}
+
+void salz_gpu_dist_comm_destroy(salz_gpu_dist_comm *comm)
+{
+    using namespace salz;
+    auto *c = reinterpret_cast<DistComm *>(comm);
+    if (!c)
+        return;
+    (void)hipSetDevice(c->device);
+    if (c->dcnt)
+        (void)hipFree(c->dcnt);
+    if (c->comm)
+        rccl().comm_destroy(c->comm);
+    delete c;
+}
+
+}  // extern "C"

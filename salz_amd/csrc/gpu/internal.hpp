@@ -175,9 +175,16 @@ constexpr uint32_t kMaxBatchBlocks = 4096;
 // stages; every one takes the batch geometry (one block: Blocks{0xffffffff, 1, n})
 // One block's suffix array split over ranks (dsa.hip): this rank sorts the suffixes whose first
 // two bytes fall in its bucket (list, m0 of them, global SA positions gbase ..); rank[i + h] of
-// other buckets comes through the caller's all-to-all (ops).
+// other buckets comes through the exchange (the caller's salz_dist_ops callbacks, or RCCL inside
+// the library: salz_gpu_dist_comm).
+struct DistXchg {
+    virtual ~DistXchg() = default;
+    // all-to-all of u32 words xsend -> xrecv, packed in rank order; recv_counts filled
+    virtual int alltoall(const uint64_t *send_counts, uint64_t *recv_counts) = 0;
+    virtual int allreduce_sum(uint64_t *value) = 0;
+};
 struct DistSa {
-    const struct ::salz_dist_ops *ops;
+    DistXchg *x;
     int rank, nranks;
     const uint8_t *owner;  // device: owning rank per two-byte class (65536)
     const uint32_t *list;  // device: own suffixes in round-0 order
@@ -185,12 +192,24 @@ struct DistSa {
     uint32_t n;               // the block's suffixes
     uint32_t *xsend, *xrecv;  // device exchange buffers (u32 words), xcap each
     size_t xcap;
+    bool text1;   // round 1 keyed by the text (no exchange before it); the same on every rank
+    bool local;   // one rank: rank[i + h] is read here, no collectives at all
 };
-int dist_suffix_array(Workspace &ws, uint32_t n, int nranks, int rank, const salz_dist_ops *ops, uint32_t *xsend,
+int dist_suffix_array(Workspace &ws, uint32_t n, int nranks, int rank, DistXchg *x, uint32_t *xsend,
                       uint32_t *xrecv, size_t xcap, uint64_t *offsets, uint32_t *m0_out);
 int dist_keys(Workspace &ws, const DistSa &d, const uint32_t *nval, const uint32_t *ngid, uint32_t m, uint32_t h,
               int kb, uint64_t *key);
-int dist_idle_rounds(Workspace &ws, const DistSa &d);
+struct DistComm;  // RCCL communicator of the split suffix sort (dsa.hip, salz_gpu_dist_comm)
+int dist_suffix_array_ops(Workspace &ws, uint32_t n, int nranks, int rank, const salz_dist_ops *ops, uint32_t *xsend,
+                          uint32_t *xrecv, size_t xcap, uint64_t *offsets, uint32_t *m0_out);
+int dist_suffix_array_comm(Workspace &ws, uint32_t n, DistComm *c, uint32_t *xsend, uint32_t *xrecv, size_t xcap,
+                           uint64_t *offsets, uint32_t *m0_out);
+// An idle rank (its bucket sorted after round `round`; an empty bucket: round 0, after the first
+// allreduce) keeps answering the others' requests, one exchange and one allreduce per round,
+// until every bucket is sorted.
+int dist_idle_rounds(Workspace &ws, const DistSa &d, int round);
+// The round-0 alphabet's symbol width (0: raw bytes), as stage_suffix_array computes it (sa.hip).
+int block_alpha_bits(Workspace &ws, uint32_t n);
 int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist = nullptr);  // sa.hip -> ws.sa
 // dc3.hip -> ws.sa for one block (repetitive inputs); symbols = codes.code[byte] (1..sigma) or
 // byte + 1 when raw

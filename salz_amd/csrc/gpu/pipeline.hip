@@ -958,16 +958,13 @@ static int encode_host_locked(salz_gpu_ctx *ctx, const uint8_t *src, size_t src_
     return 0;
 }
 
-int salz_gpu_dist_suffix_array(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t N, int nranks, int rank,
-                               const salz_dist_ops *ops, uint32_t *d_xsend, uint32_t *d_xrecv,
-                               size_t xcap, uint32_t *d_sa_piece, uint32_t *d_lcp_piece,
-                               uint64_t *offsets, int *lcp_ok)
+}  // extern "C"
+
+// The split suffix sort's piece of this rank (dsa.hip), through either kind of collectives.
+template <typename Sort>
+static int dist_piece(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t N, uint32_t *d_sa_piece,
+                      uint32_t *d_lcp_piece, int *lcp_ok, Sort sort)
 {
-    if (!ctx || !d_text || !ops || !ops->alltoall || !ops->allreduce_sum || !d_xsend || !d_xrecv ||
-        !d_sa_piece || !d_lcp_piece || !offsets || !lcp_ok) {
-        set_error("NULL argument");
-        return -1;
-    }
     if (N <= 8 || N - 8 >= 0x7fffffffu) {
         set_error("block of %zu bytes: the reference codec needs more than 8 bytes", N);
         return -1;
@@ -983,7 +980,7 @@ int salz_gpu_dist_suffix_array(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t 
     SALZ_HIP(hipMemsetAsync(ws.text + N, 0, 128, st));
     const uint32_t n = (uint32_t)(N - 8);
     uint32_t m0 = 0;
-    if (dist_suffix_array(ws, n, nranks, rank, ops, d_xsend, d_xrecv, xcap, offsets, &m0) != 0)
+    if (sort(ws, n, &m0) != 0)
         return -1;
     if (m0) {
         SALZ_HIP(hipMemcpyAsync(d_sa_piece, ws.sa, (size_t)m0 * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
@@ -994,6 +991,36 @@ int salz_gpu_dist_suffix_array(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t 
     SALZ_HIP(hipStreamSynchronize(st));
     *lcp_ok = m0 == 0 || ws.lcps_ok ? 1 : 0;
     return 0;
+}
+
+extern "C" {
+
+int salz_gpu_dist_suffix_array(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t N, int nranks, int rank,
+                               const salz_dist_ops *ops, uint32_t *d_xsend, uint32_t *d_xrecv,
+                               size_t xcap, uint32_t *d_sa_piece, uint32_t *d_lcp_piece,
+                               uint64_t *offsets, int *lcp_ok)
+{
+    if (!ctx || !d_text || !ops || !ops->alltoall || !ops->allreduce_sum || !d_xsend || !d_xrecv ||
+        !d_sa_piece || !d_lcp_piece || !offsets || !lcp_ok) {
+        set_error("NULL argument");
+        return -1;
+    }
+    return dist_piece(ctx, d_text, N, d_sa_piece, d_lcp_piece, lcp_ok, [&](Workspace &ws, uint32_t n, uint32_t *m0) {
+        return dist_suffix_array_ops(ws, n, nranks, rank, ops, d_xsend, d_xrecv, xcap, offsets, m0);
+    });
+}
+
+int salz_gpu_dist_suffix_array_comm(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t N, salz_gpu_dist_comm *comm,
+                                    uint32_t *d_xsend, uint32_t *d_xrecv, size_t xcap, uint32_t *d_sa_piece,
+                                    uint32_t *d_lcp_piece, uint64_t *offsets, int *lcp_ok)
+{
+    if (!ctx || !d_text || !comm || !d_xsend || !d_xrecv || !d_sa_piece || !d_lcp_piece || !offsets || !lcp_ok) {
+        set_error("NULL argument");
+        return -1;
+    }
+    return dist_piece(ctx, d_text, N, d_sa_piece, d_lcp_piece, lcp_ok, [&](Workspace &ws, uint32_t n, uint32_t *m0) {
+        return dist_suffix_array_comm(ws, n, reinterpret_cast<DistComm *>(comm), d_xsend, d_xrecv, xcap, offsets, m0);
+    });
 }
 
 int salz_gpu_encode_from_sa(salz_gpu_ctx *ctx, const uint8_t *d_src, size_t N, const uint32_t *d_sa,

@@ -1300,6 +1300,27 @@ __global__ void k_putback_text(const uint64_t *__restrict__ KS, const uint32_t *
 
 }  // namespace
 
+int block_alpha_bits(Workspace &ws, uint32_t n)
+{
+    if (env_flag("SALZ_SA", "noalpha") || n < 64)
+        return 0;
+    hipStream_t st = ws.stream;
+    uint32_t *words = reinterpret_cast<uint32_t *>(ws.dscal) + 240;
+    SALZ_HIP(hipMemsetAsync(words, 0, 8 * sizeof(uint32_t), st));
+    const size_t P = (size_t)n + 8;
+    hipLaunchKernelGGL(k_alpha_presence, dim3(grid_for(P, kT * 16) < 2048 ? grid_for(P, kT * 16) : 2048), dim3(kT), 0,
+                       st, ws.text, P, words);
+    SALZ_LAUNCH_CHECK();
+    if (read_scalars(ws, 960, 32, "sa.alpha_bits") != 0)
+        return -1;
+    const uint32_t *pw = reinterpret_cast<const uint32_t *>(ws.hscal) + 240;
+    uint32_t sigma = 0;
+    for (int w = 0; w < 8; w++)
+        sigma += (uint32_t)__builtin_popcount(pw[w]);
+    const int bits = bit_width(sigma);
+    return bits <= 7 ? bits : 0;
+}
+
 int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
 {
     hipStream_t st = ws.stream;
@@ -1433,6 +1454,13 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         hipLaunchKernelGGL(k_list_init, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.text, dist->list, nsa, n, alpha,
                            K, V);
         SALZ_LAUNCH_CHECK();
+        if (dist->text1 && alpha.bits) {  // (the list in u3 is consumed: the mapped text takes its place)
+            tmapped = reinterpret_cast<uint8_t *>(ws.u3);
+            const size_t P = (size_t)n + 8;
+            hipLaunchKernelGGL(k_map_text, dim3(grid_for(P + 64, kT * 16)), dim3(kT), 0, st, ws.text, P, alpha,
+                               tmapped);
+            SALZ_LAUNCH_CHECK();
+        }
     } else if (!text_first) {
         hipLaunchKernelGGL(k_sa_init, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.text, tmapped, bl, alpha, K, V,
                            rdig);
@@ -1472,7 +1500,12 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // Round 1 keyed by text (see k_keys_text): one block or a batch, the block's own sort (not a
     // split block's bucket), an alphabet of at most 127 bytes (symbols >= 1, so zero padding
     // is unambiguous). SALZ_SA=rank1 keeps round 1 on ranks.
-    const bool text1 = !env_flag("SALZ_SA", "rank1") && !dist && alpha.bits > 0;
+    // (a split block: the decision every rank made in dist_suffix_array, from the same alphabet)
+    const bool text1 = dist ? dist->text1 : !env_flag("SALZ_SA", "rank1") && alpha.bits > 0;
+    if (text1 && (!alpha.bits || !tmapped)) {
+        set_error("suffix sort: text round without a compacted alphabet");
+        return -1;
+    }
     const int tbits = (int)(alpha.k * alpha.bits);
     // group ids of the text round's list (its keys are the text): the upper half of lsc, free
     // during every round (the window plan and tile map take its first entries)
@@ -1706,7 +1739,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         if (dist) {  // a split block ends when every rank's bucket is sorted
             constexpr uint64_t kFailedRank = 1ull << 48;
             uint64_t g = failed ? kFailedRank : mnew;
-            if (dist->ops->allreduce_sum(dist->ops->user, &g) != 0) {
+            if (!dist->local && dist->x->allreduce_sum(&g) != 0) {
                 set_error("split suffix sort: allreduce failed");
                 return -1;
             }
@@ -1720,7 +1753,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             if (g == 0)
                 break;
             if (mnew == 0) {  // sorted here: keep answering the other ranks' rank requests
-                if (dist_idle_rounds(ws, *dist) != 0)
+                if (dist_idle_rounds(ws, *dist, ws.stats.sa_rounds - 1) != 0)
                     return -1;
                 break;
             }
@@ -1729,13 +1762,13 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         }
         if (dc3_auto && h >= 32 && (uint64_t)mnew * 4 > (uint64_t)n * 3)
             return stage_suffix_array_dc3(ws, bl, codes, codes_raw);
-        if (dist) {  // rank[i + h] lives with the rank that owns suffix i + h
-            if (dist_keys(ws, *dist, Vx, ngid, mnew, h, kb, Kx) != 0)
-                return -1;
-        } else if (textnext) {  // the text round's keys: the h0 symbols at i + h0
+        if (textnext) {  // the text round's keys: the h0 symbols at i + h0 (every rank holds the text)
             hipLaunchKernelGGL(k_keys_text, dim3(grid_for(mnew, kT)), dim3(kT), 0, st, Vx, mnew, bl, alpha, h,
                                tmapped, Kx);
             SALZ_LAUNCH_CHECK();
+        } else if (dist && !dist->local) {  // rank[i + h] lives with the rank that owns suffix i + h
+            if (dist_keys(ws, *dist, Vx, ngid, mnew, h, kb, Kx) != 0)
+                return -1;
         } else {
             hipLaunchKernelGGL(k_keys, dim3(grid_for(mnew, kT)), dim3(kT), 0, st, Vx, ngid, ws.rank,
                                mnew, n, h, kb, Kx, derr);

@@ -255,63 +255,125 @@ def _gather_pieces(piece, offsets, rank: int, world: int, full, group=None, host
                 dist.recv(full[offsets[r]:offsets[r + 1]], r, group=group)
 
 
-def encode_block_split(src: np.ndarray, device: int = 0, group=None, ctx=None) -> Optional[bytes]:
+class DistComm:
+    """The library's own RCCL communicator for the split suffix sort (salz_gpu_dist_comm): rank 0
+    makes the 128-byte id, the group broadcasts it, every rank joins. The per-round all-to-all
+    and allreduce then run inside the library on its stream, with no callback into Python."""
+
+    def __init__(self, device: int, group=None):
+        import torch
+        import torch.distributed as dist
+
+        import salz_amd
+
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        idb = (ctypes.c_uint8 * 128)()
+        if self.rank == 0 and salz_amd.lib.salz_gpu_dist_comm_id(idb) != 0:
+            raise salz_amd.SalzError(f"RCCL unique id: {salz_amd.last_error()}")
+        obj = [bytes(idb) if self.rank == 0 else None]
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                   group=group, device=torch.device("cuda", device))
+        idb = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
+        self.handle = salz_amd.lib.salz_gpu_dist_comm_create(device, self.world, self.rank, idb)
+        if not self.handle:
+            raise salz_amd.SalzError(f"RCCL communicator: {salz_amd.last_error()}")
+
+    def close(self):
+        import salz_amd
+
+        if self.handle:
+            salz_amd.lib.salz_gpu_dist_comm_destroy(self.handle)
+            self.handle = None
+
+
+def encode_block_split(src, device: int = 0, group=None, ctx=None, comm: Optional[DistComm] = None,
+                       cache: Optional[dict] = None, as_tensor: bool = False):
     """One block encoded with its suffix array split over the ranks of `group` (every rank
-    passes the same block). Each rank sorts its two-byte-prefix bucket on its GPU, exchanging
-    only rank[i + h] requests per doubling round; rank 0 gathers the pieces (and their LCPs) and
-    runs the rest of the pipeline. Returns the stream on rank 0 (bit-identical to
-    salz_encode_safe), None elsewhere."""
+    passes the same block: a host array, or a uint8 tensor on this rank's GPU). Each rank sorts
+    its two-byte-prefix bucket on its GPU, exchanging only rank[i + h] requests per doubling
+    round: through the library's own RCCL communicator when `comm` is given (DistComm, nccl
+    groups), else through torch.distributed callbacks (any backend; gloo stages through host
+    memory). Rank 0 gathers the pieces (and their LCPs) and runs the rest of the pipeline.
+    `cache` (a dict kept by the caller) holds the device buffers across calls. Returns the stream
+    on rank 0 (bit-identical to salz_encode_safe; with as_tensor, the uint8 tensor of it in HBM,
+    a view of the cached output buffer), None elsewhere."""
     import torch
     import torch.distributed as dist
 
     import salz_amd
 
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    s = np.ascontiguousarray(np.asarray(src, dtype=np.uint8).reshape(-1))
-    N = len(s)
-    n = N - 8
     dev = torch.device("cuda", device)
+    if isinstance(src, torch.Tensor):
+        text = src if src.device == dev else src.to(dev)
+    else:
+        s = np.ascontiguousarray(np.asarray(src, dtype=np.uint8).reshape(-1))
+        text = torch.from_numpy(s.copy()).to(dev)
+    N = int(text.numel())
+    n = N - 8
     own = ctx is None
     if own:
         ctx = salz_amd.Context(device, N)
+    bufs = cache if cache is not None else {}
     try:
-        text = torch.from_numpy(s.copy()).to(dev)
-        xcap = N + 64
-        xsend = torch.empty(xcap, dtype=torch.int32, device=dev)
-        xrecv = torch.empty(xcap, dtype=torch.int32, device=dev)
-        sa_piece = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-        lcp_piece = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        if bufs.get("N") != N:
+            xcap = N + 64
+            bufs.update(N=N, xcap=xcap,
+                        xsend=torch.empty(xcap, dtype=torch.int32, device=dev),
+                        xrecv=torch.empty(xcap, dtype=torch.int32, device=dev),
+                        sa_piece=torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                        lcp_piece=torch.empty(max(n, 1), dtype=torch.int32, device=dev))
+            if rank == 0:
+                bufs.update(full_sa=torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                            full_lcp=torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+                            out=torch.empty(salz_amd.encoded_len_max(N), dtype=torch.uint8, device=dev))
+        xsend, xrecv, sa_piece, lcp_piece = bufs["xsend"], bufs["xrecv"], bufs["sa_piece"], bufs["lcp_piece"]
         torch.cuda.synchronize(dev)
-        coll = _Collectives(xsend, xrecv, world, group)
         offs = (ctypes.c_uint64 * (world + 1))()
         lcp_ok = ctypes.c_int(0)
-        rc = salz_amd.lib.salz_gpu_dist_suffix_array(
-            ctx.handle, text.data_ptr(), N, world, rank, ctypes.byref(coll.ops), xsend.data_ptr(),
-            xrecv.data_ptr(), xcap, sa_piece.data_ptr(), lcp_piece.data_ptr(), offs, ctypes.byref(lcp_ok))
+        host = dist.get_backend(group) == "gloo"
+        if comm is not None:
+            rc = salz_amd.lib.salz_gpu_dist_suffix_array_comm(
+                ctx.handle, text.data_ptr(), N, comm.handle, xsend.data_ptr(), xrecv.data_ptr(), bufs["xcap"],
+                sa_piece.data_ptr(), lcp_piece.data_ptr(), offs, ctypes.byref(lcp_ok))
+            err = ""
+        else:
+            coll = _Collectives(xsend, xrecv, world, group)
+            rc = salz_amd.lib.salz_gpu_dist_suffix_array(
+                ctx.handle, text.data_ptr(), N, world, rank, ctypes.byref(coll.ops), xsend.data_ptr(),
+                xrecv.data_ptr(), bufs["xcap"], sa_piece.data_ptr(), lcp_piece.data_ptr(), offs, ctypes.byref(lcp_ok))
+            err = coll.error or ""
         if rc != 0:
-            raise salz_amd.SalzError(f"split suffix sort failed: {salz_amd.last_error()} {coll.error or ''}")
+            raise salz_amd.SalzError(f"split suffix sort failed: {salz_amd.last_error()} {err}")
         offsets = [int(offs[i]) for i in range(world + 1)]
-        ok = torch.tensor([lcp_ok.value], dtype=torch.int64, device=coll.cdev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
-        with_lcp = bool(ok.item())
-        full_sa = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if rank == 0 else None
-        full_lcp = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if rank == 0 and with_lcp else None
-        _gather_pieces(sa_piece, offsets, rank, world, full_sa, group, coll.host)
-        if with_lcp:
-            _gather_pieces(lcp_piece, offsets, rank, world, full_lcp, group, coll.host)
+        if world > 1:
+            ok = torch.tensor([lcp_ok.value], dtype=torch.int64, device="cpu" if host else dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+            with_lcp = bool(ok.item())
+        else:
+            with_lcp = bool(lcp_ok.value)
+        full_sa = bufs.get("full_sa") if rank == 0 else None
+        full_lcp = bufs.get("full_lcp") if rank == 0 and with_lcp else None
+        if world > 1:
+            _gather_pieces(sa_piece, offsets, rank, world, full_sa, group, host)
+            if with_lcp:
+                _gather_pieces(lcp_piece, offsets, rank, world, full_lcp, group, host)
+        else:  # one rank: its piece is the whole array
+            full_sa, full_lcp = sa_piece, (lcp_piece if with_lcp else None)
         if rank != 0:
             return None
         fix = [o for o in offsets[:world] if o < n]  # every piece's first entry
         fixa = (ctypes.c_uint64 * max(len(fix), 1))(*fix)
-        cap = salz_amd.encoded_len_max(N)
-        out = torch.empty(cap, dtype=torch.uint8, device=dev)
+        out = bufs["out"]
         olen = ctypes.c_size_t(0)
         torch.cuda.synchronize(dev)
         if salz_amd.lib.salz_gpu_encode_from_sa(ctx.handle, text.data_ptr(), N, full_sa.data_ptr(),
                                                 full_lcp.data_ptr() if with_lcp else None, fixa,
-                                                len(fix) if with_lcp else 0, out.data_ptr(), cap,
+                                                len(fix) if with_lcp else 0, out.data_ptr(), out.numel(),
                                                 ctypes.byref(olen)) != 0:
             raise salz_amd.SalzError(f"encode from suffix array failed: {salz_amd.last_error()}")
+        if as_tensor:
+            return out[:olen.value]
         return out[:olen.value].cpu().numpy().tobytes()
     finally:
         if own:

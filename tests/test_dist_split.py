@@ -2,7 +2,7 @@
 salz_amd.dist.encode_block_split): each rank sorts its two-byte-prefix bucket on the GPU and
 exchanges rank requests per doubling round; rank 0 gathers the pieces and encodes. The stream
 must equal the CPU port's. The ranks run gloo with host-staged buffers, all on the box's one
-GPU (RCCL refuses two ranks on one device); the RCCL path differs only in the backend."""
+GPU (RCCL refuses two ranks on one device); the library's own RCCL communicator runs at one rank."""
 import os
 import socket
 import subprocess
@@ -35,12 +35,12 @@ def _inputs():
     }
 
 
-def _run_split(tmp_path, world, inputs, *extra):
+def _run_split(tmp_path, world, inputs, *extra, sa_env=""):
     src = tmp_path / "in.npz"
     out = tmp_path / "out.npz"
     np.savez(src, **inputs)
     port = _port()
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", SALZ_SA=sa_env)
     procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "split_worker.py"), str(r), str(world),
                                str(port), str(src), str(out), *extra], env=env, stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT)
@@ -62,9 +62,26 @@ def _run_split(tmp_path, world, inputs, *extra):
         assert got[k].tobytes() == ref, k
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_split_suffix_array_matches_oracle(tmp_path, world):
+    """World 1 reads rank[i + h] locally (no collective); the others exchange requests every
+    doubling round but round 1 of text blocks, which is keyed by the text every rank holds."""
     _run_split(tmp_path, world, _inputs())
+
+
+@pytest.mark.parametrize("world,sa_env", [(1, "xchg"), (2, "rank1"), (3, "rank1,xchg")])
+def test_split_exchange_variants(tmp_path, world, sa_env):
+    """The exchange forced at one rank (SALZ_SA=xchg: requests to itself through the collectives),
+    and round 1 on ranks instead of text (rank1: one exchange more per block, the idle ranks'
+    sequence without the skipped round)."""
+    _run_split(tmp_path, world, _inputs(), sa_env=sa_env)
+
+
+@pytest.mark.parametrize("sa_env", ["", "xchg"])
+def test_split_rccl_comm_one_rank(tmp_path, sa_env):
+    """The library's own RCCL communicator (salz_gpu_dist_comm: nccl backend, one rank on the
+    box's GPU): the collectives run inside the library, forced through the exchange with xchg."""
+    _run_split(tmp_path, 1, _inputs(), "nccl", sa_env=sa_env)
 
 
 def test_split_small_blocks_own_context(tmp_path):
