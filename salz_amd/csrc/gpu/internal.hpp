@@ -160,7 +160,8 @@ constexpr int kMaxDigits = 512;  // 9-bit radix digits (radix.hip)
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
                      const uint8_t *text = nullptr, const Blocks *blocks = nullptr,
-                     const Alpha *alpha = nullptr, uint8_t *digits = nullptr, bool digits_ready = false);
+                     const Alpha *alpha = nullptr, uint8_t *digits = nullptr, bool digits_ready = false,
+                     bool prefer9 = false);
 
 // Stable radix sort of (key, value) pairs whose values are indices into the extraction ranges of
 // GL large groups (lrec[g] >> 32 = start of group g's range, ascending; tmap[t] = the group of

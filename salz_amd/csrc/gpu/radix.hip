@@ -587,9 +587,9 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
 // Measured on one box (round 5, tools/ab_env.sh): a 9-bit pass costs 575 us + 120 us of
 // histogram + 30 us of row scan on C2 against 515 + 84 + 17 for an 8-bit one, so the pass it
 // saves is spent again: C2 SA 19.79 (8-bit) vs 19.95 ms, mixed 100 MB 24.82 vs 24.72 ms.
-static int digit_plan(int bits, bool allow9, int *width)
+static int digit_plan(int bits, bool allow9, bool prefer9, int *width)
 {
-    const bool nine = env_flag("SALZ_SA", "d9");
+    const bool nine = env_flag("SALZ_SA", "d9") || (prefer9 && !env_flag("SALZ_SA", "d8"));
     const int p8 = (bits + 7) / 8, p9 = (bits + 8) / 9;
     if (!allow9 || !nine || p9 >= p8) {
         for (int p = 0; p < p8; p++)
@@ -618,7 +618,7 @@ static void launch_key_scatter(int mode, uint32_t ntiles, hipStream_t st, const 
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
                      uint32_t m, int bit_lo, int bit_hi, Workspace &ws, hipStream_t st,
                      const uint8_t *text, const Blocks *blocks, const Alpha *alpha, uint8_t *digits,
-                     bool digits_ready)
+                     bool digits_ready, bool prefer9)
 {
     if (m <= 1 || bit_hi <= bit_lo)
         return 0;
@@ -639,7 +639,7 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     // 9-bit digits: key passes of 512 threads only (the generic text pass of a batch and the
     // materialised round-0 list's byte digits keep 8 bits)
     int width[64];
-    const int passes_key = digit_plan(bit_hi - bit_lo, !(text && !text_win) && !digits_ready, width);
+    const int passes_key = digit_plan(bit_hi - bit_lo, !(text && !text_win) && !digits_ready, prefer9, width);
     const int passes = passes_key + (blk_bits + 7) / 8;
     bool wide = false;  // a 9-bit pass: every digit array of this sort is 16-bit
     for (int p = 0; p < passes_key; p++)

@@ -1585,7 +1585,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             if (mode_global || mode_seg)
                 seg = mode_seg;
             if (!seg) {
-                if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, bits_all, ws, st, nullptr, nullptr, nullptr, rdig) != 0)
+                if (radix_sort_pairs(&K, &V, Kx, Vx, m, 0, bits_all, ws, st, nullptr, nullptr, nullptr, rdig, false,
+                                     true) != 0)
                     return -1;
             } else {
                 how = "segmented";
@@ -1610,7 +1611,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                     SALZ_LAUNCH_CHECK();
                     uint64_t *KS = KC;
                     uint32_t *VS = VC;
-                    if (radix_sort_pairs(&KS, &VS, Kx, Vx, mL, 0, bits_large, ws, st, nullptr, nullptr, nullptr, rdig) != 0)
+                    if (radix_sort_pairs(&KS, &VS, Kx, Vx, mL, 0, bits_large, ws, st, nullptr, nullptr, nullptr, rdig,
+                                         false, true) != 0)
                         return -1;
                     hipLaunchKernelGGL(k_putback, dim3(grid_for(mL, kT)), dim3(kT), 0, st, KS, VS,
                                        tab.lrec, tab.lg2g, mL, GL, m, kb, K, V, derr);
