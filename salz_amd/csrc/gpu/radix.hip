@@ -56,6 +56,8 @@ __device__ __forceinline__ uint64_t init_key(const TextSrc &t, uint32_t i, const
 // bytes, or 8 / 9 symbols of a mapped text).
 __device__ __forceinline__ uint64_t window_key(uint64_t w, uint32_t w9, uint32_t left, const Alpha &a)
 {
+    if (a.bits == 9)  // 7 raw bytes as symbols byte + 1
+        return raw9_key(w, left);
     if (left < 8)
         w &= (1ull << (8u * left)) - 1ull;
     uint64_t x = __builtin_bswap64(w);
@@ -114,13 +116,16 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
             if (i < left)
                 atomicAdd(&mine[digit_of(kMode, 0, vals[base + i], shift, txt)], 1u);
         }
-    } else if (kMode == 1 && shift == 0 && (txt.a.bits == 0 || ((txt.a.k == 8 || txt.a.k == 9) && txt.a.bits >= 4))) {
+    } else if (kMode == 1 && shift == 0 &&
+               (txt.a.bits == 0 || txt.a.bits == 9 || ((txt.a.k == 8 || txt.a.k == 9) && txt.a.bits >= 4))) {
         // Round 0's first digit is its key's low 8 or 9 bits: the 8th byte (raw keys; 9-bit digits
         // add the 7th byte's low bit), or the last symbol with the low bits of the one before (8
         // or 9 symbols of >= 4 bits): two byte loads per suffix instead of the whole key. Loads
         // unconditional (the text is padded), past the suffix's end masked to 0 like the key's bytes.
+        // (9-bit symbols: the last symbol is the 7th byte + 1, and the one before lies past 9 bits)
         const uint32_t b = txt.a.bits ? txt.a.bits : 8u, kl = txt.a.bits ? txt.a.k - 1u : 7u;
-        const bool prev = txt.a.bits || DB > 8;  // (whether the digit takes bits of the byte before)
+        const bool prev = txt.a.bits ? txt.a.bits < 9 : DB > 8;  // (the digit takes bits of the byte before)
+        const uint32_t inc = txt.a.bits == 9 ? 1u : 0u;
         uint32_t d[kItems];
         if (txt.g.nb == 1 && base >= 7 && left >= (size_t)kTile) {  // (tile-uniform)
             // One block, a whole tile past the short suffixes: entry c is suffix c - 7, so a
@@ -137,7 +142,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
 #pragma unroll
             for (int j = 0; j < kItems; j++) {
                 const uint32_t i = i0 + (uint32_t)j;
-                const uint32_t s7 = i + kl < e ? byte_at((uint32_t)j + 1u) : 0u;
+                const uint32_t s7 = i + kl < e ? byte_at((uint32_t)j + 1u) + inc : 0u;
                 const uint32_t s6 = prev && i + kl - 1u < e ? byte_at((uint32_t)j) : 0u;
                 d[j] = (s7 | (s6 << b)) & kMask;
             }
@@ -150,7 +155,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
             const size_t idx = (size_t)j * kThreads + tid;
             const uint32_t i = init_suffix(idx < left ? base + idx : 0, txt.g), e = txt.g.end(i);
             const uint32_t t7 = txt.T[(size_t)i + kl], t6 = txt.T[(size_t)i + kl - 1u];
-            const uint32_t s7 = i + kl < e ? t7 : 0u, s6 = prev && i + kl - 1u < e ? t6 : 0u;
+            const uint32_t s7 = i + kl < e ? t7 + inc : 0u, s6 = prev && i + kl - 1u < e ? t6 : 0u;
             d[j] = (s7 | (s6 << b)) & kMask;
         }
 #pragma unroll
@@ -635,7 +640,8 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     // (stable), so the list is ordered by (block, key).
     const int blk_bits = blocks && g.nb > 1 ? bit_width(g.nb - 1u) : 0;
     // one block with raw-byte or 8/9-symbol keys: the text pass builds keys from an LDS window
-    const bool text_win = g.nb == 1 && g.npos >= 7 && (!alpha || alpha->bits == 0 || alpha->k == 8 || alpha->k == 9);
+    const bool text_win = g.nb == 1 && g.npos >= 7 &&
+                          (!alpha || alpha->bits == 0 || alpha->bits == 9 || alpha->k == 8 || alpha->k == 9);
     // 9-bit digits: key passes of 512 threads only (the generic text pass of a batch and the
     // materialised round-0 list's byte digits keep 8 bits)
     int width[64];

@@ -1420,6 +1420,16 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             // 22.2 -> 21.6 ms against 8 symbols, profiles/r03g_alpha9_ab.txt).
             alpha.bits = bits;
             alpha.k = 64u / bits;
+        } else if (bl.nb == 1 && !dist && env_flag("SALZ_SA", "rawtext")) {
+            // SALZ_SA=rawtext: more than 127 distinct bytes (binary or mixed data) keyed so that
+            // round 1 can be keyed by the text too (symbols >= 1): 8 symbols of 8 bits for 128..255
+            // distinct bytes (the depth of raw keys), 7 of 9 bits (byte + 1) for all 256 (depth 7).
+            // Not the default: on the mixed input the SA went 24.76 -> 25.57 ms and C3 2977 ->
+            // 2897 MB/s (round 5, tools/ab_env.sh on one box). Its long repeats leave large groups
+            // at depth 7 whose 63-bit text keys take 8 radix passes plus the group passes, where a
+            // rank round sorts (large group, rank) in 4 or 5; and round 0 at depth 7 finishes fewer.
+            alpha.bits = sigma <= 255 ? 8u : 9u;
+            alpha.k = sigma <= 255 ? 8u : 7u;
         }
     }
     if (dc3_force || dc3_now)
@@ -1430,7 +1440,9 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // round): one byte per position, zero padded. (A split block's bucket list lives in u3 and
     // its round 0 reads the raw text: no mapped copy there.)
     uint8_t *tmapped = nullptr;
-    if (alpha.bits && !dist) {
+    if (alpha.bits == 9) {
+        tmapped = ws.text;  // (9-bit symbols are the raw bytes + 1: nothing to map)
+    } else if (alpha.bits && !dist) {
         tmapped = reinterpret_cast<uint8_t *>(ws.u3);
         const size_t P = (size_t)n + 8;
         hipLaunchKernelGGL(k_map_text, dim3(grid_for(P + 64, kT * 16)), dim3(kT), 0, st, ws.text, P, alpha,

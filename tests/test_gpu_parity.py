@@ -258,19 +258,22 @@ def test_encode_batch_grows_workspace(salz, cap, block, size):
 
 
 @pytest.mark.parametrize("keys", ["", "noalpha", "tiny=2048", "tiny=0", "rank1", "rank1,tiny=2048",
-                                  "noalpha,tiny=2048", "d9", "rank1,d9"])
+                                  "noalpha,tiny=2048", "d9", "rank1,d9", "rawtext"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
                                                ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
                                                ("smx", 150000, 3, 20), ("runs", 120000, 0, 0),
                                                ("zeros", 70000, 0, 0), ("smx", 300000, 4, 100),
-                                               ("runs40", 700001, 0, 0)])
+                                               ("runs40", 700001, 0, 0), ("smx", 250000, 8, 200)])
 def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
     """Both doubling-round sorts (global radix on (group, rank); LDS sort of small groups +
     extracted large groups; SALZ_SA=global / segmented), with round-0 keys from the compacted
     alphabet (the default for texts of <= 127 distinct bytes: 2 to 32 symbols per key) or raw
-    bytes ("noalpha"), give the unique suffix array; round 1 keyed by the text at i + h0 (the
-    default for such alphabets) or by ranks ("rank1"); groups of up to 128 members (rank rounds)
+    bytes ("noalpha"), give the unique suffix array; blocks of more than 127 distinct bytes with raw
+    8-byte keys (the default) or with symbols >= 1 ("rawtext": 8-bit codes for 128..255 distinct
+    bytes, byte + 1 as 9-bit symbols for all 256, 7 per key) so that round 1 can be keyed by text;
+    round 1 keyed by the text at i + h0 (the default for alphabets of symbols >= 1) or by ranks
+    ("rank1"); groups of up to 128 members (rank rounds)
     or 256 (the text round) placed by counting and larger ones by LSD passes in LDS (the
     default), every group by counting ("tiny=2048"), or every group by the LSD passes ("tiny=0":
     on the repetitive small-alphabet "runs40" block the text round's LSD leaves runs of equal top
