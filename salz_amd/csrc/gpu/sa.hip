@@ -1417,7 +1417,9 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             // As many symbols as fit 64 bits: 7-bit alphabets (text) sort round 0 to depth 9 in
             // 8 passes rather than depth 8 in 7; the deeper start leaves fewer suffixes to the
             // doubling rounds (text surrogate: 12% fewer after round 0, 14% after round 1; C2 SA
-            // 22.2 -> 21.6 ms against 8 symbols, profiles/r03g_alpha9_ab.txt).
+            // 22.2 -> 21.6 ms against 8 symbols, profiles/r03g_alpha9_ab.txt). Re-measured with
+            // the text round (round 5, one box): 8 symbols 20.6 ms against 19.9, enwik9-sized
+            // blocks 12.3 against 11.9.
             alpha.bits = bits;
             alpha.k = 64u / bits;
         } else if (bl.nb == 1 && !dist && env_flag("SALZ_SA", "rawtext")) {
