@@ -632,7 +632,8 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
     // Staging: text ranges of 2^rlog positions (cand windows of 16 << rlog bytes; 16 MB by
     // default: 2^19 and 2^21 measured slower), at most kMaxRanges of them. Slots sp / stage
     // alias scratch that is free here.
-    uint32_t rlog = 20;
+    uint32_t rlog = (uint32_t)env_num("SALZ_SA", "rlog", 20);  // (test switch: staging range size)
+    rlog = rlog < 17 ? 17 : rlog > 26 ? 26 : rlog;
     while ((((uint64_t)npos - 1) >> rlog) + 1 > kMaxRanges)
         rlog++;
     uint32_t *rfill = ws.radix_counts;
