@@ -169,6 +169,18 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
 // becomes sorted by (group, key) (sa.hip's text round).
 int radix_sort_by_group(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt, uint32_t m,
                         const uint64_t *lrec, const uint32_t *tmap, uint32_t GL, Workspace &ws, hipStream_t st);
+// A list of whole radix tiles cut into segments sorted each on its own (sa.hip's large groups of a
+// rank round): segment s owns tiles [pt0[s], pt0[s] + ptn[s]), its entries first; tile t belongs
+// to segment tseg[t] and holds tcnt[t] entries; segtot: scratch of kMaxDigits words per segment.
+struct SegTiles {
+    const uint32_t *tseg, *tcnt, *pt0, *ptn;
+    uint32_t *segtot;
+    uint32_t ntiles, mvalid;  // (mvalid: entries in all, for the pass statistics)
+};
+constexpr uint32_t kSegScanMaxTiles = 512 * 24;  // one LDS row per digit (radix.hip k_radix_segscan)
+// Stable sort of every segment on key bits [0, bits) (digits: 2 bytes per list slot of scratch).
+int radix_sort_segmented(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
+                         const SegTiles &sg, int bits, Workspace &ws, hipStream_t st, uint8_t *digits);
 
 // Blocks per batch (one pipeline pass over several blocks, common.hpp Blocks).
 constexpr uint32_t kMaxBatchBlocks = 4096;

@@ -90,9 +90,10 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
                                                          uint32_t m, int shift,
                                                          uint32_t *__restrict__ counts,
                                                          uint32_t ntiles, TextSrc txt,
-                                                         const uint8_t *__restrict__ dig)
+                                                         const uint32_t *__restrict__ tcnt)
 {
-    (void)dig;  // (digit arrays are counted by k_radix_hist_dig)
+    // (tcnt: a segmented sort's entries per tile, radix_sort_segmented; digit arrays are counted
+    // by k_radix_hist_dig)
     // Sub-histograms (8 per wave by lane & 7 for 8-bit digits, 4 per wave by lane & 3 for 9-bit
     // ones), ND + 1 words apart so the copies of one digit sit in different banks: lanes of a wave
     // adding to a hot digit (text keys' leading bytes are skewed) spread over several addresses
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
     // Two keys per 16-byte load: pair j of thread t is keys 2 (j * kThreads + t) and + 1.
     const size_t base = (size_t)blockIdx.x * kTile;
     const uint4 *kp = reinterpret_cast<const uint4 *>(keys + base);
-    const size_t left = m > base ? m - base : 0;
+    const size_t left = tcnt ? tcnt[blockIdx.x] : m > base ? m - base : 0;
     if (kMode == 2 || kMode == 4) {
         for (int j = 0; j < kItems; j++) {
             const size_t i = (size_t)j * kThreads + tid;
@@ -212,7 +213,8 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
 // 100 M digits, latency-bound).
 template <typename DT, int DB>
 __global__ __launch_bounds__(kThreads) void k_radix_hist_dig(const DT *__restrict__ dig, uint32_t m,
-                                                             uint32_t *__restrict__ counts, uint32_t ntiles)
+                                                             uint32_t *__restrict__ counts, uint32_t ntiles,
+                                                             const uint32_t *__restrict__ tcnt)
 {
     // (9-bit digits: 8 copies, 2 per wave, so that the LDS stays at 16 KB: 8 workgroups per CU)
     constexpr int ND = 1 << DB, kStride = ND + 1, kDigCopies = DB == 8 ? 16 : 8, kPerWave = kDigCopies / 4;
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist_dig(const DT *__restric
     __shared__ uint32_t h[kDigCopies * kStride];
     const unsigned tid = threadIdx.x, wave = tid >> 6;
     const size_t base = (size_t)blockIdx.x * kTile;
-    const size_t left = m - base;
+    const size_t left = tcnt ? tcnt[blockIdx.x] : m - base;
     // (the digit buffer has room past m: the loads are unconditional)
     const uint4 *src = reinterpret_cast<const uint4 *>(dig + base + (size_t)tid * kItems);
     uint4 x[kLoads];
@@ -320,6 +322,74 @@ __global__ __launch_bounds__(TH) void k_radix_rowscan(uint32_t *__restrict__ cou
         totals[blockIdx.x] = carry;
 }
 
+// Segmented sort (radix_sort_segmented): the row of digit d (blockIdx.x) in LDS at once (at most
+// TH * IT tiles), scanned over all tiles as above, then made relative to the first tile of each
+// tile's segment; the segment's first tile also writes the segment's total of digit d
+// (segtot[seg * nd + d]), whose scan over the digits k_radix_scatter does per tile.
+template <int TH, int IT>
+__global__ __launch_bounds__(TH) void k_radix_segscan(uint32_t *__restrict__ counts, uint32_t ntiles,
+                                                      const uint32_t *__restrict__ tseg,
+                                                      const uint32_t *__restrict__ pt0,
+                                                      const uint32_t *__restrict__ ptn,
+                                                      uint32_t *__restrict__ segtot, uint32_t nd)
+{
+    constexpr uint32_t kStep = TH * IT;
+    __shared__ uint32_t buf[kStep + kStep / 32 + 1];
+    __shared__ uint32_t wsum[TH / 64];
+    uint32_t *row = counts + (size_t)blockIdx.x * ntiles;
+    const unsigned tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+        const uint32_t i = j * TH + tid;
+        buf[rs_pad(i)] = i < ntiles ? row[i] : 0u;
+    }
+    __syncthreads();
+    uint32_t v[IT], sum = 0;
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+        v[j] = buf[rs_pad(tid * IT + j)];
+        sum += v[j];
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (unsigned d = 1; d < 64; d <<= 1) {
+        const uint32_t y = shfl_up_u32(x, d);
+        if (lane >= d)
+            x += y;
+    }
+    if (lane == 63)
+        wsum[wave] = x;
+    __syncthreads();
+    uint32_t pre = 0, all = 0;
+#pragma unroll
+    for (unsigned w = 0; w < TH / 64; w++) {
+        const uint32_t ws = wsum[w];
+        pre += w < wave ? ws : 0u;
+        all += ws;
+    }
+    uint32_t run = pre + x - sum;
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+        buf[rs_pad(tid * IT + j)] = run;
+        run += v[j];
+    }
+    if (tid == 0)
+        buf[rs_pad(kStep)] = all;  // (the prefix past the last tile)
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+        const uint32_t i = j * TH + tid;
+        if (i < ntiles) {
+            const uint32_t sg = tseg[i], t0 = pt0[sg], p0 = buf[rs_pad(t0)];
+            row[i] = buf[rs_pad(i)] - p0;
+            if (i == t0) {
+                const uint32_t t1 = t0 + ptn[sg];
+                segtot[(size_t)sg * nd + blockIdx.x] = buf[rs_pad(t1 < ntiles ? t1 : kStep)] - p0;
+            }
+        }
+    }
+}
+
 void radix_rowscan(uint32_t *counts, uint32_t ntiles, uint32_t *totals, hipStream_t st, uint32_t ndig)
 {
     if (ntiles <= 256 * 16)
@@ -349,8 +419,12 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
     uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t m, int shift,
     const uint32_t *__restrict__ offs, uint32_t ntiles, const uint32_t *__restrict__ totals,
-    TextSrc txt, DT *__restrict__ dout, int nshift, uint32_t nmask)
+    TextSrc txt, DT *__restrict__ dout, int nshift, uint32_t nmask, const uint32_t *__restrict__ tcnt,
+    const uint32_t *__restrict__ tseg, const uint32_t *__restrict__ pt0)
 {
+    // Segmented sort (tseg set, radix_sort_segmented): tile `tile` holds tcnt[tile] entries of
+    // segment tseg[tile], whose output starts at tile pt0[seg]; offs are offsets inside the
+    // segment and totals its digit totals (ND per segment).
     constexpr int IT = kTile / TH, NW = TH / 64, ND = 1 << DB, DW = ND / 64;
     constexpr uint32_t kMask = ND - 1;
     static_assert(ND <= TH, "one thread per digit");
@@ -369,6 +443,8 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     for (int i = tid; i < NW * ND; i += TH)
         (&cnt[0][0])[i] = 0;
     __syncthreads();
+    const size_t lim = tcnt ? (size_t)tile * kTile + tcnt[tile] : (size_t)m;  // entries end
+    const uint32_t sg = tseg ? tseg[tile] : 0u;
 
     // Warp-striped: wave w owns tile elements [w*IT*64, (w+1)*IT*64), item j covers 64 of them.
     const size_t base = (size_t)tile * kTile + (size_t)wave * (IT * 64);
@@ -417,7 +493,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
         if (kMode == 3)
             break;
         size_t i = base + (size_t)j * 64 + lane;
-        bool ok = i < m;
+        bool ok = i < lim;
         if (kMode == 1) {  // unconditional text loads (clamped entry)
             const uint32_t sfx = init_suffix(ok ? i : 0, txt.g);
             const uint64_t kk = init_key(txt, sfx, nullptr);
@@ -432,7 +508,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
 #pragma unroll
     for (int j = 0; j < IT; j++) {
         size_t i = base + (size_t)j * 64 + lane;
-        bool ok = i < m;
+        bool ok = i < lim;
         unsigned d = digit_of(kMode, k[j], v[j], shift, txt) & kMask;
         uint64_t peers = wave_ballot(ok);
 #pragma unroll
@@ -462,7 +538,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     const bool dg = tid < ND;
     uint32_t xt = 0, xc = 0, tt = 0, tot = 0;
     if (dg) {
-        tt = totals[tid];
+        tt = totals[tseg ? (size_t)sg * ND + tid : tid];
 #pragma unroll
         for (int w = 0; w < NW; w++)
             tot += cnt[w][tid];
@@ -488,7 +564,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
             pt += wsum[0][w];
             pc += wsum[1][w];
         }
-        gbase[tid] = pt + xt - tt + offs[(size_t)tid * ntiles + tile];
+        gbase[tid] = pt + xt - tt + offs[(size_t)tid * ntiles + tile] + (tseg ? pt0[sg] * (uint32_t)kTile : 0u);
         const uint32_t ds = pc + xc - tot;
         dstart[tid] = ds;
         uint32_t run = 0;
@@ -549,13 +625,13 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
         size_t i = base + (size_t)j * 64 + lane;
         unsigned d = (unsigned)(k[j] >> shift) & kMask;
         pos[j] = dstart[d] + cnt[wave][d] + lrank[j];
-        if (i < m)
+        if (i < lim)
             skey[pos[j]] = k[j];
     }
     __syncthreads();
 
     size_t tbase = (size_t)tile * kTile;
-    uint32_t tcount = (uint32_t)((m - tbase) < (size_t)kTile ? (m - tbase) : (size_t)kTile);
+    uint32_t tcount = (uint32_t)((lim - tbase) < (size_t)kTile ? (lim - tbase) : (size_t)kTile);
     uint32_t gdst[IT];  // global destination of staged slot tid + j * TH
 #pragma unroll
     for (int j = 0; j < IT; j++) {
@@ -573,7 +649,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
 #pragma unroll
     for (int j = 0; j < IT; j++) {
         size_t i = base + (size_t)j * 64 + lane;
-        if (i < m)
+        if (i < lim)
             sval[pos[j]] = v[j];
     }
     __syncthreads();
@@ -610,14 +686,16 @@ static int digit_plan(int bits, bool allow9, bool prefer9, int *width)
 template <int DB, typename DT>
 static void launch_key_scatter(int mode, uint32_t ntiles, hipStream_t st, const uint64_t *kin, const uint32_t *vin,
                                uint64_t *kout, uint32_t *vout, uint32_t m, int shift, const uint32_t *counts,
-                               const uint32_t *totals, const TextSrc &txt, DT *dout, int nshift, uint32_t nmask)
+                               const uint32_t *totals, const TextSrc &txt, DT *dout, int nshift, uint32_t nmask,
+                               const uint32_t *tcnt = nullptr, const uint32_t *tseg = nullptr,
+                               const uint32_t *pt0 = nullptr)
 {
     if (mode == 3)
         hipLaunchKernelGGL((k_radix_scatter<3, 512, DB, DT>), dim3(ntiles), dim3(512), 0, st, kin, vin, kout, vout,
-                           m, shift, counts, ntiles, totals, txt, dout, nshift, nmask);
+                           m, shift, counts, ntiles, totals, txt, dout, nshift, nmask, tcnt, tseg, pt0);
     else
         hipLaunchKernelGGL((k_radix_scatter<0, 512, DB, DT>), dim3(ntiles), dim3(512), 0, st, kin, vin, kout, vout,
-                           m, shift, counts, ntiles, totals, txt, dout, nshift, nmask);
+                           m, shift, counts, ntiles, totals, txt, dout, nshift, nmask, tcnt, tseg, pt0);
 }
 
 int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
@@ -679,13 +757,13 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
             const uint16_t *d16 = reinterpret_cast<const uint16_t *>(dig_in);
             if (db == 9)
                 hipLaunchKernelGGL((k_radix_hist_dig<uint16_t, 9>), dim3(ntiles), dim3(kThreads), 0, st, d16, m,
-                                   ws.radix_counts, ntiles);
+                                   ws.radix_counts, ntiles, nullptr);
             else
                 hipLaunchKernelGGL((k_radix_hist_dig<uint16_t, 8>), dim3(ntiles), dim3(kThreads), 0, st, d16, m,
-                                   ws.radix_counts, ntiles);
+                                   ws.radix_counts, ntiles, nullptr);
         } else if (dig_in) {
             hipLaunchKernelGGL((k_radix_hist_dig<uint8_t, 8>), dim3(ntiles), dim3(kThreads), 0, st, dig_in, m,
-                               ws.radix_counts, ntiles);
+                               ws.radix_counts, ntiles, nullptr);
         } else if (db == 9) {
             hipLaunchKernelGGL((k_radix_hist<0, 9>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, shift,
                                ws.radix_counts, ntiles, txt, nullptr);
@@ -704,10 +782,11 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
             SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used], st));
         if (mode == 1)
             hipLaunchKernelGGL((k_radix_scatter<1, kThreads, 8, uint8_t>), dim3(ntiles), dim3(kThreads), 0, st, kin,
-                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift, nmask);
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, dig_out, nshift, nmask, nullptr,
+                               nullptr, nullptr);
         else if (mode == 2)
             hipLaunchKernelGGL((k_radix_scatter<2, kThreads, 8, uint8_t>), dim3(ntiles), dim3(kThreads), 0, st, kin,
-                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, nullptr, 0, 0u);
+                               vin, kout, vout, m, shift, ws.radix_counts, ntiles, totals, txt, nullptr, 0, 0u, nullptr, nullptr, nullptr);
         else if (wide && db == 9)
             launch_key_scatter<9, uint16_t>(mode, ntiles, st, kin, vin, kout, vout, m, shift, ws.radix_counts, totals,
                                             txt, reinterpret_cast<uint16_t *>(dig_out), nshift, nmask);
@@ -762,7 +841,7 @@ int radix_sort_by_group(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, ui
         radix_rowscan(ws.radix_counts, ntiles, totals, st, 256);
         SALZ_LAUNCH_CHECK();
         hipLaunchKernelGGL((k_radix_scatter<4, kThreads, 8, uint8_t>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin,
-                           kout, vout, m, 8 * pass, ws.radix_counts, ntiles, totals, txt, nullptr, 0, 0u);
+                           kout, vout, m, 8 * pass, ws.radix_counts, ntiles, totals, txt, nullptr, 0, 0u, nullptr, nullptr, nullptr);
         SALZ_LAUNCH_CHECK();
         uint64_t *tk = kin;
         kin = kout;
@@ -770,6 +849,79 @@ int radix_sort_by_group(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, ui
         uint32_t *tv = vin;
         vin = vout;
         vout = tv;
+    }
+    *keys = kin;
+    *vals = vin;
+    return 0;
+}
+
+int radix_sort_segmented(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint32_t *vals_alt,
+                         const SegTiles &sg, int bits, Workspace &ws, hipStream_t st, uint8_t *digits)
+{
+    const uint32_t ntiles = sg.ntiles, m = ntiles * (uint32_t)kTile;
+    const size_t ncounts = (size_t)ntiles * kMaxDigits;
+    if (ntiles > kSegScanMaxTiles || ncounts + kMaxDigits > ws.radix_counts_elems || !digits) {
+        set_error("radix: segmented sort too large");
+        return -1;
+    }
+    uint64_t *kin = *keys, *kout = keys_alt;
+    uint32_t *vin = *vals, *vout = vals_alt;
+    int width[64];
+    const int passes = digit_plan(bits, true, true, width);
+    bool wide = false;
+    for (int p = 0; p < passes; p++)
+        wide |= width[p] > 8;
+    const TextSrc txt{nullptr, Blocks{0xffffffffu, 1u, m}, Alpha{}, nullptr, nullptr, 0u};
+    int shift = 0;
+    for (int pass = 0; pass < passes; pass++) {
+        const int db = width[pass], nshift = shift + db;
+        const uint32_t nmask = pass + 1 < passes ? (1u << width[pass + 1]) - 1u : 255u;
+        uint8_t *dig_out = pass + 1 < passes ? digits : nullptr;
+        const uint16_t *d16 = reinterpret_cast<const uint16_t *>(digits);
+        if (pass == 0 && db == 9)
+            hipLaunchKernelGGL((k_radix_hist<0, 9>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, shift,
+                               ws.radix_counts, ntiles, txt, sg.tcnt);
+        else if (pass == 0)
+            hipLaunchKernelGGL((k_radix_hist<0, 8>), dim3(ntiles), dim3(kThreads), 0, st, kin, vin, m, shift,
+                               ws.radix_counts, ntiles, txt, sg.tcnt);
+        else if (wide && db == 9)
+            hipLaunchKernelGGL((k_radix_hist_dig<uint16_t, 9>), dim3(ntiles), dim3(kThreads), 0, st, d16, m,
+                               ws.radix_counts, ntiles, sg.tcnt);
+        else if (wide)
+            hipLaunchKernelGGL((k_radix_hist_dig<uint16_t, 8>), dim3(ntiles), dim3(kThreads), 0, st, d16, m,
+                               ws.radix_counts, ntiles, sg.tcnt);
+        else
+            hipLaunchKernelGGL((k_radix_hist_dig<uint8_t, 8>), dim3(ntiles), dim3(kThreads), 0, st, digits, m,
+                               ws.radix_counts, ntiles, sg.tcnt);
+        SALZ_LAUNCH_CHECK();
+        hipLaunchKernelGGL((k_radix_segscan<512, 24>), dim3(1u << db), dim3(512), 0, st, ws.radix_counts, ntiles,
+                           sg.tseg, sg.pt0, sg.ptn, sg.segtot, 1u << db);
+        SALZ_LAUNCH_CHECK();
+        const bool timed = ws.timing && ws.rx_used + 2 <= ws.rx_pool.size();
+        if (timed)
+            SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used], st));
+        if (wide && db == 9)
+            launch_key_scatter<9, uint16_t>(0, ntiles, st, kin, vin, kout, vout, m, shift, ws.radix_counts, sg.segtot,
+                                            txt, reinterpret_cast<uint16_t *>(dig_out), nshift, nmask, sg.tcnt,
+                                            sg.tseg, sg.pt0);
+        else if (wide)
+            launch_key_scatter<8, uint16_t>(0, ntiles, st, kin, vin, kout, vout, m, shift, ws.radix_counts, sg.segtot,
+                                            txt, reinterpret_cast<uint16_t *>(dig_out), nshift, nmask, sg.tcnt,
+                                            sg.tseg, sg.pt0);
+        else
+            launch_key_scatter<8, uint8_t>(0, ntiles, st, kin, vin, kout, vout, m, shift, ws.radix_counts, sg.segtot,
+                                           txt, dig_out, nshift, nmask, sg.tcnt, sg.tseg, sg.pt0);
+        SALZ_LAUNCH_CHECK();
+        if (timed) {
+            SALZ_HIP(hipEventRecord(ws.rx_pool[ws.rx_used + 1], st));
+            ws.rx_used += 2;
+            ws.stats.radix_scatter_launches++;
+            ws.stats.radix_scatter_elems += sg.mvalid;
+            ws.stats.radix_scatter_bytes += (uint64_t)sg.mvalid * (dig_out ? (wide ? 26u : 25u) : 24u);
+        }
+        shift += db;
+        std::swap(kin, kout);
+        std::swap(vin, vout);
     }
     *keys = kin;
     *vals = vin;

@@ -495,6 +495,7 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
                 const uint32_t lg = (uint32_t)l;
                 tab.lrec[lg] = (l & 0xffffffff00000000ull) | idx;
                 tab.lg2g[lg] = ng;
+                atomicAdd(lcount + 1, (unsigned long long)((size + kRadixTile - 1) / kRadixTile));  // its radix tiles
             }
         }
     }
@@ -1059,6 +1060,76 @@ __global__ void k_extract(const uint64_t *__restrict__ K, const uint32_t *__rest
     VC[x] = V[orig];
 }
 
+// Segmented large-group sort (the rank rounds' default, radix_sort_segmented): every large group
+// takes whole radix tiles, so its entries are sorted on the rank bits alone (kb bits: 3 passes of
+// 9 for 100 MB blocks) instead of on (large group, rank) (kb + 9..11 bits: 4-5 passes). Tiles of
+// each group (ptn), scanned to its first tile (pt0), then the group and entry count of every tile.
+__global__ void k_lg_tiles(const uint64_t *__restrict__ lrec, uint32_t GL, uint32_t mL, uint32_t *__restrict__ ptn)
+{
+    const uint32_t lg = blockIdx.x * kT + threadIdx.x;
+    if (lg >= GL)
+        return;
+    const uint32_t s0 = (uint32_t)(lrec[lg] >> 32), s1 = lg + 1u < GL ? (uint32_t)(lrec[lg + 1u] >> 32) : mL;
+    ptn[lg] = (s1 - s0 + kRadixTile - 1u) / kRadixTile;
+}
+
+__global__ void k_lg_tilemap(const uint64_t *__restrict__ lrec, const uint32_t *__restrict__ pt0, uint32_t GL,
+                             uint32_t mL, uint32_t ntiles, uint32_t *__restrict__ tseg, uint32_t *__restrict__ tcnt)
+{
+    const uint32_t t = blockIdx.x * kT + threadIdx.x;
+    if (t >= ntiles)
+        return;
+    uint32_t lo = 0, hi = GL - 1u;  // the last group whose first tile is at or before t
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1u) >> 1;
+        if (pt0[mid] <= t)
+            lo = mid;
+        else
+            hi = mid - 1u;
+    }
+    const uint32_t s0 = (uint32_t)(lrec[lo] >> 32), s1 = lo + 1u < GL ? (uint32_t)(lrec[lo + 1u] >> 32) : mL;
+    const uint32_t off = (t - pt0[lo]) * kRadixTile, left = s1 - s0 - off;
+    tseg[t] = lo;
+    tcnt[t] = left < kRadixTile ? left : kRadixTile;
+}
+
+// Entry x of the tiled list: tile x / 4096 of its group, slot x % 4096 (past the tile's count:
+// padding). The key keeps its group id in the upper bits (the same for the whole group), so the
+// sorted entries go back unchanged.
+__global__ void k_extract_seg(const uint64_t *__restrict__ K, const uint32_t *__restrict__ V,
+                              const uint64_t *__restrict__ lrec, const uint32_t *__restrict__ pt0,
+                              const uint32_t *__restrict__ tseg, const uint32_t *__restrict__ tcnt, uint32_t m,
+                              uint32_t ntiles, uint64_t *__restrict__ KC, uint32_t *__restrict__ VC, uint32_t *err)
+{
+    const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
+    const uint32_t t = (uint32_t)(x / kRadixTile), j = (uint32_t)(x % kRadixTile);
+    if (t >= ntiles || j >= tcnt[t])
+        return;
+    const uint32_t lg = tseg[t];
+    const uint32_t orig = (uint32_t)lrec[lg] + (t - pt0[lg]) * kRadixTile + j;
+    if (bad_index(orig >= m, err, kErrExtract))
+        return;
+    KC[x] = K[orig];
+    VC[x] = V[orig];
+}
+
+__global__ void k_putback_seg(const uint64_t *__restrict__ KS, const uint32_t *__restrict__ VS,
+                              const uint64_t *__restrict__ lrec, const uint32_t *__restrict__ pt0,
+                              const uint32_t *__restrict__ tseg, const uint32_t *__restrict__ tcnt, uint32_t m,
+                              uint32_t ntiles, uint64_t *__restrict__ K, uint32_t *__restrict__ V, uint32_t *err)
+{
+    const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;
+    const uint32_t t = (uint32_t)(x / kRadixTile), j = (uint32_t)(x % kRadixTile);
+    if (t >= ntiles || j >= tcnt[t])
+        return;
+    const uint32_t lg = tseg[t];
+    const uint32_t orig = (uint32_t)lrec[lg] + (t - pt0[lg]) * kRadixTile + j;
+    if (bad_index(orig >= m, err, kErrPutback))
+        return;
+    K[orig] = KS[x];
+    V[orig] = VS[x];
+}
+
 // Sorted large groups back to their places in the active list, original key format.
 __global__ void k_putback(const uint64_t *__restrict__ KS, const uint32_t *__restrict__ VS,
                           const uint64_t *__restrict__ lrec, const uint32_t *__restrict__ lg2g,
@@ -1494,11 +1565,12 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         }
     }
 
-    uint32_t m = nsa, h = h0, G_act = 0, GL = 0, mL = 0;
+    uint32_t m = nsa, h = h0, G_act = 0, GL = 0, mL = 0, lgtiles = 0;
     int kb_old = 0, round0 = 1;
     const int kb = bit_width(n);
     static const bool verbose = env_flag("SALZ_DEBUG", "sa");
     const bool mode_global = env_flag("SALZ_SA", "global"), mode_seg = env_flag("SALZ_SA", "segmented");
+    const bool lg_flat = env_flag("SALZ_SA", "lgflat");
     // groups of at most seg_tiny members are ordered by counting in k_seg_sort (SALZ_SA=tiny=0:
     // LSD passes everywhere). C2 SA 21.9 / 21.0 / 20.9 / 20.8 / 20.6 / 20.5 / 20.4 / 22.7 ms at
     // 0 / 8 / 16 / 32 / 64 / 128 / 256 / 2048; mixed 100 MB 27.2 (0) -> 25.7 ms (64-256)
@@ -1591,7 +1663,13 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             // groups + global sort of the large ones on (large group, rank): pick the one
             // with less HBM traffic (32 B per element and 8-bit pass; 24 B per LDS-sorted or
             // extracted/put-back element).
-            const int bits_all = kb + bit_width(G_act - 1), bits_large = kb + bit_width(GL ? GL - 1 : 0);
+            // the large groups in whole tiles, sorted each on its own (SALZ_SA=lgflat: on (large
+            // group, rank) in one list); tile tables in u1 (free until k_surv)
+            const size_t seg_words = 2 * (size_t)lgtiles + 2 * (size_t)GL + (size_t)kMaxDigits * GL;
+            const bool lg_seg = mL && GL > 1 && !lg_flat && lgtiles <= kSegScanMaxTiles &&
+                                (size_t)lgtiles * kRadixTile <= ws.cap_s && seg_words <= ws.cap_s;
+            const int bits_all = kb + bit_width(G_act - 1),
+                      bits_large = lg_seg ? kb : kb + bit_width(GL ? GL - 1 : 0);
             const double c_all = (double)m * ((bits_all + 7) / 8) * 32.0;
             const double c_seg = (double)(m - mL) * 24.0 + m * 8.0 +
                                  (double)mL * (((bits_large + 7) / 8) * 32.0 + 48.0);
@@ -1615,7 +1693,30 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                 hipLaunchKernelGGL(k_seg_sort<false>, dim3(nwin), dim3(kSegThreads), 0, st, K, V, nullptr, plan,
                                    tab.ginfo, m, kb, seg_tiny, nullptr, nullptr, derr, 0);
                 SALZ_LAUNCH_CHECK();
-                if (mL) {
+                if (lg_seg) {
+                    SegTiles sgt{ws.u1, ws.u1 + lgtiles, ws.u1 + 2 * lgtiles, ws.u1 + 2 * lgtiles + GL,
+                                 ws.u1 + 2 * lgtiles + 2 * GL, lgtiles, mL};
+                    uint32_t *ptn = const_cast<uint32_t *>(sgt.ptn), *pt0 = const_cast<uint32_t *>(sgt.pt0);
+                    hipLaunchKernelGGL(k_lg_tiles, dim3(grid_for(GL, kT)), dim3(kT), 0, st, tab.lrec, GL, mL, ptn);
+                    SALZ_LAUNCH_CHECK();
+                    if (scan_sum_u32(ptn, pt0, GL, false, nullptr, ws, st) != 0)
+                        return -1;
+                    hipLaunchKernelGGL(k_lg_tilemap, dim3(grid_for(lgtiles, kT)), dim3(kT), 0, st, tab.lrec, pt0, GL,
+                                       mL, lgtiles, const_cast<uint32_t *>(sgt.tseg),
+                                       const_cast<uint32_t *>(sgt.tcnt));
+                    SALZ_LAUNCH_CHECK();
+                    const uint32_t ngrid = lgtiles * (uint32_t)(kRadixTile / kT);
+                    hipLaunchKernelGGL(k_extract_seg, dim3(ngrid), dim3(kT), 0, st, K, V, tab.lrec, pt0, sgt.tseg,
+                                       sgt.tcnt, m, lgtiles, KC, VC, derr);
+                    SALZ_LAUNCH_CHECK();
+                    uint64_t *KS = KC;
+                    uint32_t *VS = VC;
+                    if (radix_sort_segmented(&KS, &VS, Kx, Vx, sgt, kb, ws, st, rdig) != 0)
+                        return -1;
+                    hipLaunchKernelGGL(k_putback_seg, dim3(ngrid), dim3(kT), 0, st, KS, VS, tab.lrec, pt0, sgt.tseg,
+                                       sgt.tcnt, m, lgtiles, K, V, derr);
+                    SALZ_LAUNCH_CHECK();
+                } else if (mL) {
                     uint32_t *tmap = pw + 4 * nwin;  // (lsc, after the window plan)
                     const uint32_t ntile = grid_for(mL, kT);
                     hipLaunchKernelGGL(k_tile_lg, dim3(grid_for(ntile, kT)), dim3(kT), 0, st, tab.lrec, GL, mL, tmap);
@@ -1689,7 +1790,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             SALZ_LAUNCH_CHECK();
             if (scan_sum_u64(P, P, nw, false, d64, ws, st) != 0)
                 return -1;
-            SALZ_HIP(hipMemsetAsync(d64 + 1, 0, sizeof(uint64_t), st));
+            SALZ_HIP(hipMemsetAsync(d64 + 1, 0, 2 * sizeof(uint64_t), st));
         }
         // Rank updates:
         //   direct  k_commit writes rank[i] (small rounds);
@@ -1796,6 +1897,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         G_act = Gnew;
         GL = (uint32_t)ltot;
         mL = (uint32_t)(ltot >> 32);
+        lgtiles = failed ? 0u : (uint32_t)ws.hscal[10];
         kb_old = kb;
         round0 = 0;
         h = (h > 0x7fffffffu) ? 0xffffffffu : 2 * h;

@@ -258,7 +258,7 @@ def test_encode_batch_grows_workspace(salz, cap, block, size):
 
 
 @pytest.mark.parametrize("keys", ["", "noalpha", "tiny=2048", "tiny=0", "rank1", "rank1,tiny=2048",
-                                  "noalpha,tiny=2048", "d9", "rank1,d9", "rawtext"])
+                                  "noalpha,tiny=2048", "d9", "rank1,d9", "rawtext", "lgflat"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
                                                ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
@@ -278,7 +278,9 @@ def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
     default), every group by counting ("tiny=2048"), or every group by the LSD passes ("tiny=0":
     on the repetitive small-alphabet "runs40" block the text round's LSD leaves runs of equal top
     key bits longer than 64 entries, which k_seg_text_fix orders with its bitonic network); radix passes of 8-bit digits (the default) or of 9-bit digits where they save a
-    pass ("d9": 63-bit text keys in 7 passes)."""
+    pass ("d9": 63-bit text keys in 7 passes); the large groups of a rank round in whole radix
+    tiles sorted each on its rank bits (the default) or in one list on (large group, rank)
+    ("lgflat")."""
     monkeypatch.setenv("SALZ_SA", ",".join(x for x in (mode, keys) if x))
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
@@ -390,7 +392,8 @@ def test_suffix_sort_round_checks():
         "from tests.helpers import oracle_encode\n"
         "ctx = salz_amd.Context(0, 1 << 21)\n"
         "for kind, n, seed, alpha in (('text', 600000, 5, 0), ('mixed', 300000, 6, 0), ('smx', 200000, 2, 20),\n"
-        "                             ('fib', 100000, 0, 0), ('runs40', 400001, 0, 0)):\n"
+        "                             ('fib', 100000, 0, 0), ('runs40', 400001, 0, 0), ('mixed', 2000000, 7, 0),\n"
+        "                             ('text', 2000000, 9, 0)):\n"
         "    src = _make(kind, n, seed, alpha)\n"
         "    assert ctx.encode(src) == oracle_encode(src)[1], kind\n"
         "print('round checks ok')\n" % ROOT)
