@@ -1195,7 +1195,11 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         // candidates 3 steps ahead instead of 4 and 7: mixed 100 MB parse 8.22 -> 7.9 ms, Silesia
         // blocks 3.1 -> 2.9 ms (profiles/r04zi_parse_near_prefetch_ab.txt); text at K = 512 is
         // 0.03 ms slower so
-        const bool near = klog <= 7;
+        // From the fourth pass on, where few waves walk and a pass is one lane's latency chain,
+        // the 4 / 7 distances again (SALZ_PARSE=farlate=N: from pass N; mixed 100 MB parse 7.88 ->
+        // 7.77 ms at 3, 7.79 at 5, Silesia-sized blocks even to +1%: r05fl_parse_farlate_ab.txt)
+        static const long far_late = env_num("SALZ_PARSE", "farlate", 3);
+        const bool near = klog <= 7 && it < far_late;
         if (pack && it > 0)
             hipLaunchKernelGGL((near ? k_parse_chunk<CandPacked, 1, 3> : k_parse_chunk<CandPacked, 4, 7>),
                                dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, cand8,
