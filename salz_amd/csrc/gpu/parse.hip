@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
     const uint8_t *chold, uint8_t *chnew, uint32_t n, Blocks bl, uint32_t klog,
     uint32_t *__restrict__ changed, uint32_t *err, uint8_t *__restrict__ eflag,
     const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum, uint32_t *__restrict__ reach,
-    uint32_t *__restrict__ rlo, Lazy lz, int first)
+    uint32_t *__restrict__ rlo, Lazy lz, int first, uint8_t *__restrict__ ttouch)
 {
     constexpr uint32_t kDepth = DEP, kCDepth = CDEP;
     static_assert(kDepth <= kWin && kCDepth >= kDepth && ((kCDepth + 1) % kDepth) == 0, "ring depths");
@@ -281,7 +281,10 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             // partial vmcnt waits depending on whether it ran (tests/test_codegen.py); a lane
             // whose exit did not change writes the root's flag (set anyway), so those lanes
             // share one line instead of each touching its own.
-            eflag[sidx(ex != last_ex ? ex : n, klog)] = 1u;
+            const size_t sx = sidx(ex != last_ex ? ex : n, klog);
+            eflag[sx] = 1u;
+            if (ttouch)  // (skipping passes: the 64-chunk tiles whose exit flags this walk set)
+                ttouch[sx >> (klog + 6)] = 1u;
             last_ex = ex;
             if (lz.summ && live && ex != tex) {  // (consecutive positions mostly share their exit)
                 tex = ex;
@@ -614,13 +617,18 @@ __global__ __launch_bounds__(kT) void k_mark_final(uint32_t n, uint32_t klog, co
 // Exit flags (bytes marked by the chunk pass, storage-slot order) -> ExitBits: the set as one
 // bit per slot, 64 slots a word (one row of a 64-chunk tile), and per-word popcounts for the
 // scan that numbers E. A thread packs 8 flag bytes, 8 lanes one word.
-// (nd: the pass's dirty-wave count when its test ran; none dirty -> E unchanged, nothing to pack)
+// (nd: the pass's dirty-wave count when its test ran; none dirty -> E unchanged, nothing to pack.
+// ttouch: the tiles whose flags the pass's walk set; the flags of the others, which accumulate
+// while waves skip passes, are as the last pack left them)
 __global__ __launch_bounds__(kT) void k_exit_pack(const uint64_t *__restrict__ eflag8, size_t S8, ExitBits eb,
-                                                  const uint32_t *__restrict__ nd)
+                                                  const uint32_t *__restrict__ nd,
+                                                  const uint8_t *__restrict__ ttouch, uint32_t klog)
 {
     if (nd && *nd == 0u)
         return;
     const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;  // slots [8x, 8x + 8)
+    if (ttouch && !ttouch[(x < S8 ? 8 * x : 0) >> (klog + 6)])  // (tile-uniform: 8K slots per tile)
+        return;
     uint64_t v = eflag8[x < S8 ? x : 0];  // (unconditional load, clamped)
     v |= v >> 4;
     v |= v >> 2;
@@ -1079,7 +1087,12 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     const MarkSplit ms{split_on ? pbrk + (6 + kSummW) * nc64 : nullptr, ms_count,
                        reinterpret_cast<uint8_t *>(pbrk + (8 + kSummW) * nc64), pbrk + (7 + kSummW) * nc64};
     uint32_t *ce = pbrk + (9 + kSummW) * nc64;
-    if ((size_t)(ce - reinterpret_cast<uint32_t *>(ws.lsc)) + ws.cap_n + 2 > 4 * (ws.cap_s > ws.cap_n + 2 ? ws.cap_s : ws.cap_n + 2)) {
+    // per 64-chunk tile: exit flags set by this pass's walk (skipping passes; SALZ_PARSE=notouch:
+    // every pass packs every tile)
+    const size_t ntiles = S / tile;
+    uint8_t *ttouch = env_flag("SALZ_PARSE", "notouch") ? nullptr : reinterpret_cast<uint8_t *>(ce + ws.cap_n + 2);
+    if ((size_t)(ce - reinterpret_cast<uint32_t *>(ws.lsc)) + ws.cap_n + 2 + ntiles / 4 + 1 >
+        4 * (ws.cap_s > ws.cap_n + 2 ? ws.cap_s : ws.cap_n + 2)) {
         set_error("parse: lazy-cost scratch does not fit");
         return -1;
     }
@@ -1189,6 +1202,9 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             SALZ_HIP(hipMemsetAsync(eflag, 0, S, st));
         uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
         uint8_t *wd = skipping && skip_on ? wdirty : nullptr;
+        uint8_t *tt = wd ? ttouch : nullptr;  // (flags accumulate only while waves skip)
+        if (tt)
+            SALZ_HIP(hipMemsetAsync(tt, 0, ntiles, st));
         uint32_t *rch = it == 0 && range_on ? reach : nullptr;
         const Lazy lzw{lazy ? Lv[lc] : nullptr, lazy_on ? summ : nullptr, lazy_on ? chg : nullptr};
         // Chunks of K <= 128 (non-text and mid-size blocks) prefetch far targets 1 step and
@@ -1204,12 +1220,12 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             hipLaunchKernelGGL((near ? k_parse_chunk<CandPacked, 1, 3> : k_parse_chunk<CandPacked, 4, 7>),
                                dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, cand8,
                                nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr, eflag, wd, dsum, rch,
-                               rlo, lzw, it == 0 ? 1 : 0);
+                               rlo, lzw, it == 0 ? 1 : 0, tt);
         else
             hipLaunchKernelGGL((near ? k_parse_chunk<CandFull, 1, 3> : k_parse_chunk<CandFull, 4, 7>),
                                dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
                                it == 0 ? cand8 : nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr,
-                               eflag, wd, dsum, rch, rlo, lzw, it == 0 ? 1 : 0);
+                               eflag, wd, dsum, rch, rlo, lzw, it == 0 ? 1 : 0, tt);
         SALZ_LAUNCH_CHECK();
         // The exit set of the new decisions (E was marked by the chunk pass) as bits and word
         // counts, numbered by the scan, before the pass's one host read: that read then returns
@@ -1218,7 +1234,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         // Packing is skipped on "no dirty wave" only when the walk itself skipped the clean waves
         // (wd): under SALZ_PARSE=noskip every chunk is walked and E is packed every pass.
         hipLaunchKernelGGL(k_exit_pack, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st,
-                           reinterpret_cast<const uint64_t *>(eflag), S / 8, eb, wd ? ndirty : nullptr);
+                           reinterpret_cast<const uint64_t *>(eflag), S / 8, eb, wd ? ndirty : nullptr, tt, klog);
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u32(eb.wcnt, eb.wpre, S / 64, false, etotal, ws, st) != 0)
             return -1;
