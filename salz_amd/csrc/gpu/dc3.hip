@@ -78,6 +78,116 @@ __global__ void k_dc3_first_keys(const uint2 *__restrict__ tr, const uint32_t *_
     key[c] = tr[dc3_pos(val[c], n1)].x;
 }
 
+// Levels whose triples fit kLutMaxBits bits (up to 8 bits a symbol: Fibonacci's first seven
+// levels, byte texts' first) are named without sorting: the names are the ranks of the distinct
+// triples, so a presence bitmap of the triple keys and its prefix counts give every sample its
+// name in sample order, written coalesced into the child string (no radix sort of the sample, no
+// name scatter). The sample's sorted order then comes from the child's suffix array, as it does
+// after a sort whenever names repeat; a level whose names are all distinct (D = ns) takes the
+// sorting path for that order. Bitmaps of up to kLutBits bits are built in LDS per workgroup.
+constexpr int kLutBits = 18;
+constexpr uint32_t kLutWords = 1u << (kLutBits - 5);
+constexpr int kLutMaxBits = 24;
+
+__device__ __forceinline__ uint32_t triple_key(const uint2 *__restrict__ tr, uint32_t j, uint32_t n1, int b)
+{
+    const uint32_t p = dc3_pos(j, n1);
+    return (tr[p].x << (2 * b)) | (tr[p + 1].x << b) | tr[p + 2].x;
+}
+
+// Presence bits of the sample's triple keys: per workgroup in LDS (a bit is read before it is
+// set, so a level with few distinct triples sets each one once per workgroup), then OR'd into
+// the global bitmap.
+__global__ __launch_bounds__(kT) void k_dc3_presence(const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1, int b,
+                                                     uint32_t nwords, uint32_t *__restrict__ bits)
+{
+    __shared__ uint32_t sb[kLutWords];
+    for (uint32_t i = threadIdx.x; i < nwords; i += kT)
+        sb[i] = 0;
+    __syncthreads();
+    for (size_t j = (size_t)blockIdx.x * kT + threadIdx.x; j < ns; j += (size_t)gridDim.x * kT) {
+        const uint32_t key = triple_key(tr, (uint32_t)j, n1, b), w = key >> 5, m = 1u << (key & 31u);
+        if (!(sb[w] & m))
+            atomicOr(&sb[w], m);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nwords; i += kT)
+        if (sb[i])
+            atomicOr(&bits[i], sb[i]);
+}
+
+// The same into a global bitmap of up to 2^kLutMaxBits bits (read before set: a bit is set by few
+// atomics), and the popcount of every word for the prefix scan.
+__global__ void k_dc3_presence_global(const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1, int b,
+                                      uint32_t *__restrict__ bits)
+{
+    const size_t j = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (j >= ns)
+        return;
+    const uint32_t key = triple_key(tr, (uint32_t)j, n1, b), w = key >> 5, m = 1u << (key & 31u);
+    if (!(bits[w] & m))  // (a stale cached 0 only costs a redundant atomic)
+        atomicOr(&bits[w], m);
+}
+
+__global__ void k_dc3_popc(const uint32_t *__restrict__ bits, uint32_t nwords, uint32_t *__restrict__ cnt)
+{
+    const uint32_t w = blockIdx.x * kT + threadIdx.x;
+    if (w < nwords)
+        cnt[w] = (uint32_t)__popc(bits[w]);
+}
+
+// Exclusive prefix popcounts of the bitmap words (one workgroup, 8 words a thread) and D.
+__global__ __launch_bounds__(1024) void k_dc3_lut_scan(const uint32_t *__restrict__ bits, uint32_t nwords,
+                                                       uint32_t *__restrict__ pre, uint32_t *__restrict__ D)
+{
+    static_assert(kLutWords == 1024 * 8, "8 words a thread");
+    __shared__ uint32_t wsum[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    uint32_t c[8], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+        const uint32_t w = 8 * tid + k;
+        c[k] = w < nwords ? (uint32_t)__popc(bits[w]) : 0u;
+        sum += c[k];
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = shfl_up_u32(x, d);
+        if (lane >= d)
+            x += y;
+    }
+    if (lane == 63)
+        wsum[wave] = x;
+    __syncthreads();
+    uint32_t run = x - sum, all = 0;
+    for (uint32_t w = 0; w < 16; w++) {
+        run += w < wave ? wsum[w] : 0u;
+        all += wsum[w];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+        const uint32_t w = 8 * tid + k;
+        if (w < nwords)
+            pre[w] = run;
+        run += c[k];
+    }
+    if (tid == 0)
+        *D = all;
+}
+
+// The child's string in sample order: R[j] = 1 + the distinct triples below j's.
+__global__ void k_dc3_names_lut(const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1, int b,
+                                const uint32_t *__restrict__ bits, const uint32_t *__restrict__ pre,
+                                uint2 *__restrict__ child)
+{
+    const size_t j = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (j >= ns)
+        return;
+    const uint32_t key = triple_key(tr, (uint32_t)j, n1, b), w = key >> 5;
+    child[j] = make_uint2(1u + pre[w] + (uint32_t)__popc(bits[w] & ((1u << (key & 31u)) - 1u)), 0u);
+}
+
 // Name boundaries of the sorted sample: a new triple starts a new name.
 __global__ void k_dc3_heads(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
                             const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1, int full,
@@ -322,51 +432,92 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
     uint64_t *K = ws.keyA;
     uint32_t *V = ws.valA;
     const bool full = 3 * b <= 64;
-    hipLaunchKernelGGL(k_dc3_sample_keys, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, ns, n1, b, full ? 1 : 0, K,
-                       V);
-    SALZ_LAUNCH_CHECK();
-    if (radix_sort_pairs(&K, &V, K == ws.keyA ? ws.keyB : ws.keyA, V == ws.valA ? ws.valB : ws.valA, ns, 0,
-                         full ? 3 * b : 2 * b, ws, st) != 0)
-        return -1;
-    if (!full) {
-        hipLaunchKernelGGL(k_dc3_first_keys, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, V, ns, n1, K);
-        SALZ_LAUNCH_CHECK();
-        if (radix_sort_pairs(&K, &V, K == ws.keyA ? ws.keyB : ws.keyA, V == ws.valA ? ws.valB : ws.valA, ns, 0, b,
-                             ws, st) != 0)
+    uint8_t *mark = d.top;
+    uint32_t *sar = nullptr;
+    // Naming by the triples' presence bitmap (SALZ_SA=dc3sort: by sorting at every level)
+    static const bool lut_off = env_flag("SALZ_SA", "dc3sort");
+    const uint32_t nwords = 3 * b <= kLutMaxBits ? ((1u << (3 * b)) + 31u) / 32u : 0u;
+    const size_t lut_room = nwords > kLutWords ? 2 * (size_t)nwords : 2 * (size_t)kLutWords;
+    if (nwords && !lut_off && ws.radix_counts_elems >= lut_room) {
+        uint32_t *bits = ws.radix_counts, *pre = bits + (lut_room / 2);
+        SALZ_HIP(hipMemsetAsync(bits, 0, sizeof(uint32_t) * nwords, st));
+        if (nwords <= kLutWords) {
+            const uint32_t g = grid_for(ns, kT) < 2048u ? grid_for(ns, kT) : 2048u;
+            hipLaunchKernelGGL(k_dc3_presence, dim3(g), dim3(kT), 0, st, tr, ns, n1, b, nwords, bits);
+            SALZ_LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_dc3_lut_scan, dim3(1), dim3(1024), 0, st, bits, nwords, pre, d32);
+            SALZ_LAUNCH_CHECK();
+        } else {
+            hipLaunchKernelGGL(k_dc3_presence_global, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, ns, n1, b, bits);
+            SALZ_LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_dc3_popc, dim3(grid_for(nwords, kT)), dim3(kT), 0, st, bits, nwords, pre);
+            SALZ_LAUNCH_CHECK();
+            if (scan_sum_u32(pre, pre, nwords, false, d32, ws, st) != 0)
+                return -1;
+        }
+        if (read_scalars(ws, 1200, 8, "dc3.D") != 0)
             return -1;
+        const uint32_t D = reinterpret_cast<const uint32_t *>(ws.hscal)[300];
+        if (D < ns) {
+            uint2 *child = arena_take<uint2>(d, (size_t)ns + 8);
+            sar = arena_take<uint32_t>(d, ns);
+            if (!child || !sar) {
+                set_error("dc3: arena exhausted at level %d (n=%u)", d.levels, n);
+                return -1;
+            }
+            SALZ_HIP(hipMemsetAsync(child + ns, 0, 8 * sizeof(uint2), st));
+            hipLaunchKernelGGL(k_dc3_names_lut, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, ns, n1, b, bits, pre,
+                               child);
+            SALZ_LAUNCH_CHECK();
+            if (dc3_level(d, child, ns, bit_width(D), sar) != 0)
+                return -1;
+        }
     }
     uint32_t *flag = ws.u0, *name = ws.u1;
-    hipLaunchKernelGGL(k_dc3_heads, dim3(grid_for(ns, kT)), dim3(kT), 0, st, K, V, tr, ns, n1, full ? 1 : 0, flag);
-    SALZ_LAUNCH_CHECK();
-    if (scan_sum_u32(flag, name, ns, true, d32, ws, st) != 0)
-        return -1;
-    if (read_scalars(ws, 1200, 8, "dc3.D") != 0)
-        return -1;
-    const uint32_t D = reinterpret_cast<const uint32_t *>(ws.hscal)[300];
-    uint8_t *mark = d.top;
-    uint32_t *sar;
-    if (D < ns) {
-        uint2 *child = arena_take<uint2>(d, (size_t)ns + 8);
-        sar = arena_take<uint32_t>(d, ns);
-        if (!child || !sar) {
-            set_error("dc3: arena exhausted at level %d (n=%u)", d.levels, n);
+    if (!sar) {
+        hipLaunchKernelGGL(k_dc3_sample_keys, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, ns, n1, b, full ? 1 : 0, K,
+                           V);
+        SALZ_LAUNCH_CHECK();
+        if (radix_sort_pairs(&K, &V, K == ws.keyA ? ws.keyB : ws.keyA, V == ws.valA ? ws.valB : ws.valA, ns, 0,
+                             full ? 3 * b : 2 * b, ws, st) != 0)
             return -1;
+        if (!full) {
+            hipLaunchKernelGGL(k_dc3_first_keys, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, V, ns, n1, K);
+            SALZ_LAUNCH_CHECK();
+            if (radix_sort_pairs(&K, &V, K == ws.keyA ? ws.keyB : ws.keyA, V == ws.valA ? ws.valB : ws.valA, ns, 0, b,
+                                 ws, st) != 0)
+                return -1;
         }
-        if (scatter_stage_wanted((size_t)ns * sizeof(uint2))) {  // x = name, y = 0
-            SALZ_HIP(hipMemsetAsync(child, 0, ((size_t)ns + 8) * sizeof(uint2), st));
-            if (scatter_staged(NameSrc{V, name, ns}, ns, ns, reinterpret_cast<uint32_t *>(child), 2u, 0u,
-                               reinterpret_cast<uint2 *>(ws.lsc), 2 * ws.cap_s, ws.radix_counts, st) != 0)
+        hipLaunchKernelGGL(k_dc3_heads, dim3(grid_for(ns, kT)), dim3(kT), 0, st, K, V, tr, ns, n1, full ? 1 : 0, flag);
+        SALZ_LAUNCH_CHECK();
+        if (scan_sum_u32(flag, name, ns, true, d32, ws, st) != 0)
+            return -1;
+        if (read_scalars(ws, 1200, 8, "dc3.D") != 0)
+            return -1;
+        const uint32_t D = reinterpret_cast<const uint32_t *>(ws.hscal)[300];
+        if (D < ns) {
+            uint2 *child = arena_take<uint2>(d, (size_t)ns + 8);
+            sar = arena_take<uint32_t>(d, ns);
+            if (!child || !sar) {
+                set_error("dc3: arena exhausted at level %d (n=%u)", d.levels, n);
+                return -1;
+            }
+            if (scatter_stage_wanted((size_t)ns * sizeof(uint2))) {  // x = name, y = 0
+                SALZ_HIP(hipMemsetAsync(child, 0, ((size_t)ns + 8) * sizeof(uint2), st));
+                if (scatter_staged(NameSrc{V, name, ns}, ns, ns, reinterpret_cast<uint32_t *>(child), 2u, 0u,
+                                   reinterpret_cast<uint2 *>(ws.lsc), 2 * ws.cap_s, ws.radix_counts, st) != 0)
+                    return -1;
+            } else {
+                SALZ_HIP(hipMemsetAsync(child + ns, 0, 8 * sizeof(uint2), st));
+                hipLaunchKernelGGL(k_dc3_names, dim3(grid_for(ns, kT)), dim3(kT), 0, st, V, name, ns, child);
+                SALZ_LAUNCH_CHECK();
+            }
+            if (dc3_level(d, child, ns, bit_width(D), sar) != 0)
                 return -1;
         } else {
-            SALZ_HIP(hipMemsetAsync(child + ns, 0, 8 * sizeof(uint2), st));
-            hipLaunchKernelGGL(k_dc3_names, dim3(grid_for(ns, kT)), dim3(kT), 0, st, V, name, ns, child);
-            SALZ_LAUNCH_CHECK();
+            sar = ws.u2;  // the sorted sample is the order (survives the mod-0 sort below)
+            SALZ_HIP(hipMemcpyAsync(sar, V, (size_t)ns * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
         }
-        if (dc3_level(d, child, ns, bit_width(D), sar) != 0)
-            return -1;
-    } else {
-        sar = ws.u2;  // the sorted sample is the order (survives the mod-0 sort below)
-        SALZ_HIP(hipMemcpyAsync(sar, V, (size_t)ns * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
     }
     if (scatter_stage_wanted((size_t)n * sizeof(uint2))) {
         if (scatter_staged(RankSrc{sar, ns, n1, n}, ns, n, reinterpret_cast<uint32_t *>(tr), 2u, 1u,

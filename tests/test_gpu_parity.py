@@ -295,12 +295,14 @@ DC3_CASES = STAGE_CASES + [("text", 300001, 4, 0), ("smx", 40000, 7, 200), ("mix
                            ("fib", 65537, 0, 0), ("zeros", 3000, 0, 0)]
 
 
-@pytest.mark.parametrize("keys", ["1", "0"])
+@pytest.mark.parametrize("keys", ["1", "0", "1s"])
 @pytest.mark.parametrize("kind,n,seed,alpha", DC3_CASES)
 def test_dc3_matches_oracle(ctx, monkeypatch, keys, kind, n, seed, alpha):
     """The DC3 suffix sorter (dc3.hip, forced with SALZ_SA=dc3) gives the unique suffix array on
-    every input kind, from the block's byte codes (the default) or raw bytes + 1 ("noalpha")."""
-    monkeypatch.setenv("SALZ_SA", "dc3" if keys == "1" else "dc3,noalpha")
+    every input kind, from the block's byte codes (the default) or raw bytes + 1 ("noalpha"), with
+    the levels of small triples named from their presence bitmap (the default) or every level
+    named by sorting ("1s", dc3sort)."""
+    monkeypatch.setenv("SALZ_SA", {"1": "dc3", "0": "dc3,noalpha", "1s": "dc3,dc3sort"}[keys])
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
     assert ctx.stats()["sa_dc3_levels"] > 0
