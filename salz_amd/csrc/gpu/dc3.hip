@@ -264,10 +264,16 @@ __global__ void k_dc3_mod0_flags(const uint32_t *__restrict__ sar, uint32_t ns, 
         flag[r] = sar[r] < n1 ? 1u : 0u;
 }
 
-// Mod-0 suffixes in rank[i + 1] order (the dummy stands for i = n - 1), keyed by t[i].
+// Mod-0 suffixes in rank[i + 1] order (the dummy stands for i = n - 1), keyed by t[i]. With
+// packb (symbols of at most 4 bits, positions and ranks under 2^28) the rest of the merge's
+// comparison operands of i ride along, read from the same TR run as t[i], so the merge reads no
+// TR for them: key = t[i] | rank[i + 1] << 8 | rank[i + 2] << 36 (the sort's one 8-bit digit is
+// t[i] alone), value = i | t[i + 1] << 28.
+constexpr int kRankBits = 28;
+constexpr uint32_t kPosMask = (1u << kRankBits) - 1u;
 __global__ void k_dc3_mod0(const uint32_t *__restrict__ sar, const uint32_t *__restrict__ idx, uint32_t ns,
                            uint32_t n1, uint32_t n0, const uint2 *__restrict__ tr, uint64_t *__restrict__ key,
-                           uint32_t *__restrict__ val, uint32_t *err)
+                           uint32_t *__restrict__ val, uint32_t *err, int packb)
 {
     const size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
     if (r >= ns)
@@ -278,8 +284,14 @@ __global__ void k_dc3_mod0(const uint32_t *__restrict__ sar, const uint32_t *__r
     const uint32_t c = idx[r], i = 3u * j;
     if (bad_index(c >= n0, err, kErrDc3))
         return;
-    key[c] = tr[i].x;
-    val[c] = i;
+    if (packb) {
+        const uint2 x0 = tr[i], x1 = tr[i + 1], x2 = tr[i + 2];
+        key[c] = x0.x | ((uint64_t)x1.y << 8) | ((uint64_t)x2.y << (8 + kRankBits));
+        val[c] = i | (x1.x << kRankBits);
+    } else {
+        key[c] = tr[i].x;
+        val[c] = i;
+    }
 }
 
 // ---- merge of the sorted sample (A) and the sorted mod-0 suffixes (B) ----------------------
@@ -314,7 +326,24 @@ struct MergeIn {
     const uint32_t *posb;  // sorted mod-0 positions (B)
     uint32_t nb;
     const uint2 *tr;
+    const uint64_t *keyb;  // B's sorted keys: with packb, their operands (k_dc3_mod0)
+    int packb;
 };
+
+// Position and comparison operands of B element k (sorted mod-0 index)
+__device__ __forceinline__ uint32_t b_pos(const MergeIn &m, uint32_t k)
+{
+    return m.packb ? m.posb[k] & kPosMask : m.posb[k];
+}
+
+__device__ __forceinline__ Quad b_quad(const MergeIn &m, uint32_t k)
+{
+    if (!m.packb)
+        return quad_of(m.tr, m.posb[k]);
+    const uint64_t x = m.keyb[k];
+    return Quad{(uint32_t)x & 255u, m.posb[k] >> kRankBits, (uint32_t)(x >> 8) & kPosMask,
+                (uint32_t)(x >> (8 + kRankBits))};
+}
 
 __device__ __forceinline__ uint32_t a_pos(const MergeIn &m, uint32_t r)
 {
@@ -333,8 +362,8 @@ __global__ void k_dc3_partition(MergeIn m, uint32_t ntiles, uint32_t *__restrict
     uint32_t lo = diag > m.nb ? diag - m.nb : 0u, hi = diag < m.na ? diag : m.na;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        const uint32_t pa = a_pos(m, mid), pb = m.posb[diag - 1u - mid];
-        if (b_before_a(quad_of(m.tr, pb), quad_of(m.tr, pa), pa % 3u))
+        const uint32_t pa = a_pos(m, mid);
+        if (b_before_a(b_quad(m, diag - 1u - mid), quad_of(m.tr, pa), pa % 3u))
             hi = mid;
         else
             lo = mid + 1u;
@@ -356,9 +385,9 @@ __global__ __launch_bounds__(kT) void k_dc3_merge(MergeIn m, const uint32_t *__r
     const uint32_t na = a1 - a0, cnt = d1 - d0;
     // A run then B run, each element's position and comparison operands
     for (uint32_t s = tid; s < cnt; s += kT) {
-        const uint32_t p = s < na ? a_pos(m, a0 + s) : m.posb[b0 + (s - na)];
+        const uint32_t p = s < na ? a_pos(m, a0 + s) : b_pos(m, b0 + (s - na));
         sp[s] = p;
-        sq[s] = quad_of(m.tr, p);
+        sq[s] = s < na ? quad_of(m.tr, p) : b_quad(m, b0 + (s - na));
     }
     __syncthreads();
     const uint32_t nb = b1 - b0;
@@ -534,13 +563,15 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
         return -1;
     K = ws.keyA;
     V = ws.valA;
+    // (SALZ_SA=dc3sort: unpacked keys too, the merge reading every operand from TR)
+    const int packb = !lut_off && b <= 4 && n < (1u << kRankBits) && ns < (1u << kRankBits) ? b : 0;
     hipLaunchKernelGGL(k_dc3_mod0, dim3(grid_for(ns, kT)), dim3(kT), 0, st, sar, name, ns, n1, n0, tr, K, V,
-                       d.derr);
+                       d.derr, packb);
     SALZ_LAUNCH_CHECK();
     if (radix_sort_pairs(&K, &V, ws.keyB, ws.valB, n0, 0, b, ws, st) != 0)
         return -1;
     // merge
-    MergeIn mi{sar, ns - dummy, dummy, n1, V, n0, tr};
+    MergeIn mi{sar, ns - dummy, dummy, n1, V, n0, tr, K, packb};
     const uint32_t ntiles = grid_for(n, kMergeTile);
     uint32_t *split = ws.offA;
     hipLaunchKernelGGL(k_dc3_partition, dim3(grid_for((size_t)ntiles + 1, kT)), dim3(kT), 0, st, mi, ntiles, split);
