@@ -99,7 +99,8 @@ __device__ __forceinline__ uint32_t triple_key(const uint2 *__restrict__ tr, uin
 // set, so a level with few distinct triples sets each one once per workgroup), then OR'd into
 // the global bitmap.
 __global__ __launch_bounds__(kT) void k_dc3_presence(const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1, int b,
-                                                     uint32_t nwords, uint32_t *__restrict__ bits)
+                                                     uint32_t nwords, uint32_t *__restrict__ bits,
+                                                     uint32_t *__restrict__ keys)
 {
     __shared__ uint32_t sb[kLutWords];
     for (uint32_t i = threadIdx.x; i < nwords; i += kT)
@@ -107,6 +108,7 @@ __global__ __launch_bounds__(kT) void k_dc3_presence(const uint2 *__restrict__ t
     __syncthreads();
     for (size_t j = (size_t)blockIdx.x * kT + threadIdx.x; j < ns; j += (size_t)gridDim.x * kT) {
         const uint32_t key = triple_key(tr, (uint32_t)j, n1, b), w = key >> 5, m = 1u << (key & 31u);
+        keys[j] = key;
         if (!(sb[w] & m))
             atomicOr(&sb[w], m);
     }
@@ -119,12 +121,13 @@ __global__ __launch_bounds__(kT) void k_dc3_presence(const uint2 *__restrict__ t
 // The same into a global bitmap of up to 2^kLutMaxBits bits (read before set: a bit is set by few
 // atomics), and the popcount of every word for the prefix scan.
 __global__ void k_dc3_presence_global(const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1, int b,
-                                      uint32_t *__restrict__ bits)
+                                      uint32_t *__restrict__ bits, uint32_t *__restrict__ keys)
 {
     const size_t j = (size_t)blockIdx.x * kT + threadIdx.x;
     if (j >= ns)
         return;
     const uint32_t key = triple_key(tr, (uint32_t)j, n1, b), w = key >> 5, m = 1u << (key & 31u);
+    keys[j] = key;
     if (!(bits[w] & m))  // (a stale cached 0 only costs a redundant atomic)
         atomicOr(&bits[w], m);
 }
@@ -176,15 +179,15 @@ __global__ __launch_bounds__(1024) void k_dc3_lut_scan(const uint32_t *__restric
         *D = all;
 }
 
-// The child's string in sample order: R[j] = 1 + the distinct triples below j's.
-__global__ void k_dc3_names_lut(const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1, int b,
-                                const uint32_t *__restrict__ bits, const uint32_t *__restrict__ pre,
-                                uint2 *__restrict__ child)
+// The child's string in sample order: R[j] = 1 + the distinct triples below j's (keys: the triple
+// keys the presence pass wrote in sample order, 4 bytes a sample instead of three 8-byte TR reads).
+__global__ void k_dc3_names_lut(const uint32_t *__restrict__ keys, uint32_t ns, const uint32_t *__restrict__ bits,
+                                const uint32_t *__restrict__ pre, uint2 *__restrict__ child)
 {
     const size_t j = (size_t)blockIdx.x * kT + threadIdx.x;
     if (j >= ns)
         return;
-    const uint32_t key = triple_key(tr, (uint32_t)j, n1, b), w = key >> 5;
+    const uint32_t key = keys[j], w = key >> 5;
     child[j] = make_uint2(1u + pre[w] + (uint32_t)__popc(bits[w] & ((1u << (key & 31u)) - 1u)), 0u);
 }
 
@@ -469,15 +472,17 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
     const size_t lut_room = nwords > kLutWords ? 2 * (size_t)nwords : 2 * (size_t)kLutWords;
     if (nwords && !lut_off && ws.radix_counts_elems >= lut_room) {
         uint32_t *bits = ws.radix_counts, *pre = bits + (lut_room / 2);
+        uint32_t *tkeys = reinterpret_cast<uint32_t *>(ws.keyA);  // (free until the mod-0 sort)
         SALZ_HIP(hipMemsetAsync(bits, 0, sizeof(uint32_t) * nwords, st));
         if (nwords <= kLutWords) {
             const uint32_t g = grid_for(ns, kT) < 2048u ? grid_for(ns, kT) : 2048u;
-            hipLaunchKernelGGL(k_dc3_presence, dim3(g), dim3(kT), 0, st, tr, ns, n1, b, nwords, bits);
+            hipLaunchKernelGGL(k_dc3_presence, dim3(g), dim3(kT), 0, st, tr, ns, n1, b, nwords, bits, tkeys);
             SALZ_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_dc3_lut_scan, dim3(1), dim3(1024), 0, st, bits, nwords, pre, d32);
             SALZ_LAUNCH_CHECK();
         } else {
-            hipLaunchKernelGGL(k_dc3_presence_global, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, ns, n1, b, bits);
+            hipLaunchKernelGGL(k_dc3_presence_global, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, ns, n1, b, bits,
+                               tkeys);
             SALZ_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_dc3_popc, dim3(grid_for(nwords, kT)), dim3(kT), 0, st, bits, nwords, pre);
             SALZ_LAUNCH_CHECK();
@@ -495,8 +500,7 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
                 return -1;
             }
             SALZ_HIP(hipMemsetAsync(child + ns, 0, 8 * sizeof(uint2), st));
-            hipLaunchKernelGGL(k_dc3_names_lut, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, ns, n1, b, bits, pre,
-                               child);
+            hipLaunchKernelGGL(k_dc3_names_lut, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tkeys, ns, bits, pre, child);
             SALZ_LAUNCH_CHECK();
             if (dc3_level(d, child, ns, bit_width(D), sar) != 0)
                 return -1;
