@@ -894,8 +894,19 @@ int radix_sort_segmented(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, u
             hipLaunchKernelGGL((k_radix_hist_dig<uint8_t, 8>), dim3(ntiles), dim3(kThreads), 0, st, digits, m,
                                ws.radix_counts, ntiles, sg.tcnt);
         SALZ_LAUNCH_CHECK();
-        hipLaunchKernelGGL((k_radix_segscan<512, 24>), dim3(1u << db), dim3(512), 0, st, ws.radix_counts, ntiles,
-                           sg.tseg, sg.pt0, sg.ptn, sg.segtot, 1u << db);
+        // (the row's LDS sized to the tile count: the small sorts run beside other encodes)
+        if (ntiles <= 256 * 8)
+            hipLaunchKernelGGL((k_radix_segscan<256, 8>), dim3(1u << db), dim3(256), 0, st, ws.radix_counts, ntiles,
+                               sg.tseg, sg.pt0, sg.ptn, sg.segtot, 1u << db);
+        else if (ntiles <= 256 * 16)
+            hipLaunchKernelGGL((k_radix_segscan<256, 16>), dim3(1u << db), dim3(256), 0, st, ws.radix_counts, ntiles,
+                               sg.tseg, sg.pt0, sg.ptn, sg.segtot, 1u << db);
+        else if (ntiles <= 512 * 16)
+            hipLaunchKernelGGL((k_radix_segscan<512, 16>), dim3(1u << db), dim3(512), 0, st, ws.radix_counts, ntiles,
+                               sg.tseg, sg.pt0, sg.ptn, sg.segtot, 1u << db);
+        else
+            hipLaunchKernelGGL((k_radix_segscan<512, 24>), dim3(1u << db), dim3(512), 0, st, ws.radix_counts, ntiles,
+                               sg.tseg, sg.pt0, sg.ptn, sg.segtot, 1u << db);
         SALZ_LAUNCH_CHECK();
         const bool timed = ws.timing && ws.rx_used + 2 <= ws.rx_pool.size();
         if (timed)
