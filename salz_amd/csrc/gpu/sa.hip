@@ -1597,6 +1597,35 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // during every round (the window plan and tile map take its first entries)
     uint32_t *gin = reinterpret_cast<uint32_t *>(ws.lsc) + 2 * ws.cap_s;
     auto t_round = std::chrono::steady_clock::now();
+    // The current round's large groups, each in whole radix tiles and sorted on its key bits
+    // [0, bits) alone (k_lg_tiles: tiles per group, scanned to first tiles; k_lg_tilemap; extract;
+    // radix_sort_segmented; put back): the tile tables in u1, free until k_surv.
+    auto sort_large_segmented = [&](int bits) -> int {
+        SegTiles sgt{ws.u1, ws.u1 + lgtiles, ws.u1 + 2 * lgtiles, ws.u1 + 2 * lgtiles + GL,
+                     ws.u1 + 2 * lgtiles + 2 * GL, lgtiles, mL};
+        uint32_t *ptn = const_cast<uint32_t *>(sgt.ptn), *pt0 = const_cast<uint32_t *>(sgt.pt0);
+        hipLaunchKernelGGL(k_lg_tiles, dim3(grid_for(GL, kT)), dim3(kT), 0, st, tab.lrec, GL, mL, ptn);
+        SALZ_LAUNCH_CHECK();
+        if (scan_sum_u32(ptn, pt0, GL, false, nullptr, ws, st) != 0)
+            return -1;
+        hipLaunchKernelGGL(k_lg_tilemap, dim3(grid_for(lgtiles, kT)), dim3(kT), 0, st, tab.lrec, pt0, GL, mL, lgtiles,
+                           const_cast<uint32_t *>(sgt.tseg), const_cast<uint32_t *>(sgt.tcnt));
+        SALZ_LAUNCH_CHECK();
+        uint64_t *Kx = (K == ws.keyA) ? ws.keyB : ws.keyA;
+        uint32_t *Vx = (V == ws.valA) ? ws.valB : ws.valA;
+        const uint32_t ngrid = lgtiles * (uint32_t)(kRadixTile / kT);
+        hipLaunchKernelGGL(k_extract_seg, dim3(ngrid), dim3(kT), 0, st, K, V, tab.lrec, pt0, sgt.tseg, sgt.tcnt, m,
+                           lgtiles, KC, VC, derr);
+        SALZ_LAUNCH_CHECK();
+        uint64_t *KS = KC;
+        uint32_t *VS = VC;
+        if (radix_sort_segmented(&KS, &VS, Kx, Vx, sgt, bits, ws, st, rdig) != 0)
+            return -1;
+        hipLaunchKernelGGL(k_putback_seg, dim3(ngrid), dim3(kT), 0, st, KS, VS, tab.lrec, pt0, sgt.tseg, sgt.tcnt, m,
+                           lgtiles, K, V, derr);
+        SALZ_LAUNCH_CHECK();
+        return 0;
+    };
     for (;;) {
         ws.stats.sa_rounds++;
         ws.stats.sa_sorted_elems += m;
@@ -1626,7 +1655,15 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             SALZ_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_seg_text_fix, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, rb, need);
             SALZ_LAUNCH_CHECK();
-            if (mL) {
+            // the large groups: each in whole radix tiles on its 63 key bits (7 passes of 9), or
+            // (SALZ_SA=lgflat) radix-sorted on the key and then on their large group
+            const size_t tseg_words = 2 * (size_t)lgtiles + 2 * (size_t)GL + (size_t)kMaxDigits * GL;
+            const bool tlg_seg = mL && GL > 1 && !lg_flat && lgtiles <= kSegScanMaxTiles &&
+                                 (size_t)lgtiles * kRadixTile <= ws.cap_s && tseg_words <= ws.cap_s;
+            if (tlg_seg) {
+                if (sort_large_segmented(tbits) != 0)
+                    return -1;
+            } else if (mL) {
                 uint32_t *tmap = pw + 4 * nwin;
                 const uint32_t ntile = grid_for(mL, kT);
                 // the extracted suffixes beside the group table in cand (16 B per slot: VC 4,
@@ -1694,28 +1731,8 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                                    tab.ginfo, m, kb, seg_tiny, nullptr, nullptr, derr, 0);
                 SALZ_LAUNCH_CHECK();
                 if (lg_seg) {
-                    SegTiles sgt{ws.u1, ws.u1 + lgtiles, ws.u1 + 2 * lgtiles, ws.u1 + 2 * lgtiles + GL,
-                                 ws.u1 + 2 * lgtiles + 2 * GL, lgtiles, mL};
-                    uint32_t *ptn = const_cast<uint32_t *>(sgt.ptn), *pt0 = const_cast<uint32_t *>(sgt.pt0);
-                    hipLaunchKernelGGL(k_lg_tiles, dim3(grid_for(GL, kT)), dim3(kT), 0, st, tab.lrec, GL, mL, ptn);
-                    SALZ_LAUNCH_CHECK();
-                    if (scan_sum_u32(ptn, pt0, GL, false, nullptr, ws, st) != 0)
+                    if (sort_large_segmented(kb) != 0)
                         return -1;
-                    hipLaunchKernelGGL(k_lg_tilemap, dim3(grid_for(lgtiles, kT)), dim3(kT), 0, st, tab.lrec, pt0, GL,
-                                       mL, lgtiles, const_cast<uint32_t *>(sgt.tseg),
-                                       const_cast<uint32_t *>(sgt.tcnt));
-                    SALZ_LAUNCH_CHECK();
-                    const uint32_t ngrid = lgtiles * (uint32_t)(kRadixTile / kT);
-                    hipLaunchKernelGGL(k_extract_seg, dim3(ngrid), dim3(kT), 0, st, K, V, tab.lrec, pt0, sgt.tseg,
-                                       sgt.tcnt, m, lgtiles, KC, VC, derr);
-                    SALZ_LAUNCH_CHECK();
-                    uint64_t *KS = KC;
-                    uint32_t *VS = VC;
-                    if (radix_sort_segmented(&KS, &VS, Kx, Vx, sgt, kb, ws, st, rdig) != 0)
-                        return -1;
-                    hipLaunchKernelGGL(k_putback_seg, dim3(ngrid), dim3(kT), 0, st, KS, VS, tab.lrec, pt0, sgt.tseg,
-                                       sgt.tcnt, m, lgtiles, K, V, derr);
-                    SALZ_LAUNCH_CHECK();
                 } else if (mL) {
                     uint32_t *tmap = pw + 4 * nwin;  // (lsc, after the window plan)
                     const uint32_t ntile = grid_for(mL, kT);
