@@ -433,7 +433,8 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
     // with the counters of 512 threads, instead of 2 with a 48 KB key + value stage).
     __shared__ uint64_t skey[kTile];
     uint32_t *sval = reinterpret_cast<uint32_t *>(skey);
-    __shared__ uint32_t cnt[NW][ND];
+    // (16-bit: a tile's counts stay below 2^16, and the 8-bit passes then fit 4 workgroups per CU)
+    __shared__ uint16_t cnt[NW][ND];
     __shared__ uint32_t dstart[ND];
     __shared__ uint32_t gbase[ND];
     __shared__ uint32_t wsum[2][DW];
@@ -525,7 +526,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
         uint32_t old = 0;
         if (ok && (int)lane == leader) {
             old = cnt[wave][d];
-            cnt[wave][d] = old + total;
+            cnt[wave][d] = (uint16_t)(old + total);
         }
         old = shfl_u32(old, leader);
         lrank[j] = old + below;
@@ -571,7 +572,7 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
 #pragma unroll
         for (int w = 0; w < NW; w++) {
             const uint32_t c = cnt[w][tid];
-            cnt[w][tid] = run;
+            cnt[w][tid] = (uint16_t)run;
             run += c;
         }
     }
