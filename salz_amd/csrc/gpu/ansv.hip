@@ -53,6 +53,19 @@ __device__ __forceinline__ uint2 half(uint32_t p, uint32_t pos, uint32_t len, co
                                                    : make_uint2(p - pos, len);
 }
 
+// Packed staging (blocks of at most 2^27 positions, text ranges of at most 2^20): each half of a
+// staged answer is one 64-bit word, offset (27 bits) | length (27) << 27 | ten bits of the
+// suffix's position within its text range << 54 (PSV half: the low ten, NSV half: the high ten),
+// so the scatter needs no separate position array (sp). A half still unanswered holds only its
+// position bits; its answer comes later (block walk, or k_ansv_global straight into cand).
+constexpr uint32_t kPk27 = (1u << 27) - 1u;
+__device__ __forceinline__ uint2 pk_half(uint2 h, uint32_t p, uint32_t rlog, int side)
+{
+    const uint32_t lowp = p & ((1u << rlog) - 1u), part = side ? lowp >> 10 : lowp & 1023u;
+    const uint64_t w = (uint64_t)h.x | ((uint64_t)h.y << 27) | ((uint64_t)part << 54);
+    return make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+}
+
 // cand is stored in the parse's chunk-interleaved layout (common.hpp, sidx).
 __device__ __forceinline__ void put_psv(uint4 *cand, uint32_t klog, uint32_t p, uint32_t psv_pos,
                                         uint32_t len, const Blocks &bl)
@@ -84,7 +97,7 @@ __device__ __forceinline__ uint32_t shard_base(uint32_t s, uint32_t used_blocks,
 __device__ __forceinline__ void block_walk(uint32_t e, uint32_t slot, const uint32_t *vsa,
                                            const uint32_t *vlc, uint32_t b0, uint2 *sh, uint32_t *qp, uint32_t *qp_len,
                                            uint32_t *qn, uint32_t *qn_len, uint32_t *qcount,
-                                           uint32_t qbase, const Blocks &bl)
+                                           uint32_t qbase, const Blocks &bl, int pk, uint32_t rlog)
 {
     const uint32_t l = e >> 1, r = b0 + l;
     const uint32_t v = vsa[kB + l];
@@ -113,8 +126,10 @@ __device__ __forceinline__ void block_walk(uint32_t e, uint32_t slot, const uint
             }
             node >>= 1;
         }
-        if (hit != kInf)
-            sh[2 * slot] = half(v, vsa[kB + hit], lm, bl);
+        if (hit != kInf) {
+            const uint2 hh = half(v, vsa[kB + hit], lm, bl);
+            sh[2 * slot] = pk ? pk_half(hh, v, rlog, 0) : hh;
+        }
     } else {
         // NSV: nearest smaller to the right; LCP minimum over (r, r'].
         lm = kInf;
@@ -139,8 +154,10 @@ __device__ __forceinline__ void block_walk(uint32_t e, uint32_t slot, const uint
             }
             node >>= 1;
         }
-        if (hit != kInf)
-            sh[2 * slot + 1] = half(v, vsa[kB + hit], lm, bl);
+        if (hit != kInf) {
+            const uint2 hh = half(v, vsa[kB + hit], lm, bl);
+            sh[2 * slot + 1] = pk ? pk_half(hh, v, rlog, 1) : hh;
+        }
     }
     // global queue: one atomic per wave and side on this block's shard counter
     const bool miss = hit == kInf;
@@ -170,7 +187,7 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     uint32_t *__restrict__ sp, uint32_t *__restrict__ rfill,
     uint32_t rlog, uint32_t *__restrict__ qp, uint32_t *__restrict__ qp_len,
     uint32_t *__restrict__ qn, uint32_t *__restrict__ qn_len, uint32_t *__restrict__ qcount,
-    unsigned long long *prof)
+    unsigned long long *prof, int pk)
 {
     __shared__ uint32_t vsa[2 * kB + kNear];  // heap: [1, kB) tree, [kB, 2kB) leaves, + pad
     __shared__ uint32_t vlc[2 * kB + kNear];
@@ -288,7 +305,7 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
             wq[slot] = (uint16_t)e;
         else
             block_walk(e, slot_of(e >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len, qcount,
-                       qbase, bl);
+                       qbase, bl, pk, rlog);
     };
     if (tid == 0)
         wq_n = 0;
@@ -334,6 +351,16 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
         const uint32_t hitP = mP ? l - dP - 1u : kInf, hitN = mN ? l + dN + 1u : kInf;
         const uint32_t pvP = mP ? vsa[kB + hitP] : 0u, pvN = mN ? vsa[kB + hitN] : 0u;
         const uint32_t slot = slot_of(l);
+        if (pk) {  // both halves at once, an unanswered one with its position bits only
+            const uint2 hp = pk_half(hitP != kInf ? half(v, pvP, lmP, bl) : make_uint2(0u, 0u), v, rlog, 0);
+            const uint2 hn = pk_half(hitN != kInf ? half(v, pvN, lmN, bl) : make_uint2(0u, 0u), v, rlog, 1);
+            stage[slot] = make_uint4(hp.x, hp.y, hn.x, hn.y);
+            if (hitP == kInf)
+                enqueue(l << 1);
+            if (hitN == kInf)
+                enqueue(l << 1 | 1u);
+            continue;
+        }
         sp[slot] = v;
         if (hitP != kInf && hitN != kInf) {
             const uint2 hp = half(v, pvP, lmP, bl), hn = half(v, pvN, lmN, bl);
@@ -359,7 +386,7 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     const uint32_t nw = wq_n < kWQ ? wq_n : kWQ;
     for (uint32_t w = tid; w < nw; w += kT)
         block_walk(wq[w], slot_of(wq[w] >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len,
-                   qcount, qbase, bl);
+                   qcount, qbase, bl, pk, rlog);
     if (prof) {
         __syncthreads();
         if (tid == 0) {
@@ -380,7 +407,7 @@ __global__ __launch_bounds__(kT) void k_cand_scatter(const uint32_t *__restrict_
                                                      uint4 *__restrict__ cand, uint32_t klog,
                                                      uint32_t rlog, uint32_t nranges,
                                                      const uint32_t *__restrict__ rfill,
-                                                     uint32_t *__restrict__ err)
+                                                     uint32_t *__restrict__ err, int pk)
 {
     // XCD-aware: workgroups are dealt round-robin over the 8 XCDs, so workgroup g runs on
     // XCD g mod 8; XCD x takes text ranges x, x + 8, ... in turn, and the lines of one cand
@@ -397,8 +424,17 @@ __global__ __launch_bounds__(kT) void k_cand_scatter(const uint32_t *__restrict_
     if (x >= rfill[r])
         return;
     const size_t i = ((size_t)r << rlog) + x;
-    const uint32_t p = sp[i];
     const uint4 c = stage[i];
+    if (pk) {  // (the position from the halves' bits, the halves back to {offset, length})
+        const uint32_t p = (r << rlog) | (c.y >> 22) | ((c.w >> 22) << 10);
+        if (bad_index(p >= npos, err, kErrAnsv))
+            return;
+        const uint64_t w0 = (uint64_t)c.y << 32 | c.x, w1 = (uint64_t)c.w << 32 | c.z;
+        cand[sidx(p, klog)] = make_uint4((uint32_t)w0 & kPk27, (uint32_t)(w0 >> 27) & kPk27, (uint32_t)w1 & kPk27,
+                                         (uint32_t)(w1 >> 27) & kPk27);
+        return;
+    }
+    const uint32_t p = sp[i];
     if (bad_index(p >= npos, err, kErrAnsv))
         return;
     cand[sidx(p, klog)] = c;
@@ -645,8 +681,12 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
         return -1;
     }
     SALZ_HIP(hipMemsetAsync(rfill, 0, kMaxRanges * sizeof(uint32_t), st));
+    // packed staging (no position array) where offsets, lengths and range bits fit 16 bytes
+    // (SALZ_SA=ansvsp: the position array always)
+    const bool two_req = npos > (1u << 22) && env_flag("SALZ_SA", "ansv2");
+    const int pk = !two_req && npos <= (1u << 27) && rlog <= 20 && !env_flag("SALZ_SA", "ansvsp") ? 1 : 0;
     hipLaunchKernelGGL(k_ansv_local, dim3(used_blocks), dim3(kT), 0, st, ws.sa, lcp, n, bl, np2, tsa,
-                       tlcp, stage, sp, rfill, rlog, qp, qpl, qn, qnl, cnt, prof);
+                       tlcp, stage, sp, rfill, rlog, qp, qpl, qn, qnl, cnt, prof, pk);
     SALZ_LAUNCH_CHECK();
     const uint32_t nranges = (uint32_t)((((uint64_t)npos - 1) >> rlog) + 1);
     // SALZ_SA=ansv2: a second staging level for large blocks (cand past 64 MB). Measured slower on
@@ -671,7 +711,7 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
     } else {
         const uint32_t sgrid = 8u * ((nranges + 7u) / 8u) << (rlog - 8);
         hipLaunchKernelGGL(k_cand_scatter, dim3(sgrid), dim3(kT), 0, st, sp, stage, npos, ws.cand,
-                           ws.klog, rlog, nranges, rfill, derr);
+                           ws.klog, rlog, nranges, rfill, derr, pk);
         SALZ_LAUNCH_CHECK();
     }
     if (prof) {

@@ -365,12 +365,13 @@ def test_dc3_edge_sizes(ctx, monkeypatch):
             assert rc == 0 and out == ref, (N, kind)
 
 
-@pytest.mark.parametrize("keys", ["", "ansv2"])
+@pytest.mark.parametrize("keys", ["", "ansv2", "ansvsp"])
 @pytest.mark.parametrize("kind,n,seed", [("text", 6_000_007, 8), ("mixed", 5_000_001, 9)])
 def test_ansv_staging_levels(ctx, monkeypatch, keys, kind, n, seed):
     """Candidates of blocks past 2^22 positions through one staging level (the default) or two
     (SALZ_SA=ansv2: each 2^20-position run re-sorted into 2^17-position sub-runs before the scatter
-    into cand): psv/nsv and their lengths equal the oracle's either way."""
+    into cand), staged with the suffix's position bits packed into the answer (the default) or in a
+    position array of their own ("ansvsp"): psv/nsv and their lengths equal the oracle's."""
     monkeypatch.setenv("SALZ_SA", keys)
     src = gen(kind, n, seed)
     out, d = ctx.encode_dump(src)
