@@ -60,6 +60,32 @@ __global__ void k_mark_start(ExitBits eb, const uint64_t *__restrict__ pst, uint
     emark[bits_index(eb.mask, eb.wpre, sidx((uint32_t)pst[sidx(p0, klog)], klog))] = 1u;
 }
 
+// One block's path in one launch (instead of a launch per level): thread j marks the path nodes at
+// distances [j L, (j + 1) L) from the start, reaching its first by binary lifting over the parse's
+// stored levels (parents 2^k steps up at jt + k ne), then walking level 0. The root is its own
+// parent, so lifting or walking past the path's end stays there.
+__global__ void k_mark_path(ExitBits eb, const uint64_t *__restrict__ pst, uint32_t klog, const uint32_t *__restrict__ jt,
+                            uint32_t ne, uint32_t levels, uint32_t L, uint32_t nthreads, uint32_t *emark)
+{
+    const uint32_t j = blockIdx.x * kT + threadIdx.x;
+    if (j >= nthreads)
+        return;
+    const uint64_t d = (uint64_t)j * L;
+    if (d >> levels || d > (uint64_t)ne)
+        return;  // (beyond every path)
+    uint32_t x = bits_index(eb.mask, eb.wpre, sidx((uint32_t)pst[sidx(0u, klog)], klog));  // the start's exit
+    for (uint32_t k = 0; k < levels; k++)
+        if ((d >> k) & 1u)
+            x = jt[(size_t)k * ne + x];
+    for (uint32_t i = 0; i < L; i++) {
+        emark[x] = 1u;
+        const uint32_t nx = jt[x];
+        if (nx == x)
+            break;
+        x = nx;
+    }
+}
+
 __global__ void k_mark_step(const uint32_t *__restrict__ jt, uint32_t *emark, uint32_t ne)
 {
     uint32_t x = blockIdx.x * kT + threadIdx.x;
@@ -461,6 +487,19 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
     SALZ_HIP(hipMemsetAsync(entry, 0xff, sizeof(uint32_t) * ((size_t)nch + 1), st));
     if (ne) {
         SALZ_HIP(hipMemsetAsync(emark, 0, sizeof(uint32_t) * ne, st));
+        // one block with its levels stored: the path in one launch (SALZ_PARSE=marksteps: a launch
+        // per level)
+        static const bool steps = env_flag("SALZ_PARSE", "marksteps");
+        const bool one = nb == 1 && ps.snaps && ps.levels > 0 && !steps;
+        if (one) {
+            // (a path takes at most one exit per chunk: nch + 1 nodes with the root)
+            constexpr uint32_t kPathThreads = 32768;
+            const uint64_t reach = (uint64_t)nch + 2;
+            const uint32_t L = (uint32_t)((reach + kPathThreads - 1) / kPathThreads);
+            hipLaunchKernelGGL(k_mark_path, dim3(grid_for(kPathThreads, kT)), dim3(kT), 0, st, ps.ebits, ps.pst,
+                               ws.klog, ps.jt0, ne, ps.levels, L, kPathThreads, emark);
+            SALZ_LAUNCH_CHECK();
+        } else {
         hipLaunchKernelGGL(k_mark_start, dim3(grid_for(nb, kT)), dim3(kT), 0, st, ps.ebits, ps.pst, ws.klog,
                            emark, bl);
         SALZ_LAUNCH_CHECK();
@@ -479,6 +518,7 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
             }
             hipLaunchKernelGGL(k_mark_step, dim3(grid_for(ne, kT)), dim3(kT), 0, st, lev, emark, ne);
             SALZ_LAUNCH_CHECK();
+        }
         }
         hipLaunchKernelGGL(k_entries, dim3(grid_for(ne, kT)), dim3(kT), 0, st, emark, ps.elist, ne,
                            n, ps.chunk, entry);

@@ -443,7 +443,7 @@ def test_lcp_paths(ctx, monkeypatch, lcp_sa, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
-@pytest.mark.parametrize("skip", ["1", "1l0", "1s0", "1n2", "1r0", "0", "1p0", "1t0"])
+@pytest.mark.parametrize("skip", ["1", "1l0", "1s0", "1n2", "1r0", "0", "1p0", "1t0", "1m0"])
 @pytest.mark.parametrize("kind,n,seed,alpha,klog", [("mixed", 3_000_000, 3, 0, "6"),
                                                     ("mixed", 2_000_001, 7, 0, "9"),
                                                     ("text", 1_500_000, 2, 0, "7"),
@@ -459,9 +459,10 @@ def test_parse_wave_skip(ctx, monkeypatch, skip, kind, n, seed, alpha, klog):
     as a wave per listed chunk (the default) or inside the test kernel ("1s0", nosplit), and with
     the exit set compacted a thread per node ("1n2", nodes=2; by default only where it is
     sparse), and with the exit set re-packed only in the tiles the walk touched (the default) or
-    in every tile ("1t0", notouch)."""
+    in every tile ("1t0", notouch); emission marks the path in one launch (the default) or a launch per
+    jump level ("1m0", marksteps)."""
     flags = {"0": "noskip", "1l0": "nolazy", "1s0": "nosplit", "1n2": "nodes=2", "1r0": "norange",
-             "1p0": "nopack", "1t0": "notouch"}.get(skip)
+             "1p0": "nopack", "1t0": "notouch", "1m0": "marksteps"}.get(skip)
     monkeypatch.setenv("SALZ_PARSE", f"klog={klog}" + (f",{flags}" if flags else ""))
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
