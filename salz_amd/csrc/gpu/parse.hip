@@ -737,6 +737,30 @@ __global__ __launch_bounds__(kT) void k_compact_nodes(ExitBits eb, const uint32_
 // emission's path marking): from level k (jt, js) to k + 1 (jt1, written) and k + 2 (jt2, js2).
 // A thread derives its node's level-(k + 1) successor itself, so no other thread's result of
 // this launch is read.
+// Three levels per launch (levels k + 1, k + 2, k + 3 from level k: eight dependent loads per
+// thread through the L2-resident tables), for fewer launches where passes repeat.
+__global__ void k_jump3(const uint32_t *__restrict__ jt, const uint32_t *__restrict__ js,
+                        uint32_t *__restrict__ jt1, uint32_t *__restrict__ jt2, uint32_t *__restrict__ jt3,
+                        uint32_t *__restrict__ js3, uint32_t ne)
+{
+    const uint32_t x = blockIdx.x * kT + threadIdx.x;
+    if (x >= ne)
+        return;
+    uint32_t p[9];
+    p[0] = x;
+#pragma unroll
+    for (int k = 1; k <= 8; k++)
+        p[k] = jt[p[k - 1]];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        s += js[p[k]];
+    jt1[x] = p[2];
+    jt2[x] = p[4];
+    jt3[x] = p[8];
+    js3[x] = s;
+}
+
 __global__ void k_jump2(const uint32_t *__restrict__ jt, const uint32_t *__restrict__ js,
                         uint32_t *__restrict__ jt1, uint32_t *__restrict__ jt2,
                         uint32_t *__restrict__ js2, uint32_t ne, int two)
@@ -1292,13 +1316,25 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         SALZ_LAUNCH_CHECK();
         int jc = 0;
         if (snaps) {
-            for (uint32_t k = 0; k < K; k += 2) {
+            // (SALZ_PARSE=jump2: two levels per launch everywhere)
+            static const bool jump2_only = env_flag("SALZ_PARSE", "jump2");
+            for (uint32_t k = 0; k < K;) {
+                if (!jump2_only && k + 3 <= K && (size_t)(k + 4) * ne <= snap_cap) {
+                    hipLaunchKernelGGL(k_jump3, dim3(grid_for(ne, kT)), dim3(kT), 0, st, snap + (size_t)k * ne, js[jc],
+                                       snap + (size_t)(k + 1) * ne, snap + (size_t)(k + 2) * ne,
+                                       snap + (size_t)(k + 3) * ne, js[jc ^ 1], ne);
+                    SALZ_LAUNCH_CHECK();
+                    jc ^= 1;
+                    k += 3;
+                    continue;
+                }
                 const int two = k + 1 < K;
                 hipLaunchKernelGGL(k_jump2, dim3(grid_for(ne, kT)), dim3(kT), 0, st,
                                    snap + (size_t)k * ne, js[jc], snap + (size_t)(k + 1) * ne,
                                    two ? snap + (size_t)(k + 2) * ne : nullptr, js[jc ^ 1], ne, two);
                 SALZ_LAUNCH_CHECK();
                 jc ^= 1;
+                k += 2;
             }
         } else {
             uint32_t *pp[2] = {ws.u2, ws.u3};  // free during the parse
