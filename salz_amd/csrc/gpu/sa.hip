@@ -437,6 +437,16 @@ struct GroupTab {
     uint32_t *lg2g;
 };
 
+// Round 0 before a text round: the survivors' text-round keys are written with their compacted
+// entries (the symbols at i + h0, k_keys_text's gather done here), when `key` is set.
+struct TextNext {
+    const uint8_t *Tm;
+    uint64_t *key;
+    Blocks bl;
+    Alpha a;
+    uint32_t h0;
+};
+
 // gin: the text round (round 1 keyed by text, below): entry c's group id, which its key no
 // longer holds; every rank is written there (no entry keeps one: round 0 wrote no survivor's).
 // surv_rank = 0: round 0 before a text round writes only the ranks of the suffixes it finishes.
@@ -448,7 +458,7 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
                          uint32_t *__restrict__ rank, uint32_t *__restrict__ sa, GroupTab tab,
                          uint32_t m, uint32_t n, uint32_t nsa, int kb_old, int round0, uint32_t *err,
                          uint32_t ihi, uint32_t *__restrict__ later, uint32_t gbase,
-                         const uint32_t *__restrict__ gin, int surv_rank)
+                         const uint32_t *__restrict__ gin, int surv_rank, TextNext tn)
 {
     size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= m)
@@ -487,6 +497,8 @@ __global__ void k_commit(const uint64_t *__restrict__ key, const uint32_t *__res
         const uint32_t ng = (uint32_t)pw + (uint32_t)__popcll(sh & (below | (below + 1ull))) - 1u;
         nval[idx] = i;
         ngid[idx] = ng;
+        if (tn.key)
+            tn.key[idx] = round0_key_mapped(tn.Tm, i + tn.h0, tn.bl.end(i), tn.a);
         if ((uint32_t)c == hp) {  // (idx is the group's compact start)
             off_new[ng] = hp + o - idx;
             tab.ginfo[ng] = ((uint64_t)size << 32) | idx;
@@ -1828,10 +1840,15 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         const uint32_t span = (uint32_t)(((uint64_t)n + parts - 1) / parts);
         uint32_t *later = reinterpret_cast<uint32_t *>(Kx);  // free until k_keys
         const uint32_t ihi = mode == 0 ? 0xffffffffu : mode == 1 ? span : 0u;
+        // (the text round's keys with the survivors' entries, where Kx is not the rank list: SALZ_SA=
+        // keystext keeps the separate gather)
+        static const bool keys_apart = env_flag("SALZ_SA", "keystext");
+        const bool fuse_keys = textnext && mode == 0 && !keys_apart;
+        const TextNext tn{tmapped, fuse_keys ? Kx : nullptr, bl, alpha, h};
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, headpos,
                            P, reinterpret_cast<unsigned long long *>(d64 + 1), offo, offn, Vx, textnext ? gin : ngid,
                            ws.rank, ws.sa, tab, m, n, nsa, kb_old, round0, derr, ihi, mode ? later : nullptr,
-                           dist ? dist->gbase : 0u, textr ? gin : nullptr, textnext ? 0 : 1);
+                           dist ? dist->gbase : 0u, textr ? gin : nullptr, textnext ? 0 : 1, tn);
         SALZ_LAUNCH_CHECK();
         for (uint32_t q = 1; q < parts; q++) {
             hipLaunchKernelGGL(k_rank_upper, dim3(grid_for(m, kT)), dim3(kT), 0, st, V, later, m,
@@ -1896,7 +1913,9 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         }
         if (dc3_auto && h >= 32 && (uint64_t)mnew * 4 > (uint64_t)n * 3)
             return stage_suffix_array_dc3(ws, bl, codes, codes_raw);
-        if (textnext) {  // the text round's keys: the h0 symbols at i + h0 (every rank holds the text)
+        if (textnext && fuse_keys) {
+            // (written by k_commit)
+        } else if (textnext) {  // the text round's keys: the h0 symbols at i + h0 (every rank holds the text)
             hipLaunchKernelGGL(k_keys_text, dim3(grid_for(mnew, kT)), dim3(kT), 0, st, Vx, mnew, bl, alpha, h,
                                tmapped, Kx);
             SALZ_LAUNCH_CHECK();

@@ -258,7 +258,7 @@ def test_encode_batch_grows_workspace(salz, cap, block, size):
 
 
 @pytest.mark.parametrize("keys", ["", "noalpha", "tiny=2048", "tiny=0", "rank1", "rank1,tiny=2048",
-                                  "noalpha,tiny=2048", "d9", "rank1,d9", "rawtext", "lgflat"])
+                                  "noalpha,tiny=2048", "d9", "rank1,d9", "rawtext", "lgflat", "keystext"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
                                                ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
@@ -280,7 +280,7 @@ def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
     key bits longer than 64 entries, which k_seg_text_fix orders with its bitonic network); radix passes of 8-bit digits (the default) or of 9-bit digits where they save a
     pass ("d9": 63-bit text keys in 7 passes); the large groups of a rank round in whole radix
     tiles sorted each on its rank bits (the default) or in one list on (large group, rank)
-    ("lgflat")."""
+    ("lgflat"); the text round's keys gathered by round 0's commit (the default) or apart ("keystext")."""
     monkeypatch.setenv("SALZ_SA", ",".join(x for x in (mode, keys) if x))
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
