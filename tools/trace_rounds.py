@@ -3,7 +3,8 @@
   python tools/trace_rounds.py <kernel_trace.csv> [encode index]
 
 An encode starts at the text-sourced radix histogram (round 0); each doubling round ends with
-k_commit / k_rank_upper and the next round's k_keys. Prints per-round kernel time (sum of
+k_commit / k_rank_upper and the next round's k_keys (or, for round 0 whose commit gathers the text
+round's keys, with k_commit). Prints per-round kernel time (sum of
 dispatch durations) and the wall span, and the per-kernel totals of the later stages."""
 import collections
 import csv
@@ -29,14 +30,18 @@ def main(path, which=0):
     rounds, cur = [], []
     stage = "sa"
     post = collections.OrderedDict()
-    for r in enc:
-        name = kname(r["Kernel_Name"])
+    names = [kname(r["Kernel_Name"]) for r in enc]
+    for idx, r in enumerate(enc):
+        name = names[idx]
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         if name.startswith("k_ansv_local") or name.startswith("k_phi"):
             stage = "post"
         if stage == "sa":
             cur.append((name, dur, int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
-            if name.startswith("k_keys"):
+            nxt = next((x for x in names[idx + 1:] if x != "k_read_scalars"), "")
+            # (round 0 before the text round gathers the text keys inside k_commit: no k_keys)
+            fused_end = name in ("k_commit", "k_rank_upper") and not nxt.startswith(("k_keys", "k_rank_upper"))
+            if name.startswith("k_keys") or fused_end:
                 rounds.append(cur)
                 cur = []
         else:
