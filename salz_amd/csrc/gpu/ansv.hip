@@ -649,22 +649,22 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
     uint32_t *qp = ws.valA, *qpl = ws.valB, *qn = ws.offA, *qnl = ws.offB;
     uint32_t *cnt = reinterpret_cast<uint32_t *>(ws.dscal) + kQCountWord;
 
-    SALZ_HIP(hipMemsetAsync(cnt, 0, 2 * kShards * sizeof(uint32_t), st));
+    SALZ_HIP(fill_async(cnt, 0, 2 * kShards * sizeof(uint32_t), st));
     uint32_t nblocks = np2 / kB;
     uint32_t used_blocks = (n + kB - 1) / kB;
     // Blocks past the text only hold +inf leaves: fill their subtree roots directly.
     if (used_blocks < nblocks) {
         // Each unused block root and its descendants would be +inf; only nodes at or above
         // the block-root level are ever read for them, so set those roots to +inf.
-        SALZ_HIP(hipMemsetAsync(tsa + nblocks + used_blocks, 0xff,
+        SALZ_HIP(fill_async(tsa + nblocks + used_blocks, 0xff,
                                 sizeof(uint32_t) * (nblocks - used_blocks), st));
-        SALZ_HIP(hipMemsetAsync(tlcp + nblocks + used_blocks, 0xff,
+        SALZ_HIP(fill_async(tlcp + nblocks + used_blocks, 0xff,
                                 sizeof(uint32_t) * (nblocks - used_blocks), st));
     }
     static const bool prof_on = env_flag("SALZ_DEBUG", "ansv");
     unsigned long long *prof = prof_on ? reinterpret_cast<unsigned long long *>(ws.dscal) + 200 : nullptr;
     if (prof)
-        SALZ_HIP(hipMemsetAsync(prof, 0, 32, st));
+        SALZ_HIP(fill_async(prof, 0, 32, st));
     // Staging: text ranges of 2^rlog positions (cand windows of 16 << rlog bytes; 16 MB by
     // default: 2^19 and 2^21 measured slower), at most kMaxRanges of them. Slots sp / stage
     // alias scratch that is free here.
@@ -680,7 +680,7 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
         set_error("ansv: range counters do not fit");
         return -1;
     }
-    SALZ_HIP(hipMemsetAsync(rfill, 0, kMaxRanges * sizeof(uint32_t), st));
+    SALZ_HIP(fill_async(rfill, 0, kMaxRanges * sizeof(uint32_t), st));
     // packed staging (no position array) where offsets, lengths and range bits fit 16 bytes
     // (SALZ_SA=ansvsp: the position array always)
     const bool two_req = npos > (1u << 22) && env_flag("SALZ_SA", "ansv2");
@@ -697,7 +697,7 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
                      ws.radix_counts_elems >= (size_t)kMaxRanges * 9;
     if (two) {
         uint32_t *sfill = rfill + kMaxRanges;  // per sub-range fill
-        SALZ_HIP(hipMemsetAsync(sfill, 0, (size_t)kMaxRanges * 8 * sizeof(uint32_t), st));
+        SALZ_HIP(fill_async(sfill, 0, (size_t)kMaxRanges * 8 * sizeof(uint32_t), st));
         uint32_t *sp2 = ws.rank;  // (free after the suffix sort; the parse takes it later)
         uint2 *lo2 = reinterpret_cast<uint2 *>(ws.g64), *hi2 = reinterpret_cast<uint2 *>(ws.pst);
         hipLaunchKernelGGL(k_ansv_restage, dim3(nranges << (rlog - 12)), dim3(kT), 0, st, sp, stage, rlog, rfill, sfill,

@@ -455,7 +455,7 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
     hipStream_t st = d.st;
     d.levels++;
     if (n == 1) {
-        SALZ_HIP(hipMemsetAsync(sa_out, 0, sizeof(uint32_t), st));
+        SALZ_HIP(fill_async(sa_out, 0, sizeof(uint32_t), st));
         return 0;
     }
     const uint32_t dummy = n % 3u == 1u ? 1u : 0u;
@@ -473,7 +473,7 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
     if (nwords && !lut_off && ws.radix_counts_elems >= lut_room) {
         uint32_t *bits = ws.radix_counts, *pre = bits + (lut_room / 2);
         uint32_t *tkeys = reinterpret_cast<uint32_t *>(ws.keyA);  // (free until the mod-0 sort)
-        SALZ_HIP(hipMemsetAsync(bits, 0, sizeof(uint32_t) * nwords, st));
+        SALZ_HIP(fill_async(bits, 0, sizeof(uint32_t) * nwords, st));
         if (nwords <= kLutWords) {
             const uint32_t g = grid_for(ns, kT) < 2048u ? grid_for(ns, kT) : 2048u;
             hipLaunchKernelGGL(k_dc3_presence, dim3(g), dim3(kT), 0, st, tr, ns, n1, b, nwords, bits, tkeys);
@@ -499,7 +499,7 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
                 set_error("dc3: arena exhausted at level %d (n=%u)", d.levels, n);
                 return -1;
             }
-            SALZ_HIP(hipMemsetAsync(child + ns, 0, 8 * sizeof(uint2), st));
+            SALZ_HIP(fill_async(child + ns, 0, 8 * sizeof(uint2), st));
             hipLaunchKernelGGL(k_dc3_names_lut, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tkeys, ns, bits, pre, child);
             SALZ_LAUNCH_CHECK();
             if (dc3_level(d, child, ns, bit_width(D), sar) != 0)
@@ -536,12 +536,12 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
                 return -1;
             }
             if (scatter_stage_wanted((size_t)ns * sizeof(uint2))) {  // x = name, y = 0
-                SALZ_HIP(hipMemsetAsync(child, 0, ((size_t)ns + 8) * sizeof(uint2), st));
+                SALZ_HIP(fill_async(child, 0, ((size_t)ns + 8) * sizeof(uint2), st));
                 if (scatter_staged(NameSrc{V, name, ns}, ns, ns, reinterpret_cast<uint32_t *>(child), 2u, 0u,
                                    reinterpret_cast<uint2 *>(ws.lsc), 2 * ws.cap_s, ws.radix_counts, st) != 0)
                     return -1;
             } else {
-                SALZ_HIP(hipMemsetAsync(child + ns, 0, 8 * sizeof(uint2), st));
+                SALZ_HIP(fill_async(child + ns, 0, 8 * sizeof(uint2), st));
                 hipLaunchKernelGGL(k_dc3_names, dim3(grid_for(ns, kT)), dim3(kT), 0, st, V, name, ns, child);
                 SALZ_LAUNCH_CHECK();
             }

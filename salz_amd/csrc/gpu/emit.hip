@@ -484,9 +484,9 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
     BlockOut *binfo = reinterpret_cast<BlockOut *>(ws.g64 + 2 * ((size_t)nch + 2) + 2);
     uint64_t *wcnt = reinterpret_cast<uint64_t *>(binfo + nb);
 
-    SALZ_HIP(hipMemsetAsync(entry, 0xff, sizeof(uint32_t) * ((size_t)nch + 1), st));
+    SALZ_HIP(fill_async(entry, 0xff, sizeof(uint32_t) * ((size_t)nch + 1), st));
     if (ne) {
-        SALZ_HIP(hipMemsetAsync(emark, 0, sizeof(uint32_t) * ne, st));
+        SALZ_HIP(fill_async(emark, 0, sizeof(uint32_t) * ne, st));
         // one block with its levels stored: the path in one launch (SALZ_PARSE=marksteps: a launch
         // per level)
         static const bool steps = env_flag("SALZ_PARSE", "marksteps");
@@ -561,8 +561,8 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
         }
         lens[b] = (size_t)out;
     }
-    SALZ_HIP(hipMemsetAsync(W, 0, sizeof(uint64_t) * (nwords + 1), st));
-    SALZ_HIP(hipMemsetAsync(Yk, 0, sizeof(uint32_t) * (nwords + 1), st));
+    SALZ_HIP(fill_async(W, 0, sizeof(uint64_t) * (nwords + 1), st));
+    SALZ_HIP(fill_async(Yk, 0, sizeof(uint32_t) * (nwords + 1), st));
     hipLaunchKernelGGL(k_emit_write, dim3(grid_for((size_t)nch + 1, kT)), dim3(kT), 0, st,
                        ws.text, tok, ntok, bl, N_last, ps.chunk, nch, cbits, cbytes, btotal, W, Yk, dst, stride,
                        binfo, ws.klog);

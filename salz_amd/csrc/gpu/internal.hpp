@@ -137,6 +137,8 @@ void workspace_free(Workspace &ws);
 
 // scans (scan.hip)
 size_t scan_temp_elems(size_t n);
+// hipMemsetAsync's semantics in one kernel launch (scan.hip)
+hipError_t fill_async(void *ptr, int value, size_t bytes, hipStream_t st);
 int scan_sum_u32(const uint32_t *in, uint32_t *out, size_t n, bool inclusive,
                  uint32_t *total_out, Workspace &ws, hipStream_t st);
 int scan_max_u32(const uint32_t *in, uint32_t *out, size_t n, bool inclusive,

@@ -186,7 +186,7 @@ int stage_lcp(Workspace &ws, const Blocks &bl, uint32_t *lcp_out)
         hipLaunchKernelGGL(k_phi, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.sa, bl, phi, derr);
         SALZ_LAUNCH_CHECK();
     }
-    SALZ_HIP(hipMemsetAsync(cnt, 0, 8, st));
+    SALZ_HIP(fill_async(cnt, 0, 8, st));
     hipLaunchKernelGGL(k_plcp_short, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, phi, bl, plv,
                        qa, cnt);
     SALZ_LAUNCH_CHECK();
@@ -203,8 +203,8 @@ int stage_lcp(Workspace &ws, const Blocks &bl, uint32_t *lcp_out)
         uint64_t W = L < kTaskBytes ? kTaskBytes : L;
         W = (W + kTaskBytes - 1) / kTaskBytes * kTaskBytes;
         uint32_t nch = (uint32_t)(W / kTaskBytes);
-        SALZ_HIP(hipMemsetAsync(found, 0xff, sizeof(uint32_t) * nitems, st));
-        SALZ_HIP(hipMemsetAsync(cnt + 1, 0, 4, st));
+        SALZ_HIP(fill_async(found, 0xff, sizeof(uint32_t) * nitems, st));
+        SALZ_HIP(fill_async(cnt + 1, 0, 4, st));
         size_t tasks = (size_t)nitems * nch;
         hipLaunchKernelGGL(k_plcp_long, dim3(grid_for(tasks * 64, 256)), dim3(256), 0, st,
                            ws.text, phi, bl, qa, nitems, nch, (uint32_t)L, found);

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
     const uint8_t *chold, uint8_t *chnew, uint32_t n, Blocks bl, uint32_t klog,
     uint32_t *__restrict__ changed, uint32_t *err, uint8_t *__restrict__ eflag,
     const uint8_t *__restrict__ wdirty, uint32_t *__restrict__ dsum, uint32_t *__restrict__ reach,
-    uint32_t *__restrict__ rlo, Lazy lz, int first, uint8_t *__restrict__ ttouch)
+    uint32_t *__restrict__ rlo, Lazy lz, int first, uint8_t *__restrict__ ttouch, uint32_t tgen)
 {
     constexpr uint32_t kDepth = DEP, kCDepth = CDEP;
     static_assert(kDepth <= kWin && kCDepth >= kDepth && ((kCDepth + 1) % kDepth) == 0, "ring depths");
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(kT) void k_parse_chunk(
             const size_t sx = sidx(ex != last_ex ? ex : n, klog);
             eflag[sx] = 1u;
             if (ttouch)  // (skipping passes: the 64-chunk tiles whose exit flags this walk set)
-                ttouch[sx >> (klog + 6)] = 1u;
+                ttouch[sx >> (klog + 6)] = (uint8_t)tgen;
             last_ex = ex;
             if (lz.summ && live && ex != tex) {  // (consecutive positions mostly share their exit)
                 tex = ex;
@@ -618,16 +618,16 @@ __global__ __launch_bounds__(kT) void k_mark_final(uint32_t n, uint32_t klog, co
 // bit per slot, 64 slots a word (one row of a 64-chunk tile), and per-word popcounts for the
 // scan that numbers E. A thread packs 8 flag bytes, 8 lanes one word.
 // (nd: the pass's dirty-wave count when its test ran; none dirty -> E unchanged, nothing to pack.
-// ttouch: the tiles whose flags the pass's walk set; the flags of the others, which accumulate
-// while waves skip passes, are as the last pack left them)
+// ttouch: the tiles whose flags the pass's walk set (tagged with the pass's generation tgen); the
+// flags of the others, which accumulate while waves skip passes, are as the last pack left them)
 __global__ __launch_bounds__(kT) void k_exit_pack(const uint64_t *__restrict__ eflag8, size_t S8, ExitBits eb,
                                                   const uint32_t *__restrict__ nd,
-                                                  const uint8_t *__restrict__ ttouch, uint32_t klog)
+                                                  const uint8_t *__restrict__ ttouch, uint32_t tgen, uint32_t klog)
 {
     if (nd && *nd == 0u)
         return;
     const size_t x = (size_t)blockIdx.x * kT + threadIdx.x;  // slots [8x, 8x + 8)
-    if (ttouch && !ttouch[(x < S8 ? 8 * x : 0) >> (klog + 6)])  // (tile-uniform: 8K slots per tile)
+    if (ttouch && ttouch[(x < S8 ? 8 * x : 0) >> (klog + 6)] != (uint8_t)tgen)  // (tile-uniform: 8K slots per tile)
         return;
     uint64_t v = eflag8[x < S8 ? x : 0];  // (unconditional load, clamped)
     v |= v >> 4;
@@ -996,6 +996,8 @@ __global__ __launch_bounds__(kT) void k_lazy_breaks(const uint8_t *__restrict__ 
                                                     uint32_t nchunks, uint32_t *__restrict__ brk)
 {
     const uint32_t k = blockIdx.x * kT + threadIdx.x;
+    if (k == 0)
+        brk[nchunks] = 0u;  // (the scan's last entry)
     if (k >= nchunks)
         return;
     brk[k] = !uni[k] || !uni[k + 1] || dl[k] != dl[k + 1] ? 1u : 0u;
@@ -1085,7 +1087,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     // per chunk: uniform cost shift since its last pass; per wave: dirty flag (lsc is free here)
     uint32_t *dsum = reinterpret_cast<uint32_t *>(ws.lsc);
     uint8_t *wdirty = reinterpret_cast<uint8_t *>(dsum + ps.nchunks);
-    SALZ_HIP(hipMemsetAsync(dsum, 0, sizeof(uint32_t) * ps.nchunks, st));
+    SALZ_HIP(fill_async(dsum, 0, sizeof(uint32_t) * ps.nchunks, st));
     // Range test of k_parse_mark (SALZ_PARSE=norange: per-candidate test only): each chunk's
     // farthest target, and per test the shift breaks per chunk and their prefix counts.
     const bool range_on = !env_flag("SALZ_PARSE", "norange");
@@ -1135,7 +1137,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     // position as changed)
     // counters changed (48), ndirty (50), listed chunks (51): zeroed here, then by the scalar reads
     // that consume them
-    SALZ_HIP(hipMemsetAsync(changed, 0, 16, st));
+    SALZ_HIP(fill_async(changed, 0, 16, st));
 
     ps.pst = ws.pst;
     ps.n_exit = 0;
@@ -1174,11 +1176,10 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                 hipLaunchKernelGGL(k_lazy_breaks, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, uni, dl, ps.nchunks,
                                    brk);
                 SALZ_LAUNCH_CHECK();
-                SALZ_HIP(hipMemsetAsync(brk + ps.nchunks, 0, sizeof(uint32_t), st));
                 if (scan_sum_u32(brk, pbrk, (size_t)ps.nchunks + 1, false, nullptr, ws, st) != 0)
                     return -1;
             } else if (range_on) {
-                SALZ_HIP(hipMemsetAsync(brk, 0, sizeof(uint32_t) * ((size_t)ps.nchunks + 1), st));
+                SALZ_HIP(fill_async(brk, 0, sizeof(uint32_t) * ((size_t)ps.nchunks + 1), st));
                 const size_t bthreads = (size_t)((ps.nchunks + 63) / 64) * 64 * (ps.chunk / kRowsBrk);
                 hipLaunchKernelGGL(k_shift_breaks, dim3(grid_for(bthreads, kT)), dim3(kT), 0, st, cin, cout, n, klog,
                                    ps.nchunks, brk);
@@ -1217,18 +1218,20 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             // wave clean, and stops at the read below with nothing changed)
         }
         if (entering) {  // offsets 0 (entries past the last chunk: uniform, delta 0)
-            SALZ_HIP(hipMemsetAsync(Lv[0], 0, sizeof(uint32_t) * 4 * nc64, st));  // Lv[0], Lv[1], dl
-            SALZ_HIP(hipMemsetAsync(uni, 1, nc64, st));
+            SALZ_HIP(fill_async(Lv[0], 0, sizeof(uint32_t) * 4 * nc64, st));  // Lv[0], Lv[1], dl
+            SALZ_HIP(fill_async(uni, 1, nc64, st));
         }
         // Exit flags accumulate once waves skip passes: a skipped chunk's exits stay marked
         // from the pass that chose them (stale exits only add nodes to the forest).
         if (!skipping)
-            SALZ_HIP(hipMemsetAsync(eflag, 0, S, st));
+            SALZ_HIP(fill_async(eflag, 0, S, st));
         uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
         uint8_t *wd = skipping && skip_on ? wdirty : nullptr;
         uint8_t *tt = wd ? ttouch : nullptr;  // (flags accumulate only while waves skip)
-        if (tt)
-            SALZ_HIP(hipMemsetAsync(tt, 0, ntiles, st));
+        // (tile flags carry the pass's generation 1..255: reset once every 255 passes, not per pass)
+        const uint32_t tgen = (uint32_t)(it % 255) + 1u;
+        if (ttouch && tgen == 1u)
+            SALZ_HIP(fill_async(ttouch, 0, ntiles, st));
         uint32_t *rch = it == 0 && range_on ? reach : nullptr;
         const Lazy lzw{lazy ? Lv[lc] : nullptr, lazy_on ? summ : nullptr, lazy_on ? chg : nullptr};
         // Chunks of K <= 128 (non-text and mid-size blocks) prefetch far targets 1 step and
@@ -1244,12 +1247,12 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             hipLaunchKernelGGL((near ? k_parse_chunk<CandPacked, 1, 3> : k_parse_chunk<CandPacked, 4, 7>),
                                dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, cand8,
                                nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr, eflag, wd, dsum, rch,
-                               rlo, lzw, it == 0 ? 1 : 0, tt);
+                               rlo, lzw, it == 0 ? 1 : 0, tt, tgen);
         else
             hipLaunchKernelGGL((near ? k_parse_chunk<CandFull, 1, 3> : k_parse_chunk<CandFull, 4, 7>),
                                dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, ws.cand,
                                it == 0 ? cand8 : nullptr, cin, ws.pst, chold, chnew, n, bl, klog, changed, derr,
-                               eflag, wd, dsum, rch, rlo, lzw, it == 0 ? 1 : 0, tt);
+                               eflag, wd, dsum, rch, rlo, lzw, it == 0 ? 1 : 0, tt, tgen);
         SALZ_LAUNCH_CHECK();
         // The exit set of the new decisions (E was marked by the chunk pass) as bits and word
         // counts, numbered by the scan, before the pass's one host read: that read then returns
@@ -1258,7 +1261,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         // Packing is skipped on "no dirty wave" only when the walk itself skipped the clean waves
         // (wd): under SALZ_PARSE=noskip every chunk is walked and E is packed every pass.
         hipLaunchKernelGGL(k_exit_pack, dim3(grid_for(S / 8, kT)), dim3(kT), 0, st,
-                           reinterpret_cast<const uint64_t *>(eflag), S / 8, eb, wd ? ndirty : nullptr, tt, klog);
+                           reinterpret_cast<const uint64_t *>(eflag), S / 8, eb, wd ? ndirty : nullptr, tt, tgen, klog);
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u32(eb.wcnt, eb.wpre, S / 64, false, etotal, ws, st) != 0)
             return -1;

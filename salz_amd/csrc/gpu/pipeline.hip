@@ -583,7 +583,7 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P
         SALZ_HIP(hipMemcpyAsync(ws.text, src, P, hipMemcpyDeviceToDevice, st));
     else if (copy_h2d(ws, ws.text, src, P) != 0)
         return -1;
-    SALZ_HIP(hipMemsetAsync(ws.text + P, 0, 128, st));
+    SALZ_HIP(fill_async(ws.text + P, 0, 128, st));
     // (a batch's chunk length follows its block size: the per-block trade-off of pass count
     // against pass length, parse.hip)
     ws.klog = parse_chunk_log(nbz == 1 ? P : bs);
@@ -977,7 +977,7 @@ static int dist_piece(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t N, uint32
     hipStream_t st = ws.stream;
     ws.stats = StageStats{};
     SALZ_HIP(hipMemcpyAsync(ws.text, d_text, N, hipMemcpyDeviceToDevice, st));
-    SALZ_HIP(hipMemsetAsync(ws.text + N, 0, 128, st));
+    SALZ_HIP(fill_async(ws.text + N, 0, 128, st));
     const uint32_t n = (uint32_t)(N - 8);
     uint32_t m0 = 0;
     if (sort(ws, n, &m0) != 0)

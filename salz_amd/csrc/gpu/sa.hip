@@ -419,9 +419,12 @@ __device__ __forceinline__ void surv_masks(const HeadBits &hb, size_t w, uint32_
 }
 
 // Per wave word: (survivor entries << 32 | survivor heads); k_commit reads their exclusive scan.
-__global__ __launch_bounds__(kT) void k_surv(HeadBits hb, uint32_t m, uint64_t *__restrict__ P)
+__global__ __launch_bounds__(kT) void k_surv(HeadBits hb, uint32_t m, uint64_t *__restrict__ P,
+                                             uint64_t *__restrict__ lcount)
 {
     const size_t w = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (w < 2)  // k_commit's large-group counters (lcount[0..1]), zeroed for its atomics
+        lcount[w] = 0;
     if (w >= ((size_t)m + 63) / 64)
         return;
     uint64_t se, sh;
@@ -1389,7 +1392,7 @@ int block_alpha_bits(Workspace &ws, uint32_t n)
         return 0;
     hipStream_t st = ws.stream;
     uint32_t *words = reinterpret_cast<uint32_t *>(ws.dscal) + 240;
-    SALZ_HIP(hipMemsetAsync(words, 0, 8 * sizeof(uint32_t), st));
+    SALZ_HIP(fill_async(words, 0, 8 * sizeof(uint32_t), st));
     const size_t P = (size_t)n + 8;
     hipLaunchKernelGGL(k_alpha_presence, dim3(grid_for(P, kT * 16) < 2048 ? grid_for(P, kT * 16) : 2048), dim3(kT), 0,
                        st, ws.text, P, words);
@@ -1420,7 +1423,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     uint32_t *d32 = reinterpret_cast<uint32_t *>(ws.dscal);
     uint64_t *d64 = ws.dscal + 8;
     uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
-    SALZ_HIP(hipMemsetAsync(derr, 0, sizeof(uint32_t) * 12, st));
+    SALZ_HIP(fill_async(derr, 0, sizeof(uint32_t) * 12, st));
     ws.stats.sa_rounds = 0;
     ws.stats.sa_sorted_elems = 0;
     ws.stats.sa_dc3_levels = 0;
@@ -1455,7 +1458,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     int codes_raw = 1;
     if (alpha_on && n >= 64) {
         uint32_t *words = reinterpret_cast<uint32_t *>(ws.dscal) + 240;
-        SALZ_HIP(hipMemsetAsync(words, 0, 8 * sizeof(uint32_t), st));
+        SALZ_HIP(fill_async(words, 0, 8 * sizeof(uint32_t), st));
         const size_t P = (size_t)n + 8;
         hipLaunchKernelGGL(k_alpha_presence, dim3(grid_for(P, kT * 16) < 2048 ? grid_for(P, kT * 16) : 2048),
                            dim3(kT), 0, st, ws.text, P, words);
@@ -1534,7 +1537,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                            tmapped);
         SALZ_LAUNCH_CHECK();
     }
-    SALZ_HIP(hipMemsetAsync(ws.rank + n, 0, sizeof(uint32_t), st));  // rank[n] = 0
+    SALZ_HIP(fill_async(ws.rank + n, 0, sizeof(uint32_t), st));  // rank[n] = 0
     if (bl.nb > 1) {
         hipLaunchKernelGGL(k_dead_ranks, dim3(grid_for(8u * (bl.nb - 1u), kT)), dim3(kT), 0, st, bl, ws.rank);
         SALZ_LAUNCH_CHECK();
@@ -1654,14 +1657,14 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             const uint32_t nwin = grid_for(m, kSegT);
             uint32_t *pw = reinterpret_cast<uint32_t *>(ws.lsc);
             SegPlan plan{pw, pw + nwin, pw + 2 * nwin, pw + 3 * nwin};
-            SALZ_HIP(hipMemsetAsync(plan.lo, 0xff, sizeof(uint32_t) * nwin, st));
+            SALZ_HIP(fill_async(plan.lo, 0xff, sizeof(uint32_t) * nwin, st));
             hipLaunchKernelGGL(k_seg_plan, dim3(grid_for(G_act, kT)), dim3(kT), 0, st, tab.ginfo, G_act, plan);
             SALZ_LAUNCH_CHECK();
             // run-start bits per window (64 words each) and fix flags, in pst (free until the large
             // groups' extraction)
             uint64_t *rb = ws.pst;
             uint32_t *need = reinterpret_cast<uint32_t *>(ws.pst + (size_t)nwin * (kSegCap / 64));
-            SALZ_HIP(hipMemsetAsync(need, 0, sizeof(uint32_t) * nwin, st));
+            SALZ_HIP(fill_async(need, 0, sizeof(uint32_t) * nwin, st));
             hipLaunchKernelGGL(k_seg_sort<true>, dim3(nwin), dim3(kSegThreads), 0, st, K, V, gin, plan, tab.ginfo,
                                m, tbits, seg_tiny_text, rb, need, derr, lsd_bits);
             SALZ_LAUNCH_CHECK();
@@ -1735,7 +1738,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                 const uint32_t nwin = grid_for(m, kSegT);
                 uint32_t *pw = reinterpret_cast<uint32_t *>(ws.lsc);  // free during the sort
                 SegPlan plan{pw, pw + nwin, pw + 2 * nwin, pw + 3 * nwin};
-                SALZ_HIP(hipMemsetAsync(plan.lo, 0xff, sizeof(uint32_t) * nwin, st));
+                SALZ_HIP(fill_async(plan.lo, 0xff, sizeof(uint32_t) * nwin, st));
                 hipLaunchKernelGGL(k_seg_plan, dim3(grid_for(G_act, kT)), dim3(kT), 0, st, tab.ginfo,
                                    G_act, plan);
                 SALZ_LAUNCH_CHECK();
@@ -1815,11 +1818,10 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         uint64_t *P = reinterpret_cast<uint64_t *>(ws.u1);
         {
             const size_t nw = ((size_t)m + 63) / 64;
-            hipLaunchKernelGGL(k_surv, dim3(grid_for(nw, kT)), dim3(kT), 0, st, hb, m, P);
+            hipLaunchKernelGGL(k_surv, dim3(grid_for(nw, kT)), dim3(kT), 0, st, hb, m, P, d64 + 1);
             SALZ_LAUNCH_CHECK();
             if (scan_sum_u64(P, P, nw, false, d64, ws, st) != 0)
                 return -1;
-            SALZ_HIP(hipMemsetAsync(d64 + 1, 0, 2 * sizeof(uint64_t), st));
         }
         // Rank updates:
         //   direct  k_commit writes rank[i] (small rounds);
@@ -1943,7 +1945,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     }
     static const bool check = env_flag("SALZ_CHECK", "sa");
     if (check && !dist) {
-        SALZ_HIP(hipMemsetAsync(ws.u0, 0, sizeof(uint32_t) * n, st));
+        SALZ_HIP(fill_async(ws.u0, 0, sizeof(uint32_t) * n, st));
         hipLaunchKernelGGL(k_sa_check, dim3(grid_for(nsa, kT)), dim3(kT), 0, st, ws.sa, nsa, n, ws.u0, derr);
         SALZ_LAUNCH_CHECK();
         if (read_scalars(ws, 0, 256, "sa.check") != 0)

@@ -249,6 +249,38 @@ int scan_sum_u8(const uint8_t *in, uint32_t *out, size_t n, bool inclusive, uint
                                                          ws.scan_tmp_bytes / 4, st);
 }
 
+// hipMemsetAsync in one launch: the runtime splits a small or unaligned fill into two or three
+// kernels, and the per-round / per-pass flag and counter resets of a block added up to about 100
+// fill launches per 16 MiB block (profiles/r05fa_*). 16-byte stores, byte stores for an unaligned
+// head and the tail.
+__global__ __launch_bounds__(256) void k_fill(uint8_t *__restrict__ p, uint32_t v4, size_t bytes, size_t head)
+{
+    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x, nt = (size_t)gridDim.x * 256;
+    const uint8_t v = (uint8_t)v4;
+    if (t < head)
+        p[t] = v;
+    uint8_t *q = p + head;
+    const size_t body = (bytes - head) / 16, tail = (bytes - head) % 16;
+    uint4 *q4 = reinterpret_cast<uint4 *>(q);
+    for (size_t i = t; i < body; i += nt)
+        q4[i] = make_uint4(v4, v4, v4, v4);
+    if (t < tail)
+        q[body * 16 + t] = v;
+}
+
+hipError_t fill_async(void *ptr, int value, size_t bytes, hipStream_t st)
+{
+    if (bytes == 0)
+        return hipSuccess;
+    const uint32_t b = (uint8_t)value, v4 = b * 0x01010101u;
+    const size_t mis = (uintptr_t)ptr & 15u, head = mis ? (16 - mis < bytes ? 16 - mis : bytes) : 0;
+    const size_t body = (bytes - head) / 16;
+    const size_t want = body > 16 ? (body + 255) / 256 : 1;
+    const unsigned grid = (unsigned)(want < 8192 ? want : 8192);
+    hipLaunchKernelGGL(k_fill, dim3(grid), dim3(256), 0, st, static_cast<uint8_t *>(ptr), v4, bytes, head);
+    return hipGetLastError();
+}
+
 int scan_sum_u64(const uint64_t *in, uint64_t *out, size_t n, bool inclusive,
                  uint64_t *total_out, Workspace &ws, hipStream_t st)
 {

@@ -89,7 +89,7 @@ int scatter_staged(Src src, uint32_t m, uint32_t nidx, uint32_t *dst, uint32_t s
         set_error("staged scatter: %u windows of 2^%u exceed the staging buffer (%zu)", nwin, rlog, stage_cap);
         return -1;
     }
-    SALZ_HIP(hipMemsetAsync(rfill, 0, nwin * sizeof(uint32_t), st));
+    SALZ_HIP(fill_async(rfill, 0, nwin * sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_sc_stage<Src>, dim3(grid_for(m, kScTile)), dim3(kScThreads), 0, st, src, m, rlog, rfill,
                        stage);
     SALZ_LAUNCH_CHECK();
