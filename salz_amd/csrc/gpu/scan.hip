@@ -10,6 +10,7 @@ namespace {
 constexpr int kScanThreads = 256;
 constexpr int kScanItems = 16;
 constexpr int kScanTile = kScanThreads * kScanItems;
+constexpr size_t kInlineTiles = 1024;
 
 template <typename T> struct SumOp {
     __device__ __forceinline__ static T id() { return T(0); }
@@ -76,7 +77,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const TI *__restri
 template <typename T, typename Op, typename TI = T>
 __global__ __launch_bounds__(kScanThreads) void k_scan_tiles(const TI *__restrict__ in, T *out,
                                                              size_t n, const T *__restrict__ carry,
-                                                             int inclusive, T *total_out)
+                                                             int inclusive, T *total_out,
+                                                             const T *__restrict__ partial)
 {
     __shared__ T s[kScanTile + kScanTile / 16];
     __shared__ T wsum[4];
@@ -99,6 +101,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_tiles(const TI *__restric
     T total;
     T run = block_excl<T, Op>(sum, wsum, total, op);
     T c = carry ? carry[blockIdx.x] : Op::id();
+    if (partial) {  // (kernel-uniform) the carry reduced here from the tiles' totals before this one
+        T a = Op::id();
+        for (uint32_t t = threadIdx.x; t < blockIdx.x; t += kScanThreads)
+            a = op(a, partial[t]);
+        T ca;
+        block_excl<T, Op>(a, wsum, ca, op);
+        c = ca;
+    }
     run = op(c, run);
 #pragma unroll
     for (int k = 0; k < kScanItems; k++) {
@@ -177,7 +187,7 @@ int scan_impl(const TI *in, T *out, size_t n, bool inclusive, T *total_out, T *t
     size_t tiles = (n + kScanTile - 1) / kScanTile;
     if (tiles == 1) {
         hipLaunchKernelGGL((k_scan_tiles<T, Op, TI>), dim3(1), dim3(kScanThreads), 0, st, in, out,
-                           n, (const T *)nullptr, inclusive ? 1 : 0, total_out);
+                           n, (const T *)nullptr, inclusive ? 1 : 0, total_out, (const T *)nullptr);
         SALZ_LAUNCH_CHECK();
         return 0;
     }
@@ -189,11 +199,21 @@ int scan_impl(const TI *in, T *out, size_t n, bool inclusive, T *total_out, T *t
     hipLaunchKernelGGL((k_scan_reduce<T, Op, TI>), dim3((unsigned)tiles), dim3(kScanThreads), 0,
                        st, in, n, partial);
     SALZ_LAUNCH_CHECK();
+    // Up to kInlineTiles tiles each scanning block reduces the totals before it itself (at most
+    // 1023 reads, L2-resident): two launches instead of three (SALZ_SCAN=3pass: the partials'
+    // own scan launch).
+    static const bool three = env_flag("SALZ_SCAN", "3pass");
+    if (tiles <= kInlineTiles && !three) {
+        hipLaunchKernelGGL((k_scan_tiles<T, Op, TI>), dim3((unsigned)tiles), dim3(kScanThreads), 0, st,
+                           in, out, n, (const T *)nullptr, inclusive ? 1 : 0, total_out, (const T *)partial);
+        SALZ_LAUNCH_CHECK();
+        return 0;
+    }
     if (scan_impl<T, Op>(partial, partial, tiles, false, nullptr, tmp + tiles,
                          tmp_elems - tiles, st) != 0)
         return -1;
     hipLaunchKernelGGL((k_scan_tiles<T, Op, TI>), dim3((unsigned)tiles), dim3(kScanThreads), 0, st,
-                       in, out, n, (const T *)partial, inclusive ? 1 : 0, total_out);
+                       in, out, n, (const T *)partial, inclusive ? 1 : 0, total_out, (const T *)nullptr);
     SALZ_LAUNCH_CHECK();
     return 0;
 }
