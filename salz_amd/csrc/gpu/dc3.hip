@@ -467,7 +467,7 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
     uint8_t *mark = d.top;
     uint32_t *sar = nullptr;
     // Naming by the triples' presence bitmap (SALZ_SA=dc3sort: by sorting at every level)
-    static const bool lut_off = env_flag("SALZ_SA", "dc3sort");
+    const bool lut_off = env_flag("SALZ_SA", "dc3sort");  // (read per call: the tests switch it)
     const uint32_t nwords = 3 * b <= kLutMaxBits ? ((1u << (3 * b)) + 31u) / 32u : 0u;
     const size_t lut_room = nwords > kLutWords ? 2 * (size_t)nwords : 2 * (size_t)kLutWords;
     if (nwords && !lut_off && ws.radix_counts_elems >= lut_room) {

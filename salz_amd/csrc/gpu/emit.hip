@@ -489,7 +489,7 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
         SALZ_HIP(fill_async(emark, 0, sizeof(uint32_t) * ne, st));
         // one block with its levels stored: the path in one launch (SALZ_PARSE=marksteps: a launch
         // per level)
-        static const bool steps = env_flag("SALZ_PARSE", "marksteps");
+        const bool steps = env_flag("SALZ_PARSE", "marksteps");
         const bool one = nb == 1 && ps.snaps && ps.levels > 0 && !steps;
         if (one) {
             // (a path takes at most one exit per chunk: nch + 1 nodes with the root)

@@ -1241,7 +1241,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         // From the fourth pass on, where few waves walk and a pass is one lane's latency chain,
         // the 4 / 7 distances again (SALZ_PARSE=farlate=N: from pass N; mixed 100 MB parse 7.88 ->
         // 7.77 ms at 3, 7.79 at 5, Silesia-sized blocks even to +1%: r05fl_parse_farlate_ab.txt)
-        static const long far_late = env_num("SALZ_PARSE", "farlate", 3);
+        const long far_late = env_num("SALZ_PARSE", "farlate", 3);
         const bool near = klog <= 7 && it < far_late;
         if (pack && it > 0)
             hipLaunchKernelGGL((near ? k_parse_chunk<CandPacked, 1, 3> : k_parse_chunk<CandPacked, 4, 7>),
@@ -1320,7 +1320,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         int jc = 0;
         if (snaps) {
             // (SALZ_PARSE=jump2: two levels per launch everywhere)
-            static const bool jump2_only = env_flag("SALZ_PARSE", "jump2");
+            const bool jump2_only = env_flag("SALZ_PARSE", "jump2");
             for (uint32_t k = 0; k < K;) {
                 if (!jump2_only && k + 3 <= K && (size_t)(k + 4) * ne <= snap_cap) {
                     hipLaunchKernelGGL(k_jump3, dim3(grid_for(ne, kT)), dim3(kT), 0, st, snap + (size_t)k * ne, js[jc],

@@ -1844,7 +1844,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         const uint32_t ihi = mode == 0 ? 0xffffffffu : mode == 1 ? span : 0u;
         // (the text round's keys with the survivors' entries, where Kx is not the rank list: SALZ_SA=
         // keystext keeps the separate gather)
-        static const bool keys_apart = env_flag("SALZ_SA", "keystext");
+        const bool keys_apart = env_flag("SALZ_SA", "keystext");
         const bool fuse_keys = textnext && mode == 0 && !keys_apart;
         const TextNext tn{tmapped, fuse_keys ? Kx : nullptr, bl, alpha, h};
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, headpos,

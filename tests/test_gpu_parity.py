@@ -83,6 +83,17 @@ def test_stages_match_oracle(ctx, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
+@pytest.mark.parametrize("scan", ["", "3pass"])
+@pytest.mark.parametrize("kind,n,seed,alpha", [("mixed", 3000000, 4, 0), ("text", 1500000, 8, 0)])
+def test_scan_launch_shapes(ctx, monkeypatch, scan, kind, n, seed, alpha):
+    """Scans of 2..1024 tiles with each tile reducing its own carry (the default) or with the
+    tile totals scanned by a launch of their own (SALZ_SCAN=3pass) give the oracle's stream."""
+    monkeypatch.setenv("SALZ_SCAN", scan)
+    src = _make(kind, n, seed, alpha)
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and ctx.encode(src) == ref
+
+
 @pytest.mark.parametrize("vec", [v for v in golden("appendix_c.json")["vectors"] if v["n"] <= 1 << 24],
                          ids=lambda v: f"{v['kind']}{v['n']}-{v['alphabet']}")
 def test_appendix_c_golden(ctx, vec):
