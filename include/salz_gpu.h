@@ -108,7 +108,10 @@ typedef struct salz_dist_ops {
  * this rank's SA range and the LCP of each entry with its predecessor (entry 0 of a piece is
  * left for the caller to fix, see salz_gpu_encode_from_sa). offsets: nranks + 1 values.
  * *lcp_ok = 0 when the LCPs were not kept (very long repeats: the PLCP stage recomputes them).
- * Collective: every rank calls it with the same block. Returns 0 / -1. */
+ * Collective: every rank calls it with the same block. Returns 0 / -1, or 1 on every rank when
+ * the block is not split: blocks of 2^20 suffixes or more that the repetition probe sends to DC3
+ * (long repeats everywhere), which the split sorter does not run; encode those whole on one GPU
+ * (salz_gpu_encode_device). */
 int salz_gpu_dist_suffix_array(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t N, int nranks, int rank,
                                const salz_dist_ops *ops, uint32_t *d_xsend, uint32_t *d_xrecv,
                                size_t xcap, uint32_t *d_sa_piece, uint32_t *d_lcp_piece,

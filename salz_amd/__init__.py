@@ -92,8 +92,11 @@ lib.salz_gpu_encode_batch_device.argtypes = [ctypes.c_void_p, _u8p, _sz, _sz, _u
 lib.salz_gpu_encode_batch_device.restype = ctypes.c_int
 lib.salz_debug_init_order.argtypes = [_sz, _sz, ctypes.c_void_p]
 lib.salz_debug_init_order.restype = ctypes.c_int
-lib.salz_debug_radix_selftest.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_uint64]
+lib.salz_debug_radix_selftest.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                          ctypes.c_int]
 lib.salz_debug_radix_selftest.restype = ctypes.c_long
+lib.salz_debug_xchg_offsets.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_uint64)] * 4
+lib.salz_debug_xchg_offsets.restype = ctypes.c_int
 lib.salz_encode_blocks.argtypes = [_u8p, _sz, _sz, _u8p, _szp, ctypes.c_int]
 lib.salz_encode_blocks.restype = ctypes.c_int
 lib.salz_blocks_len_max.argtypes = [_sz, _sz]
@@ -177,11 +180,23 @@ def last_error() -> str:
     return lib.salz_gpu_last_error().decode(errors="replace")
 
 
-def radix_selftest(m: int, bits: int, iters: int = 2, seed: int = 1, device: int = 0) -> int:
+def xchg_offsets(send_counts, recv_counts):
+    """Test hook (host only): where each peer's run starts in the send and receive buffers of one
+    exchange of the split suffix sort's in-library RCCL path (dsa.hip xchg_offsets)."""
+    n = len(send_counts)
+    U = ctypes.c_uint64 * n
+    so, ro = U(), U()
+    if lib.salz_debug_xchg_offsets(n, U(*send_counts), U(*recv_counts), so, ro) != 0:
+        raise SalzError("xchg_offsets: invalid arguments")
+    return list(so), list(ro)
+
+
+def radix_selftest(m: int, bits: int, iters: int = 2, seed: int = 1, device: int = 0, nine: bool = False) -> int:
     """Test hook: the suffix sorter's LSD radix sort on m random (key, index) pairs of `bits` key
-    bits, on the device; returns the number of runs whose output was out of order, unstable or
+    bits, on the device, with 8-bit digits or (nine) 9-bit digits wherever they save a pass (the
+    rank rounds' plan); returns the number of runs whose output was out of order, unstable or
     not a permutation of the input (-1: allocation failed)."""
-    return lib.salz_debug_radix_selftest(device, m, bits, iters, seed)
+    return lib.salz_debug_radix_selftest(device, m, bits, iters, seed, 1 if nine else 0)
 
 
 def encoded_len_max(plain_len: int) -> int:

@@ -186,8 +186,7 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp, uint4 *__restrict__ stage,
     uint32_t *__restrict__ sp, uint32_t *__restrict__ rfill,
     uint32_t rlog, uint32_t *__restrict__ qp, uint32_t *__restrict__ qp_len,
-    uint32_t *__restrict__ qn, uint32_t *__restrict__ qn_len, uint32_t *__restrict__ qcount,
-    unsigned long long *prof, int pk)
+    uint32_t *__restrict__ qn, uint32_t *__restrict__ qn_len, uint32_t *__restrict__ qcount, int pk)
 {
     __shared__ uint32_t vsa[2 * kB + kNear];  // heap: [1, kB) tree, [kB, 2kB) leaves, + pad
     __shared__ uint32_t vlc[2 * kB + kNear];
@@ -198,8 +197,6 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     if (tid < kMaxRanges)
         rbase[tid] = 0;
     const uint32_t b0 = blockIdx.x * kB;
-    // SALZ_PROF_ANSV (diagnostics): per-phase cycle totals of thread 0
-    const unsigned long long t0 = prof ? clock64() : 0ull;
 
     // Build the block's min-tree (heap: node k has children 2k, 2k + 1; leaves at kB + l) and
     // publish its internal nodes into the global heap. Thread t owns leaves 8t .. 8t + 7: the
@@ -286,11 +283,6 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
         rbase[tid] = (tid << rlog) + atomicAdd(&rfill[tid], rbase[tid]);
     __syncthreads();
 
-    unsigned long long t1 = 0;
-    if (prof) {
-        __syncthreads();
-        t1 = clock64();
-    }
     // Phase 1: most nearest smaller values are a few ranks away. Scan up to kNear neighbours
     // on each side (lanes read consecutive LDS words: no bank conflicts); queue the rest.
     // The walk queue holds kWQ entries (12% of 2 kB queries miss on text); a full queue walks
@@ -377,9 +369,6 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
         }
     }
     __syncthreads();
-    unsigned long long t2 = 0;
-    if (prof)
-        t2 = clock64();
 
     // Phase 2: the queued queries walk the block's min-tree; answers outside the block go to
     // the global queues (k_ansv_global continues from the block root).
@@ -387,16 +376,6 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     for (uint32_t w = tid; w < nw; w += kT)
         block_walk(wq[w], slot_of(wq[w] >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len,
                    qcount, qbase, bl, pk, rlog);
-    if (prof) {
-        __syncthreads();
-        if (tid == 0) {
-            const unsigned long long t3 = clock64();
-            atomicAdd(&prof[0], t1 - t0);
-            atomicAdd(&prof[1], t2 - t1);
-            atomicAdd(&prof[2], t3 - t2);
-            atomicAdd(&prof[3], (unsigned long long)nw);
-        }
-    }
 }
 
 // Staged answers -> cand in the interleaved text-order layout. Slots are grouped by text
@@ -438,91 +417,6 @@ __global__ __launch_bounds__(kT) void k_cand_scatter(const uint32_t *__restrict_
     if (bad_index(p >= npos, err, kErrAnsv))
         return;
     cand[sidx(p, klog)] = c;
-}
-
-// Second staging level (SALZ_SA=ansv2, large blocks): each text range's run is counting-sorted by
-// its 8 sub-ranges of 2^(rlog - 3) positions in LDS and appended to per-sub-range runs (structure
-// of arrays: positions, then the two halves), so the final scatter writes cand through windows of
-// 2 MB, which an XCD's 4 MB L2 holds whole (its 16-byte stores merge into full lines there instead
-// of leaving L2 as 32-byte partial-sector writes). Not the default: see stage_candidates.
-constexpr uint32_t kRsItems = 16, kRsTile = kT * kRsItems;
-__global__ __launch_bounds__(kT) void k_ansv_restage(const uint32_t *__restrict__ sp, const uint4 *__restrict__ stage,
-                                                     uint32_t rlog, const uint32_t *__restrict__ rfill,
-                                                     uint32_t *__restrict__ sfill, uint32_t *__restrict__ sp2,
-                                                     uint2 *__restrict__ lo2, uint2 *__restrict__ hi2)
-{
-    __shared__ uint32_t cnt[8], base[8];
-    const uint32_t tiles = 1u << (rlog - 12);  // kRsTile = 4096 entries per tile
-    const uint32_t r = blockIdx.x / tiles, k = blockIdx.x % tiles, tid = threadIdx.x, lane = tid & 63u;
-    const uint32_t fill = rfill[r];
-    const size_t t0 = (size_t)k * kRsTile;
-    if (t0 >= fill)
-        return;
-    if (tid < 8)
-        cnt[tid] = 0;
-    __syncthreads();
-    const size_t run = (size_t)r << rlog;
-    const uint32_t sub = rlog - 3;
-    uint32_t pv[kRsItems], loc[kRsItems];
-    uint4 cv[kRsItems];
-#pragma unroll
-    for (uint32_t j = 0; j < kRsItems; j++) {  // every load issued first (clamped, unconditional)
-        const size_t x = t0 + (size_t)j * kT + tid, xc = x < fill ? x : t0;
-        pv[j] = sp[run + xc];
-        cv[j] = stage[run + xc];
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kRsItems; j++) {
-        const bool ok = t0 + (size_t)j * kT + tid < fill;
-        const uint32_t b = (pv[j] >> sub) & 7u;
-        uint64_t peers = wave_ballot(ok);
-#pragma unroll
-        for (int q = 0; q < 3; q++) {
-            const bool bit = (b >> q) & 1u;
-            const uint64_t bb = wave_ballot(bit);
-            peers &= bit ? bb : ~bb;
-        }
-        const int leader = peers ? (int)__ffsll((unsigned long long)peers) - 1 : (int)lane;
-        uint32_t old = 0;
-        if (ok && (int)lane == leader)
-            old = atomicAdd(&cnt[b], (uint32_t)__popcll(peers));
-        loc[j] = shfl_u32(old, leader) + count_below(peers);
-    }
-    __syncthreads();
-    if (tid < 8 && cnt[tid])
-        base[tid] = ((r * 8u + tid) << sub) + atomicAdd(&sfill[r * 8u + tid], cnt[tid]);
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < kRsItems; j++) {
-        if (t0 + (size_t)j * kT + tid >= fill)
-            continue;
-        const uint32_t dst = base[(pv[j] >> sub) & 7u] + loc[j];
-        sp2[dst] = pv[j];
-        lo2[dst] = make_uint2(cv[j].x, cv[j].y);
-        hi2[dst] = make_uint2(cv[j].z, cv[j].w);
-    }
-}
-
-// The sub-range runs -> cand, XCD-aware like k_cand_scatter (XCD x takes sub-ranges x, x + 8, ..).
-__global__ __launch_bounds__(kT) void k_cand_scatter2(const uint32_t *__restrict__ sp2, const uint2 *__restrict__ lo2,
-                                                      const uint2 *__restrict__ hi2, uint32_t npos,
-                                                      uint4 *__restrict__ cand, uint32_t klog, uint32_t slog,
-                                                      uint32_t nsub, const uint32_t *__restrict__ sfill,
-                                                      uint32_t *__restrict__ err)
-{
-    const uint32_t g = blockIdx.x, tiles = 1u << (slog - 8);
-    const uint32_t k = g >> 3, r = (g & 7u) + 8u * (k >> (slog - 8));
-    if (r >= nsub)
-        return;
-    const size_t x = (size_t)(k & (tiles - 1u)) * kT + threadIdx.x;
-    if (x >= sfill[r])
-        return;
-    const size_t i = ((size_t)r << slog) + x;
-    const uint32_t p = sp2[i];
-    const uint2 a = lo2[i], b = hi2[i];
-    if (bad_index(p >= npos, err, kErrAnsv))
-        return;
-    cand[sidx(p, klog)] = make_uint4(a.x, a.y, b.x, b.y);
 }
 
 __global__ void k_tree_level(uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp,
@@ -661,15 +555,10 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
         SALZ_HIP(fill_async(tlcp + nblocks + used_blocks, 0xff,
                                 sizeof(uint32_t) * (nblocks - used_blocks), st));
     }
-    static const bool prof_on = env_flag("SALZ_DEBUG", "ansv");
-    unsigned long long *prof = prof_on ? reinterpret_cast<unsigned long long *>(ws.dscal) + 200 : nullptr;
-    if (prof)
-        SALZ_HIP(fill_async(prof, 0, 32, st));
     // Staging: text ranges of 2^rlog positions (cand windows of 16 << rlog bytes; 16 MB by
     // default: 2^19 and 2^21 measured slower), at most kMaxRanges of them. Slots sp / stage
     // alias scratch that is free here.
-    uint32_t rlog = (uint32_t)env_num("SALZ_SA", "rlog", 20);  // (test switch: staging range size)
-    rlog = rlog < 17 ? 17 : rlog > 26 ? 26 : rlog;
+    uint32_t rlog = 20;
     while ((((uint64_t)npos - 1) >> rlog) + 1 > kMaxRanges)
         rlog++;
     uint32_t *rfill = ws.radix_counts;
@@ -682,50 +571,18 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
     }
     SALZ_HIP(fill_async(rfill, 0, kMaxRanges * sizeof(uint32_t), st));
     // packed staging (no position array) where offsets, lengths and range bits fit 16 bytes
-    // (SALZ_SA=ansvsp: the position array always)
-    const bool two_req = npos > (1u << 22) && env_flag("SALZ_SA", "ansv2");
-    const int pk = !two_req && npos <= (1u << 27) && rlog <= 20 && !env_flag("SALZ_SA", "ansvsp") ? 1 : 0;
+    // (round 5: C2 ANSV 3.72 -> 3.51 ms against the position array, which blocks past 2^27
+    // positions keep). A second staging level (each run re-sorted into 2 MB windows before the
+    // scatter) measured slower in round 5 (C2 ANSV 3.65 -> 4.04 ms) and was removed in round 6.
+    const int pk = npos <= (1u << 27) && rlog <= 20 ? 1 : 0;
     hipLaunchKernelGGL(k_ansv_local, dim3(used_blocks), dim3(kT), 0, st, ws.sa, lcp, n, bl, np2, tsa,
-                       tlcp, stage, sp, rfill, rlog, qp, qpl, qn, qnl, cnt, prof, pk);
+                       tlcp, stage, sp, rfill, rlog, qp, qpl, qn, qnl, cnt, pk);
     SALZ_LAUNCH_CHECK();
     const uint32_t nranges = (uint32_t)((((uint64_t)npos - 1) >> rlog) + 1);
-    // SALZ_SA=ansv2: a second staging level for large blocks (cand past 64 MB). Measured slower on
-    // C2 (round 5, tools/ab_env.sh on one box): ANSV 3.65 -> 4.04 ms, the re-sort 0.86 ms and the
-    // 2 MB-window scatter still 1.20 ms against 1.71 ms for the one 16 MB-window scatter, since
-    // every window's lines are written back once it moves on. Kept as a tested option.
-    const bool two = npos > (1u << 22) && env_flag("SALZ_SA", "ansv2") &&
-                     ws.radix_counts_elems >= (size_t)kMaxRanges * 9;
-    if (two) {
-        uint32_t *sfill = rfill + kMaxRanges;  // per sub-range fill
-        SALZ_HIP(fill_async(sfill, 0, (size_t)kMaxRanges * 8 * sizeof(uint32_t), st));
-        uint32_t *sp2 = ws.rank;  // (free after the suffix sort; the parse takes it later)
-        uint2 *lo2 = reinterpret_cast<uint2 *>(ws.g64), *hi2 = reinterpret_cast<uint2 *>(ws.pst);
-        hipLaunchKernelGGL(k_ansv_restage, dim3(nranges << (rlog - 12)), dim3(kT), 0, st, sp, stage, rlog, rfill, sfill,
-                           sp2, lo2, hi2);
-        SALZ_LAUNCH_CHECK();
-        const uint32_t slog = rlog - 3, nsub = nranges * 8u;
-        const uint32_t sgrid = 8u * ((nsub + 7u) / 8u) << (slog - 8);
-        hipLaunchKernelGGL(k_cand_scatter2, dim3(sgrid), dim3(kT), 0, st, sp2, lo2, hi2, npos, ws.cand, ws.klog, slog,
-                           nsub, sfill, derr);
-        SALZ_LAUNCH_CHECK();
-    } else {
-        const uint32_t sgrid = 8u * ((nranges + 7u) / 8u) << (rlog - 8);
-        hipLaunchKernelGGL(k_cand_scatter, dim3(sgrid), dim3(kT), 0, st, sp, stage, npos, ws.cand,
-                           ws.klog, rlog, nranges, rfill, derr, pk);
-        SALZ_LAUNCH_CHECK();
-    }
-    if (prof) {
-        if (read_scalars(ws, 0, (kQCountWord + 2 * kShards) * sizeof(uint32_t), "ansv.prof") != 0)
-            return -1;
-        const uint64_t *h = ws.hscal + 200;
-        uint32_t gq[2] = {0, 0};
-        for (uint32_t s = 0; s < 2 * kShards; s++)
-            gq[s & 1] += reinterpret_cast<uint32_t *>(ws.hscal)[kQCountWord + s];
-        fprintf(stderr, "ansv_local: %u blocks, cycles/block build %.0f near %.0f tree %.0f; "
-                "queued %.3f per leaf; global %u + %u\n", used_blocks, (double)h[0] / used_blocks,
-                (double)h[1] / used_blocks, (double)h[2] / used_blocks, (double)h[3] / n, gq[0],
-                gq[1]);
-    }
+    const uint32_t sgrid = 8u * ((nranges + 7u) / 8u) << (rlog - 8);
+    hipLaunchKernelGGL(k_cand_scatter, dim3(sgrid), dim3(kT), 0, st, sp, stage, npos, ws.cand,
+                       ws.klog, rlog, nranges, rfill, derr, pk);
+    SALZ_LAUNCH_CHECK();
     for (uint32_t lo = nblocks / 2; lo >= 1; lo >>= 1) {
         hipLaunchKernelGGL(k_tree_level, dim3(grid_for(lo, kT)), dim3(kT), 0, st, tsa, tlcp, lo,
                            lo);

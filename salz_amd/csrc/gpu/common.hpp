@@ -229,25 +229,14 @@ __host__ __device__ __forceinline__ uint32_t init_suffix(size_t c, const Blocks 
 // (bits > 0): every byte mapped to its rank 1..sigma in the block's alphabet (order-preserving;
 // 0 = past the end, below every symbol), k symbols of `bits` bits packed big-endian into the low
 // k * bits bits: 7-bit text gives 9 symbols in 63 bits, a binary text 32 symbols (round 0 reaches
-// depth 32), 128..255 distinct bytes 8 symbols of 8 bits. bits == 9: all 256 byte values, each
-// byte + 1 as its symbol (no table), 7 symbols in 63 bits. Symbols >= 1 are what lets round 1 be
-// keyed by the text (sa.hip): a key padded with zeros past the end never equals a longer suffix's.
+// depth 32). Symbols >= 1 are what lets round 1 be keyed by the text (sa.hip): a key padded with
+// zeros past the end never equals a longer suffix's. Blocks of more than 127 distinct bytes keep
+// raw keys.
 struct Alpha {
     uint32_t bits;  // 0: raw bytes
     uint32_t k;     // symbols per key (the depth round 0 sorts to)
     uint8_t code[256];
 };
-
-// The 9-bit symbols (byte + 1) of the 7 bytes of w (little-endian from the suffix's first byte),
-// big-endian in 63 bits, 0 past `left` bytes.
-__host__ __device__ __forceinline__ uint64_t raw9_key(uint64_t w, uint32_t left)
-{
-    uint64_t key = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 7; j++)
-        key = (key << 9) | (j < left ? ((w >> (8 * j)) & 255u) + 1u : 0u);
-    return key;
-}
 
 // Unaligned little-endian 8-byte load from an 8-byte-aligned, padded byte buffer.
 __device__ __forceinline__ uint64_t load_u64_any(const uint8_t *base, size_t pos)
@@ -276,8 +265,6 @@ __device__ __forceinline__ uint64_t round0_key(const uint8_t *T, uint32_t i, uin
             w &= (1ull << (8u * left)) - 1ull;
         return __builtin_bswap64(w);
     }
-    if (a.bits == 9)
-        return raw9_key(load_u64_any(T, i), left);
     uint64_t key = 0;
     if (a.k == 8) {  // the usual text case: one load, 8 table lookups, unrolled
         const uint64_t w = load_u64_any(T, i);
@@ -305,13 +292,10 @@ __device__ __forceinline__ uint64_t round0_key(const uint8_t *T, uint32_t i, uin
 }
 
 // The same from the text already mapped to symbols (Tm[i] = a.code[T[i]], zero padded): no
-// table lookups, just the packing (the radix passes that build round 0's keys use this). 9-bit
-// symbols: Tm is the raw text (the symbol is byte + 1).
+// table lookups, just the packing (the radix passes that build round 0's keys use this).
 __device__ __forceinline__ uint64_t round0_key_mapped(const uint8_t *Tm, uint32_t i, uint32_t e, const Alpha &a)
 {
     const uint32_t left = e - i;
-    if (a.bits == 9)
-        return raw9_key(load_u64_any(Tm, i), left);
     uint64_t key = 0;
     if (a.k == 8 || a.k == 9) {  // the usual text cases: straight-line, so the loads of a thread's items batch
         // the two aligned words holding Tm[i, i + 8): the second also holds Tm[i + 8]

@@ -466,11 +466,11 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
     const bool full = 3 * b <= 64;
     uint8_t *mark = d.top;
     uint32_t *sar = nullptr;
-    // Naming by the triples' presence bitmap (SALZ_SA=dc3sort: by sorting at every level)
-    const bool lut_off = env_flag("SALZ_SA", "dc3sort");  // (read per call: the tests switch it)
+    // Naming by the triples' presence bitmap where they fit kLutMaxBits; wider triples (and a
+    // level whose names are all distinct) sort below.
     const uint32_t nwords = 3 * b <= kLutMaxBits ? ((1u << (3 * b)) + 31u) / 32u : 0u;
     const size_t lut_room = nwords > kLutWords ? 2 * (size_t)nwords : 2 * (size_t)kLutWords;
-    if (nwords && !lut_off && ws.radix_counts_elems >= lut_room) {
+    if (nwords && ws.radix_counts_elems >= lut_room) {
         uint32_t *bits = ws.radix_counts, *pre = bits + (lut_room / 2);
         uint32_t *tkeys = reinterpret_cast<uint32_t *>(ws.keyA);  // (free until the mod-0 sort)
         SALZ_HIP(fill_async(bits, 0, sizeof(uint32_t) * nwords, st));
@@ -567,8 +567,8 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
         return -1;
     K = ws.keyA;
     V = ws.valA;
-    // (SALZ_SA=dc3sort: unpacked keys too, the merge reading every operand from TR)
-    const int packb = !lut_off && b <= 4 && n < (1u << kRankBits) && ns < (1u << kRankBits) ? b : 0;
+    // (symbols of more than 4 bits: unpacked keys, the merge reading every operand from TR)
+    const int packb = b <= 4 && n < (1u << kRankBits) && ns < (1u << kRankBits) ? b : 0;
     hipLaunchKernelGGL(k_dc3_mod0, dim3(grid_for(ns, kT)), dim3(kT), 0, st, sar, name, ns, n1, n0, tr, K, V,
                        d.derr, packb);
     SALZ_LAUNCH_CHECK();

@@ -21,14 +21,27 @@
 // The collectives (DistXchg): the caller's callbacks (salz_dist_ops: torch.distributed from
 // Python, gloo in the tests) or RCCL called from the library on its own stream
 // (salz_gpu_dist_comm: no host callback per round; librccl is opened at run time, so the library
-// links no RCCL for callers that never split a block).
+// neither links RCCL nor needs its headers to build, for callers that never split a block).
 #include "internal.hpp"
 
 #include <dlfcn.h>
-#include <rccl/rccl.h>
 
 #include <cstring>
 #include <vector>
+
+// The few RCCL declarations the split sort uses, restated from rccl/rccl.h (ROCm 7.2) so that the
+// build needs no RCCL headers: the enums are int-sized in the C ABI.
+typedef struct ncclComm *ncclComm_t;
+#define NCCL_UNIQUE_ID_BYTES 128
+typedef struct {
+    char internal[NCCL_UNIQUE_ID_BYTES];
+} ncclUniqueId;
+typedef int ncclResult_t;
+typedef int ncclDataType_t;
+typedef int ncclRedOp_t;
+constexpr ncclResult_t ncclSuccess = 0;
+constexpr ncclDataType_t ncclUint32 = 3, ncclUint64 = 5;
+constexpr ncclRedOp_t ncclSum = 0;
 
 namespace salz {
 namespace {
@@ -226,16 +239,17 @@ struct OpsXchg final : DistXchg {
 // RCCL entry points, opened at run time (the copy already loaded in the process first: torch
 // brings its own; then the ROCm one).
 struct Rccl {
-    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
-    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
-    decltype(&ncclCommDestroy) comm_destroy = nullptr;
-    decltype(&ncclGroupStart) group_start = nullptr;
-    decltype(&ncclGroupEnd) group_end = nullptr;
-    decltype(&ncclSend) send = nullptr;
-    decltype(&ncclRecv) recv = nullptr;
-    decltype(&ncclAllReduce) all_reduce = nullptr;
-    decltype(&ncclAllToAll) all_to_all = nullptr;
-    decltype(&ncclGetErrorString) error_string = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    ncclResult_t (*send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    ncclResult_t (*all_to_all)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
     bool ok = false;
 };
 
@@ -285,6 +299,20 @@ namespace {
         }                                                                                           \
     } while (0)
 
+// Where peer r's run starts in the send and receive buffers of one exchange: the runs lie in rank
+// order, as in torch.distributed's all_to_all_single with split sizes (the gloo path, dist.py),
+// which the grouped sends and receives below must reproduce (tests/test_dist.py checks both).
+void xchg_offsets(int nr, const uint64_t *sc, const uint64_t *rc, uint64_t *so, uint64_t *ro)
+{
+    uint64_t s = 0, r = 0;
+    for (int k = 0; k < nr; k++) {
+        so[k] = s;
+        ro[k] = r;
+        s += sc[k];
+        r += rc[k];
+    }
+}
+
 struct RcclXchg final : DistXchg {
     DistComm *c;
     hipStream_t st;
@@ -301,15 +329,14 @@ struct RcclXchg final : DistXchg {
         SALZ_NCCL(R.all_to_all(c->dcnt, c->dcnt + nr, 1, ncclUint64, c->comm, st));
         SALZ_HIP(hipMemcpyAsync(rc, c->dcnt + nr, (size_t)nr * 8, hipMemcpyDeviceToHost, st));
         SALZ_HIP(hipStreamSynchronize(st));
+        std::vector<uint64_t> so(nr), ro(nr);
+        xchg_offsets(nr, sc, rc, so.data(), ro.data());
         SALZ_NCCL(R.group_start());
-        size_t so = 0, ro = 0;
         for (int r = 0; r < nr; r++) {
             if (sc[r])
-                SALZ_NCCL(R.send(xsend + so, sc[r], ncclUint32, r, c->comm, st));
+                SALZ_NCCL(R.send(xsend + so[r], sc[r], ncclUint32, r, c->comm, st));
             if (rc[r])
-                SALZ_NCCL(R.recv(xrecv + ro, rc[r], ncclUint32, r, c->comm, st));
-            so += sc[r];
-            ro += rc[r];
+                SALZ_NCCL(R.recv(xrecv + ro[r], rc[r], ncclUint32, r, c->comm, st));
         }
         SALZ_NCCL(R.group_end());
         return 0;
@@ -389,6 +416,23 @@ int dist_suffix_array(Workspace &ws, uint32_t n, int nranks, int rank, DistXchg 
     if (nranks < 1 || nranks > 255 || rank < 0 || rank >= nranks) {
         set_error("split suffix sort: rank %d of %d", rank, nranks);
         return -1;
+    }
+    // A block the repetition probe sends to DC3 (long repeats everywhere: Fibonacci, periodic or
+    // run-heavy blocks) is not split. Every suffix there survives ~log2(max LCP) doubling rounds
+    // (26 on C5), each a full-width sort plus an exchange, and the split sorter has no DC3. Every
+    // rank sees the same text and takes the same decision: all return 1 and the caller encodes the
+    // block whole on one GPU (salz_gpu_encode_device, which takes DC3). Smaller blocks split as
+    // usual (prefix doubling, like the single-GPU sorter below 2^20 suffixes).
+    {
+        const int rep = block_repetitive(ws, n);
+        if (rep < 0)
+            return -1;
+        if (rep) {
+            for (int r = 0; r <= nranks; r++)
+                offsets[r] = 0;
+            *m0_out = 0;
+            return 1;
+        }
     }
     if (!ws.dist_owner) {
         // owner byte per class, then the class histogram (its own room: a workspace sized for
@@ -509,7 +553,7 @@ int dist_suffix_array(Workspace &ws, uint32_t n, int nranks, int rank, DistXchg 
     const int abits = block_alpha_bits(ws, n);
     if (abits < 0)
         return -1;
-    const bool text1 = abits > 0 && !env_flag("SALZ_SA", "rank1");
+    const bool text1 = abits > 0;
     const bool local = nranks == 1 && !env_flag("SALZ_SA", "xchg");
     const DistSa d{x, rank, nranks, ws.dist_owner, list, m0, (uint32_t)offsets[rank], n, xsend, xrecv, xcap, text1,
                    local};
@@ -582,6 +626,16 @@ salz_gpu_dist_comm *salz_gpu_dist_comm_create(int device, int nranks, int rank, 
         set_error("librccl.so.1 not found (or lacks an entry point): no in-library collectives");
         return nullptr;
     }
+    int prev = -1;  // the caller's device is restored on every return (as elsewhere in the C ABI)
+    (void)hipGetDevice(&prev);
+    struct Restore {
+        int dev;
+        ~Restore()
+        {
+            if (dev >= 0)
+                (void)hipSetDevice(dev);
+        }
+    } restore{prev};
     if (hipSetDevice(device) != hipSuccess) {
         set_error("hipSetDevice(%d) failed", device);
         return nullptr;
@@ -610,12 +664,26 @@ void salz_gpu_dist_comm_destroy(salz_gpu_dist_comm *comm)
     auto *c = reinterpret_cast<DistComm *>(comm);
     if (!c)
         return;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
     (void)hipSetDevice(c->device);
     if (c->dcnt)
         (void)hipFree(c->dcnt);
     if (c->comm)
         rccl().comm_destroy(c->comm);
     delete c;
+    if (prev >= 0)
+        (void)hipSetDevice(prev);
+}
+
+// Test hook: the per-peer run offsets of one exchange (xchg_offsets).
+int salz_debug_xchg_offsets(int nranks, const uint64_t *send_counts, const uint64_t *recv_counts, uint64_t *send_off,
+                            uint64_t *recv_off)
+{
+    if (nranks < 1 || !send_counts || !recv_counts || !send_off || !recv_off)
+        return -1;
+    salz::xchg_offsets(nranks, send_counts, recv_counts, send_off, recv_off);
+    return 0;
 }
 
 }  // extern "C"

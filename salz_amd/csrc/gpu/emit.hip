@@ -487,10 +487,9 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
     SALZ_HIP(fill_async(entry, 0xff, sizeof(uint32_t) * ((size_t)nch + 1), st));
     if (ne) {
         SALZ_HIP(fill_async(emark, 0, sizeof(uint32_t) * ne, st));
-        // one block with its levels stored: the path in one launch (SALZ_PARSE=marksteps: a launch
-        // per level)
-        const bool steps = env_flag("SALZ_PARSE", "marksteps");
-        const bool one = nb == 1 && ps.snaps && ps.levels > 0 && !steps;
+        // one block with its levels stored: the path in one launch (round 5: C2 emission 1.07 ->
+        // 1.01 ms); batches, and a parse that kept level 0 only, a launch per level
+        const bool one = nb == 1 && ps.snaps && ps.levels > 0;
         if (one) {
             // (a path takes at most one exit per chunk: nch + 1 nodes with the root)
             constexpr uint32_t kPathThreads = 32768;
@@ -500,25 +499,25 @@ int stage_emit(Workspace &ws, const Blocks &bl, uint32_t N_last, uint8_t *dst, s
                                ws.klog, ps.jt0, ne, ps.levels, L, kPathThreads, emark);
             SALZ_LAUNCH_CHECK();
         } else {
-        hipLaunchKernelGGL(k_mark_start, dim3(grid_for(nb, kT)), dim3(kT), 0, st, ps.ebits, ps.pst, ws.klog,
-                           emark, bl);
-        SALZ_LAUNCH_CHECK();
-        const uint32_t *lev = ps.jt0;  // parents 2^k steps up (level k)
-        uint32_t *pp[2] = {ws.u2, ws.u3};  // recomputed levels when the parse kept only level 0
-        for (uint32_t k = 0; k < ps.levels; k++) {
-            if (k > 0) {
-                if (ps.snaps) {
-                    lev = ps.jt0 + (size_t)k * ne;
-                } else {
-                    hipLaunchKernelGGL(k_jt_double, dim3(grid_for(ne, kT)), dim3(kT), 0, st, lev,
-                                       pp[k & 1], ne);
-                    SALZ_LAUNCH_CHECK();
-                    lev = pp[k & 1];
-                }
-            }
-            hipLaunchKernelGGL(k_mark_step, dim3(grid_for(ne, kT)), dim3(kT), 0, st, lev, emark, ne);
+            hipLaunchKernelGGL(k_mark_start, dim3(grid_for(nb, kT)), dim3(kT), 0, st, ps.ebits, ps.pst, ws.klog,
+                               emark, bl);
             SALZ_LAUNCH_CHECK();
-        }
+            const uint32_t *lev = ps.jt0;  // parents 2^k steps up (level k)
+            uint32_t *pp[2] = {ws.u2, ws.u3};  // recomputed levels when the parse kept only level 0
+            for (uint32_t k = 0; k < ps.levels; k++) {
+                if (k > 0) {
+                    if (ps.snaps) {
+                        lev = ps.jt0 + (size_t)k * ne;
+                    } else {
+                        hipLaunchKernelGGL(k_jt_double, dim3(grid_for(ne, kT)), dim3(kT), 0, st, lev,
+                                           pp[k & 1], ne);
+                        SALZ_LAUNCH_CHECK();
+                        lev = pp[k & 1];
+                    }
+                }
+                hipLaunchKernelGGL(k_mark_step, dim3(grid_for(ne, kT)), dim3(kT), 0, st, lev, emark, ne);
+                SALZ_LAUNCH_CHECK();
+            }
         }
         hipLaunchKernelGGL(k_entries, dim3(grid_for(ne, kT)), dim3(kT), 0, st, emark, ps.elist, ne,
                            n, ps.chunk, entry);

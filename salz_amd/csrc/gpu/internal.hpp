@@ -225,6 +225,9 @@ int dist_suffix_array_comm(Workspace &ws, uint32_t n, DistComm *c, uint32_t *xse
 int dist_idle_rounds(Workspace &ws, const DistSa &d, int round);
 // The round-0 alphabet's symbol width (0: raw bytes), as stage_suffix_array computes it (sa.hip).
 int block_alpha_bits(Workspace &ws, uint32_t n);
+// 1 when the repetition probe (sa.hip) would send this single block of n suffixes to DC3 (blocks
+// of at least 2^20 suffixes), 0 otherwise, -1 on failure.
+int block_repetitive(Workspace &ws, uint32_t n);
 int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist = nullptr);  // sa.hip -> ws.sa
 // dc3.hip -> ws.sa for one block (repetitive inputs); symbols = codes.code[byte] (1..sigma) or
 // byte + 1 when raw

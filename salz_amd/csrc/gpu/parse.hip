@@ -427,119 +427,42 @@ struct MarkSplit {
     uint32_t *d0s;           // per chunk: the shift at its end
 };
 
-template <class C>
-__global__ __launch_bounds__(kT) void k_parse_mark(const typename C::T *__restrict__ cand,
-                                                   const uint32_t *__restrict__ cnew,
-                                                   const uint32_t *__restrict__ cold, uint32_t n,
-                                                   Blocks bl,
-                                                   uint32_t klog, uint8_t *__restrict__ wdirty,
-                                                   uint32_t *__restrict__ dsum,
-                                                   uint32_t *__restrict__ ndirty,
-                                                   const uint32_t *__restrict__ reach,
-                                                   const uint32_t *__restrict__ pbrk,
-                                                   const uint32_t *__restrict__ rlo, LazyTest lt,
-                                                   MarkSplit ms)
+// The range test of every chunk before a skipping pass: a chunk whose targets [b, reach] hold
+// no break of the shift passes; the others (and no chunk whose end cost reaches 2^30) are listed
+// for k_mark_rows, and k_mark_final sets the wave flags.
+__global__ __launch_bounds__(kT) void k_parse_mark(const uint32_t *__restrict__ cnew,
+                                                   const uint32_t *__restrict__ cold, uint32_t n, Blocks bl,
+                                                   uint32_t klog, const uint32_t *__restrict__ reach,
+                                                   const uint32_t *__restrict__ pbrk, LazyTest lt, MarkSplit ms)
 {
     const uint32_t c = blockIdx.x * kT + threadIdx.x;
     const uint64_t a64 = (uint64_t)c << klog;
-    if ((a64 & ~(((uint64_t)64 << klog) - 1)) >= n)
-        return;  // whole wave past the end
-    bool bad = false;
-    uint32_t d0 = 0;
-    if (a64 < n) {
-        const uint32_t a = (uint32_t)a64, K = 1u << klog;
-        // (a block's last chunk ends at its suffix text's end: a cost-0 end, never shifted)
-        const uint32_t e = bl.end(a), b0 = bl.start(a);
-        const uint32_t b = (e - a) < K ? e : a + K;
-        const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
-        uint32_t nb;
-        d0 = shift_of(lt, cnew, cold, klog, b, nb);
-        bad = nb >= (1u << 30);
-        bool range_ok = false;
-        if (reach) {  // breaks in (b, r] lie in chunks c + 1 .. (r - 1) >> klog
-            const uint32_t r = reach[c];  // loads unconditional (an empty range compares c + 1 twice)
-            const uint32_t hi = r > b ? ((r - 1) >> klog) + 1 : c + 1;
-            range_ok = pbrk[hi] == pbrk[c + 1];
-        }
-        if (ms.list) {  // split test: list the chunk for k_mark_rows, decide in k_mark_final
-            const bool need = !range_ok && !bad;
-            const uint64_t mk = wave_ballot(need);
-            if (mk) {
-                const int leader = (int)__ffsll((unsigned long long)mk) - 1;
-                uint32_t at = 0;
-                if ((int)lane_id() == leader)
-                    at = atomicAdd(ms.count, (uint32_t)__popcll(mk));
-                at = shfl_u32(at, leader);
-                if (need)
-                    ms.list[at + count_below(mk)] = c;
-            }
-            ms.cbad[c] = bad ? 1u : 0u;
-            ms.d0s[c] = d0;
-            return;
-        }
-        const uint32_t jn = range_ok ? 0u : b - a;
-        // Only rows from the chunk's first factor reaching past b (rlo, from the first pass) have
-        // targets to test; the wave starts at its lowest such row.
-        const uint32_t jl = rlo ? rlo[c] - a : 0u;
-        uint32_t wm = jn ? jl : K;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) {
-            const uint32_t o = shfl_xor_u32(wm, m);
-            wm = o < wm ? o : wm;
-        }
-        const uint32_t jstart = wm & ~15u;
-        // rows tested: up to K when some chunk of the wave needs the full test, else none (uniform)
-        const uint32_t rows = wave_ballot(jn != 0) != 0 ? K : 0u;
-        // K rows for every lane (rows past jn test b itself, which always passes), in batches
-        // of 8: a batch's candidates are loaded while the previous batch's costs are checked
-        // (two register sets, so no in-flight register is moved), and the loop count is
-        // wave-uniform.
-        using CT = typename C::T;
-        auto load = [&](CT(&cd)[8], uint32_t j0) {
-#pragma unroll
-            for (uint32_t u = 0; u < 8; u++) {
-                const uint32_t j = j0 + u < jn ? j0 + u : (jn ? jn - 1u : 0u);
-                cd[u] = cand[base + ((size_t)j << 6)];
-            }
-        };
-        // a target equal to the previous row's (one match's end) was checked already: such a row
-        // reads b's costs instead (which pass by definition)
-        uint32_t lqp = 0xffffffffu, lqn = 0xffffffffu;
-        auto check = [&](const CT(&cd)[8], uint32_t j0) {
-#pragma unroll
-            for (uint32_t u = 0; u < 8; u++) {
-                const uint32_t p = a + j0 + u;
-                const bool on = j0 + u >= jl && j0 + u < jn && p != b0;
-                const uint32_t lp = C::lp(cd[u]), ln = C::ln(cd[u]);
-                const uint32_t qp = p + lp, qn = p + ln;
-                const bool xp = on && lp >= 3u && qp >= b && qp != lqp;
-                const bool xn = on && ln >= 3u && qn >= b && qn != lqn;
-                lqp = on && lp >= 3u ? qp : 0xffffffffu;
-                lqn = on && ln >= 3u ? qn : 0xffffffffu;
-                uint32_t vp, vn;
-                const uint32_t dp = shift_of(lt, cnew, cold, klog, xp ? qp : b, vp);
-                const uint32_t dn = shift_of(lt, cnew, cold, klog, xn ? qn : b, vn);
-                bad |= dp != d0 || vp >= (1u << 30);
-                bad |= dn != d0 || vn >= (1u << 30);
-            }
-        };
-        CT A[8], B[8];
-        load(A, jstart);
-        for (uint32_t j0 = jstart; j0 < rows; j0 += 16) {
-            load(B, j0 + 8);
-            check(A, j0);
-            load(A, j0 + 16);
-            check(B, j0 + 8);
-        }
+    if (a64 >= n)
+        return;
+    const uint32_t a = (uint32_t)a64, K = 1u << klog;
+    // (a block's last chunk ends at its suffix text's end: a cost-0 end, never shifted)
+    const uint32_t e = bl.end(a);
+    const uint32_t b = (e - a) < K ? e : a + K;
+    uint32_t nb;
+    const uint32_t d0 = shift_of(lt, cnew, cold, klog, b, nb);
+    const bool bad = nb >= (1u << 30);
+    // breaks in (b, r] lie in chunks c + 1 .. (r - 1) >> klog (loads unconditional: an empty
+    // range compares c + 1 twice)
+    const uint32_t r = reach[c];
+    const uint32_t hi = r > b ? ((r - 1) >> klog) + 1 : c + 1;
+    const bool need = pbrk[hi] != pbrk[c + 1] && !bad;
+    const uint64_t mk = wave_ballot(need);
+    if (mk) {
+        const int leader = (int)__ffsll((unsigned long long)mk) - 1;
+        uint32_t at = 0;
+        if ((int)lane_id() == leader)
+            at = atomicAdd(ms.count, (uint32_t)__popcll(mk));
+        at = shfl_u32(at, leader);
+        if (need)
+            ms.list[at + count_below(mk)] = c;
     }
-    const uint64_t m = wave_ballot(bad);
-    if (lane_id() == 0) {
-        wdirty[c >> 6] = m ? 1u : 0u;
-        if (m)
-            atomicAdd(ndirty, 1u);
-    }
-    if (!m && a64 < n)
-        dsum[c] += d0;
+    ms.cbad[c] = bad ? 1u : 0u;
+    ms.d0s[c] = d0;
 }
 
 // Listed chunks' per-candidate tests (grid-stride over the list): a wave takes G = 512 / K chunks
@@ -566,7 +489,7 @@ __global__ __launch_bounds__(kT) void k_mark_rows(const typename C::T *__restric
         const uint32_t b = (e - a) < K ? e : a + K;
         const size_t base = ((size_t)(c >> 6) << (klog + 6)) | (c & 63u);
         const uint32_t d0 = ms.d0s[c];
-        const uint32_t jl = rlo ? rlo[c] - a : 0u, jn = b - a;
+        const uint32_t jl = rlo[c] - a, jn = b - a;
         typename C::T cd[8];
 #pragma unroll
         for (uint32_t u = 0; u < 8; u++) {
@@ -1088,35 +1011,30 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     uint32_t *dsum = reinterpret_cast<uint32_t *>(ws.lsc);
     uint8_t *wdirty = reinterpret_cast<uint8_t *>(dsum + ps.nchunks);
     SALZ_HIP(fill_async(dsum, 0, sizeof(uint32_t) * ps.nchunks, st));
-    // Range test of k_parse_mark (SALZ_PARSE=norange: per-candidate test only): each chunk's
-    // farthest target, and per test the shift breaks per chunk and their prefix counts.
-    const bool range_on = !env_flag("SALZ_PARSE", "norange");
+    // Range test of k_parse_mark: each chunk's farthest target, and per test the shift breaks per
+    // chunk and their prefix counts.
     uint32_t *reach = dsum + 2 * ((size_t)ps.nchunks + 64);
     uint32_t *brk = reach + ps.nchunks + 64, *pbrk = brk + ps.nchunks + 64;
-    // Packed candidates from the second pass on (g64 is free during the parse; SALZ_PARSE=nopack:
-    // the full ones every pass)
-    const bool pack = n < kPackLen && !env_flag("SALZ_PARSE", "nopack");
+    // Packed candidates from the second pass on (g64 is free during the parse)
+    const bool pack = n < kPackLen;
     uint2 *cand8 = pack ? reinterpret_cast<uint2 *>(ws.g64) : nullptr;
-    // Lazy costs from the first skipping pass on (SALZ_PARSE=nolazy: every pass rewrites every
-    // cost): per-chunk offsets (two generations), deltas, uniform / changed flags, exit summaries,
-    // and the pre-pass cost of every exit node.
-    const bool lazy_on = skip_on && !env_flag("SALZ_PARSE", "nolazy");
+    // Lazy costs from the first skipping pass on: per-chunk offsets (two generations), deltas,
+    // uniform / changed flags, exit summaries, and the pre-pass cost of every exit node.
+    const bool lazy_on = skip_on;
     const size_t nc64 = (size_t)ps.nchunks + 64;
     uint32_t *Lv[2] = {pbrk + nc64, pbrk + 2 * nc64};
     uint32_t *dl = pbrk + 3 * nc64;
     uint8_t *uni = reinterpret_cast<uint8_t *>(pbrk + 4 * nc64), *chg = uni + nc64;
     uint32_t *summ = pbrk + 5 * nc64;
     uint32_t *rlo = pbrk + (5 + kSummW) * nc64;  // per chunk: first row reaching past its end
-    // split test (k_mark_rows; SALZ_PARSE=nosplit: the per-candidate test inside k_parse_mark)
-    const bool split_on = range_on && !env_flag("SALZ_PARSE", "nosplit");
+    // split test: the chunks the range test does not pass get a wave each (k_mark_rows)
     uint32_t *ms_count = reinterpret_cast<uint32_t *>(ws.dscal) + 51;
-    const MarkSplit ms{split_on ? pbrk + (6 + kSummW) * nc64 : nullptr, ms_count,
+    const MarkSplit ms{pbrk + (6 + kSummW) * nc64, ms_count,
                        reinterpret_cast<uint8_t *>(pbrk + (8 + kSummW) * nc64), pbrk + (7 + kSummW) * nc64};
     uint32_t *ce = pbrk + (9 + kSummW) * nc64;
-    // per 64-chunk tile: exit flags set by this pass's walk (skipping passes; SALZ_PARSE=notouch:
-    // every pass packs every tile)
+    // per 64-chunk tile: exit flags set by this pass's walk (skipping passes)
     const size_t ntiles = S / tile;
-    uint8_t *ttouch = env_flag("SALZ_PARSE", "notouch") ? nullptr : reinterpret_cast<uint8_t *>(ce + ws.cap_n + 2);
+    uint8_t *ttouch = reinterpret_cast<uint8_t *>(ce + ws.cap_n + 2);
     if ((size_t)(ce - reinterpret_cast<uint32_t *>(ws.lsc)) + ws.cap_n + 2 + ntiles / 4 + 1 >
         4 * (ws.cap_s > ws.cap_n + 2 ? ws.cap_s : ws.cap_n + 2)) {
         set_error("parse: lazy-cost scratch does not fit");
@@ -1124,9 +1042,6 @@ int stage_parse(Workspace &ws, const Blocks &bl)
     }
     bool lazy = false;
     int lc = 0;
-    // exit compaction per node where E is sparse (SALZ_PARSE=nodes=0: per 8 slots always, 2: per
-    // node always)
-    const int node_compact = (int)env_num("SALZ_PARSE", "nodes", 1);
     uint32_t prev_listed = ps.nchunks;  // chunks the last split test listed (sizes k_mark_rows' grid)
     uint32_t *lzC = nullptr, *lzD = nullptr;
     ps.lzC = nullptr;
@@ -1172,13 +1087,13 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         const bool entering = lazy_on && skipping && !lazy;
         if (skipping) {
             LazyTest lt{lazy ? Lv[lc] : nullptr, uni, dl, lzD};
-            if (lazy && range_on) {
+            if (lazy) {
                 hipLaunchKernelGGL(k_lazy_breaks, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, uni, dl, ps.nchunks,
                                    brk);
                 SALZ_LAUNCH_CHECK();
                 if (scan_sum_u32(brk, pbrk, (size_t)ps.nchunks + 1, false, nullptr, ws, st) != 0)
                     return -1;
-            } else if (range_on) {
+            } else {
                 SALZ_HIP(fill_async(brk, 0, sizeof(uint32_t) * ((size_t)ps.nchunks + 1), st));
                 const size_t bthreads = (size_t)((ps.nchunks + 63) / 64) * 64 * (ps.chunk / kRowsBrk);
                 hipLaunchKernelGGL(k_shift_breaks, dim3(grid_for(bthreads, kT)), dim3(kT), 0, st, cin, cout, n, klog,
@@ -1187,16 +1102,10 @@ int stage_parse(Workspace &ws, const Blocks &bl)
                 if (scan_sum_u32(brk, pbrk, (size_t)ps.nchunks + 1, false, nullptr, ws, st) != 0)
                     return -1;
             }
-            if (pack)
-                hipLaunchKernelGGL(k_parse_mark<CandPacked>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st,
-                                   cand8, cin, cout, n, bl, klog, wdirty, dsum, ndirty, range_on ? reach : nullptr,
-                                   pbrk, range_on ? rlo : nullptr, lt, ms);
-            else
-                hipLaunchKernelGGL(k_parse_mark<CandFull>, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st,
-                                   ws.cand, cin, cout, n, bl, klog, wdirty, dsum, ndirty,
-                                   range_on ? reach : nullptr, pbrk, range_on ? rlo : nullptr, lt, ms);
+            hipLaunchKernelGGL(k_parse_mark, dim3(grid_for(ps.nchunks, kT)), dim3(kT), 0, st, cin, cout, n, bl, klog,
+                               reach, pbrk, lt, ms);
             SALZ_LAUNCH_CHECK();
-            if (split_on) {  // listed chunks: a wave each (2048 waves, grid-stride), then the wave flags
+            {  // listed chunks: a wave each (2048 waves, grid-stride), then the wave flags
                 // waves: the previous test's list length (lists shrink from pass to pass; any count is
                 // served by the grid-stride loop), 64 to 16384; the first test lists up to every chunk
                 const uint32_t per = klog >= 9 ? 1u : 512u >> klog;  // chunks per wave
@@ -1232,16 +1141,16 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         const uint32_t tgen = (uint32_t)(it % 255) + 1u;
         if (ttouch && tgen == 1u)
             SALZ_HIP(fill_async(ttouch, 0, ntiles, st));
-        uint32_t *rch = it == 0 && range_on ? reach : nullptr;
+        uint32_t *rch = it == 0 ? reach : nullptr;
         const Lazy lzw{lazy ? Lv[lc] : nullptr, lazy_on ? summ : nullptr, lazy_on ? chg : nullptr};
         // Chunks of K <= 128 (non-text and mid-size blocks) prefetch far targets 1 step and
         // candidates 3 steps ahead instead of 4 and 7: mixed 100 MB parse 8.22 -> 7.9 ms, Silesia
         // blocks 3.1 -> 2.9 ms (profiles/r04zi_parse_near_prefetch_ab.txt); text at K = 512 is
         // 0.03 ms slower so
         // From the fourth pass on, where few waves walk and a pass is one lane's latency chain,
-        // the 4 / 7 distances again (SALZ_PARSE=farlate=N: from pass N; mixed 100 MB parse 7.88 ->
-        // 7.77 ms at 3, 7.79 at 5, Silesia-sized blocks even to +1%: r05fl_parse_farlate_ab.txt)
-        const long far_late = env_num("SALZ_PARSE", "farlate", 3);
+        // the 4 / 7 distances again (from the fourth pass: mixed 100 MB parse 7.88 -> 7.77 ms, 7.79
+        // from the sixth, Silesia-sized blocks even to +1%: r05fl_parse_farlate_ab.txt)
+        constexpr int far_late = 3;
         const bool near = klog <= 7 && it < far_late;
         if (pack && it > 0)
             hipLaunchKernelGGL((near ? k_parse_chunk<CandPacked, 1, 3> : k_parse_chunk<CandPacked, 4, 7>),
@@ -1304,7 +1213,7 @@ int stage_parse(Workspace &ws, const Blocks &bl)
             set_error("parse: exit set larger than the text (|E|=%u)", ne);
             return -1;
         }
-        if (node_compact == 2 || (node_compact == 1 && (uint64_t)ne * 64 < S)) {  // sparse E: a thread per node
+        if ((uint64_t)ne * 64 < S) {  // sparse E: a thread per node
             const size_t nw = S / 64;
             uint32_t *nword = ws.lcps;  // (the LCP array: read by the candidates stage only)
             hipLaunchKernelGGL(k_node_words, dim3(grid_for(nw, kT)), dim3(kT), 0, st, eb, nw, nword);
@@ -1319,10 +1228,8 @@ int stage_parse(Workspace &ws, const Blocks &bl)
         SALZ_LAUNCH_CHECK();
         int jc = 0;
         if (snaps) {
-            // (SALZ_PARSE=jump2: two levels per launch everywhere)
-            const bool jump2_only = env_flag("SALZ_PARSE", "jump2");
             for (uint32_t k = 0; k < K;) {
-                if (!jump2_only && k + 3 <= K && (size_t)(k + 4) * ne <= snap_cap) {
+                if (k + 3 <= K && (size_t)(k + 4) * ne <= snap_cap) {
                     hipLaunchKernelGGL(k_jump3, dim3(grid_for(ne, kT)), dim3(kT), 0, st, snap + (size_t)k * ne, js[jc],
                                        snap + (size_t)(k + 1) * ne, snap + (size_t)(k + 2) * ne,
                                        snap + (size_t)(k + 3) * ne, js[jc ^ 1], ne);

@@ -980,8 +980,13 @@ static int dist_piece(salz_gpu_ctx *ctx, const uint8_t *d_text, size_t N, uint32
     SALZ_HIP(fill_async(ws.text + N, 0, 128, st));
     const uint32_t n = (uint32_t)(N - 8);
     uint32_t m0 = 0;
-    if (sort(ws, n, &m0) != 0)
+    const int rc = sort(ws, n, &m0);
+    if (rc < 0)
         return -1;
+    if (rc == 1) {  // not split (a repetitive block): the caller encodes it whole
+        *lcp_ok = 0;
+        return 1;
+    }
     if (m0) {
         SALZ_HIP(hipMemcpyAsync(d_sa_piece, ws.sa, (size_t)m0 * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
         if (ws.lcps_ok)
@@ -1285,6 +1290,9 @@ static salz_gpu_ctx *pool_try_acquire(int cur, size_t need, bool *create_failed,
 // release the largest. Busy contexts neither count nor get released: their callers trim after
 // their own calls. (Counting them let two concurrent 256 MiB callers, ~30 GB each against the
 // 32 GiB default, free their own workspace after every call and reallocate it on the next.)
+// The usual case, every workspace of the device together under the cap, takes no lock at all;
+// otherwise each context is locked only while its bytes are read or while it is released, so
+// another thread's pool_try_acquire never finds the whole pool locked by a trim.
 static void pool_trim(int dev, salz_gpu_ctx *mine)
 {
     const size_t cap = pool_cap_bytes();
@@ -1295,29 +1303,36 @@ static void pool_trim(int dev, salz_gpu_ctx *mine)
             return;
         snap.assign(g_default.begin() + (size_t)dev * kMaxSlots, g_default.begin() + (size_t)(dev + 1) * kMaxSlots);
     }
-    std::vector<salz_gpu_ctx *> idle;  // locked here (all but `mine`)
+    size_t all = 0;  // busy ones included: an upper bound of the idle total
     for (salz_gpu_ctx *c : snap)
-        if (c && c != kCreating && (c == mine || c->mu.try_lock()))
-            idle.push_back(c);
-    for (;;) {
+        if (c && c != kCreating)
+            all += c->held.load();
+    if (all <= cap)
+        return;
+    for (int round = 0; round < 2 * kMaxSlots; round++) {  // (each round releases one workspace)
         size_t total = 0, big = 0;
         salz_gpu_ctx *victim = nullptr;
-        for (salz_gpu_ctx *c : idle) {
+        for (salz_gpu_ctx *c : snap) {
+            if (!c || c == kCreating || (c != mine && !c->mu.try_lock()))
+                continue;  // busy: not counted
             const size_t b = c->held.load();
             total += b;
             if (b > big) {
                 big = b;
                 victim = c;
             }
+            if (c != mine)
+                c->mu.unlock();
         }
         if (total <= cap || !victim)
             break;
+        if (victim != mine && !victim->mu.try_lock())
+            continue;  // taken meanwhile: the next round counts without it
         workspace_release(victim->ws);
         victim->held.store(0);
+        if (victim != mine)
+            victim->mu.unlock();
     }
-    for (salz_gpu_ctx *c : idle)
-        if (c != mine)
-            c->mu.unlock();
 }
 
 // Restores the calling thread's current HIP device (the pool may create or run a context on

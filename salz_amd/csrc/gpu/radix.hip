@@ -56,8 +56,6 @@ __device__ __forceinline__ uint64_t init_key(const TextSrc &t, uint32_t i, const
 // bytes, or 8 / 9 symbols of a mapped text).
 __device__ __forceinline__ uint64_t window_key(uint64_t w, uint32_t w9, uint32_t left, const Alpha &a)
 {
-    if (a.bits == 9)  // 7 raw bytes as symbols byte + 1
-        return raw9_key(w, left);
     if (left < 8)
         w &= (1ull << (8u * left)) - 1ull;
     uint64_t x = __builtin_bswap64(w);
@@ -118,15 +116,13 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
                 atomicAdd(&mine[digit_of(kMode, 0, vals[base + i], shift, txt)], 1u);
         }
     } else if (kMode == 1 && shift == 0 &&
-               (txt.a.bits == 0 || txt.a.bits == 9 || ((txt.a.k == 8 || txt.a.k == 9) && txt.a.bits >= 4))) {
+               (txt.a.bits == 0 || ((txt.a.k == 8 || txt.a.k == 9) && txt.a.bits >= 4))) {
         // Round 0's first digit is its key's low 8 or 9 bits: the 8th byte (raw keys; 9-bit digits
         // add the 7th byte's low bit), or the last symbol with the low bits of the one before (8
         // or 9 symbols of >= 4 bits): two byte loads per suffix instead of the whole key. Loads
         // unconditional (the text is padded), past the suffix's end masked to 0 like the key's bytes.
-        // (9-bit symbols: the last symbol is the 7th byte + 1, and the one before lies past 9 bits)
         const uint32_t b = txt.a.bits ? txt.a.bits : 8u, kl = txt.a.bits ? txt.a.k - 1u : 7u;
-        const bool prev = txt.a.bits ? txt.a.bits < 9 : DB > 8;  // (the digit takes bits of the byte before)
-        const uint32_t inc = txt.a.bits == 9 ? 1u : 0u;
+        const bool prev = txt.a.bits ? true : DB > 8;  // (the digit takes bits of the byte before)
         uint32_t d[kItems];
         if (txt.g.nb == 1 && base >= 7 && left >= (size_t)kTile) {  // (tile-uniform)
             // One block, a whole tile past the short suffixes: entry c is suffix c - 7, so a
@@ -143,7 +139,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
 #pragma unroll
             for (int j = 0; j < kItems; j++) {
                 const uint32_t i = i0 + (uint32_t)j;
-                const uint32_t s7 = i + kl < e ? byte_at((uint32_t)j + 1u) + inc : 0u;
+                const uint32_t s7 = i + kl < e ? byte_at((uint32_t)j + 1u) : 0u;
                 const uint32_t s6 = prev && i + kl - 1u < e ? byte_at((uint32_t)j) : 0u;
                 d[j] = (s7 | (s6 << b)) & kMask;
             }
@@ -156,7 +152,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
             const size_t idx = (size_t)j * kThreads + tid;
             const uint32_t i = init_suffix(idx < left ? base + idx : 0, txt.g), e = txt.g.end(i);
             const uint32_t t7 = txt.T[(size_t)i + kl], t6 = txt.T[(size_t)i + kl - 1u];
-            const uint32_t s7 = i + kl < e ? t7 + inc : 0u, s6 = prev && i + kl - 1u < e ? t6 : 0u;
+            const uint32_t s7 = i + kl < e ? t7 : 0u, s6 = prev && i + kl - 1u < e ? t6 : 0u;
             d[j] = (s7 | (s6 << b)) & kMask;
         }
 #pragma unroll
@@ -664,14 +660,15 @@ __global__ __launch_bounds__(TH) void k_radix_scatter(
 
 }  // namespace
 
-// Digit widths of a sort over `bits` key bits: 8-bit digits, or with SALZ_SA=d9 9-bit digits
-// wherever they save a pass (63-bit text keys: 7 passes instead of 8), the 9-bit ones first.
+// Digit widths of a sort over `bits` key bits: 8-bit digits, or where the caller prefers them
+// 9-bit digits wherever they save a pass (63-bit text keys: 7 passes instead of 8), the 9-bit
+// ones first.
 // Measured on one box (round 5, tools/ab_env.sh): a 9-bit pass costs 575 us + 120 us of
 // histogram + 30 us of row scan on C2 against 515 + 84 + 17 for an 8-bit one, so the pass it
 // saves is spent again: C2 SA 19.79 (8-bit) vs 19.95 ms, mixed 100 MB 24.82 vs 24.72 ms.
 static int digit_plan(int bits, bool allow9, bool prefer9, int *width)
 {
-    const bool nine = env_flag("SALZ_SA", "d9") || (prefer9 && !env_flag("SALZ_SA", "d8"));
+    const bool nine = prefer9;
     const int p8 = (bits + 7) / 8, p9 = (bits + 8) / 9;
     if (!allow9 || !nine || p9 >= p8) {
         for (int p = 0; p < p8; p++)
@@ -720,7 +717,7 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     const int blk_bits = blocks && g.nb > 1 ? bit_width(g.nb - 1u) : 0;
     // one block with raw-byte or 8/9-symbol keys: the text pass builds keys from an LDS window
     const bool text_win = g.nb == 1 && g.npos >= 7 &&
-                          (!alpha || alpha->bits == 0 || alpha->bits == 9 || alpha->k == 8 || alpha->k == 9);
+                          (!alpha || alpha->bits == 0 || alpha->k == 8 || alpha->k == 9);
     // 9-bit digits: key passes of 512 threads only (the generic text pass of a batch and the
     // materialised round-0 list's byte digits keep 8 bits)
     int width[64];
@@ -986,8 +983,9 @@ __global__ void k_selftest_check(const uint64_t *k, const uint32_t *v, uint32_t 
 }  // namespace
 }  // namespace salz
 
+// nine: 9-bit digits wherever they save a pass (the rank rounds' plan), else 8-bit digits
 extern "C" long salz_debug_radix_selftest(int device, uint32_t m, int bits, int iters,
-                                          uint64_t seed)
+                                          uint64_t seed, int nine)
 {
     using namespace salz;
     Workspace ws;
@@ -1003,7 +1001,8 @@ extern "C" long salz_debug_radix_selftest(int device, uint32_t m, int bits, int 
                            ws.keyA, ws.valA, m, seed + it, bits, dsum);
         uint64_t *K = ws.keyA;
         uint32_t *V = ws.valA;
-        if (radix_sort_pairs(&K, &V, ws.keyB, ws.valB, m, 0, bits, ws, ws.stream) != 0) {
+        if (radix_sort_pairs(&K, &V, ws.keyB, ws.valB, m, 0, bits, ws, ws.stream, nullptr, nullptr, nullptr,
+                             nullptr, false, nine != 0) != 0) {
             failures++;
             break;
         }

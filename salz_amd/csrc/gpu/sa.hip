@@ -1386,9 +1386,46 @@ __global__ void k_putback_text(const uint64_t *__restrict__ KS, const uint32_t *
 
 }  // namespace
 
+// The repetition probe's three launches (k_repeat_probe, k_repeat_scan, k_repeat_count) over the
+// block's n suffixes (n >= 64): results in the u32 words 248 (samples sharing a fingerprint) and
+// 249 (repeated points) of dscal, read back by the caller; scratch in u1.
+static void launch_repeat_probe(Workspace &ws, uint32_t n)
+{
+    hipStream_t st = ws.stream;
+    uint32_t *words = reinterpret_cast<uint32_t *>(ws.dscal) + 240;
+    uint32_t *ptab = ws.u1, *pmul = ws.u1 + kProbeSlots, *gcnt = ws.u1 + 2 * kProbeSlots;
+    uint32_t *pfilt = ws.u1 + 3 * kProbeSlots, *pslot = pfilt + kFilterBits / 32;
+    hipLaunchKernelGGL(k_repeat_probe, dim3(1), dim3(kProbeThreads), 0, st, ws.text, n, words + 8, ptab, pmul, gcnt,
+                       pfilt, pslot);
+    const uint32_t groups = (n - 32u) / 64u + 1u;  // 8 aligned grams per thread
+    const uint32_t grid = grid_for(groups, kScanThreads) < 1024 ? grid_for(groups, kScanThreads) : 1024;
+    hipLaunchKernelGGL(k_repeat_scan, dim3(grid), dim3(kScanThreads), 0, st, ws.text, n, words + 8, ptab, pfilt,
+                       gcnt);
+    hipLaunchKernelGGL(k_repeat_count, dim3(1), dim3(kProbePoints), 0, st, words + 8, pmul, gcnt, pslot, words + 9);
+}
+
+// The probe's verdict from the words read back (hs: ws.hscal as u32): half the samples repeated
+// among themselves (long repeats everywhere), or three quarters of them anywhere in the block
+// (what the depth-32 switch of the doubling rounds tests).
+static bool probe_repetitive(const uint32_t *hs)
+{
+    return hs[248] * 2 >= kProbe || (uint64_t)hs[249] * 4 >= 3ull * kProbePoints;
+}
+
+int block_repetitive(Workspace &ws, uint32_t n)
+{
+    if (n < (1u << 20))  // (the size from which single blocks take DC3, stage_suffix_array)
+        return 0;
+    launch_repeat_probe(ws, n);
+    SALZ_LAUNCH_CHECK();
+    if (read_scalars(ws, 960, 48, "sa.probe") != 0)
+        return -1;
+    return probe_repetitive(reinterpret_cast<const uint32_t *>(ws.hscal)) ? 1 : 0;
+}
+
 int block_alpha_bits(Workspace &ws, uint32_t n)
 {
-    if (env_flag("SALZ_SA", "noalpha") || n < 64)
+    if (n < 64)
         return 0;
     hipStream_t st = ws.stream;
     uint32_t *words = reinterpret_cast<uint32_t *>(ws.dscal) + 240;
@@ -1434,14 +1471,13 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     GroupTab tab{reinterpret_cast<uint64_t *>(cb + 4 * ws.cap_s), ws.lrec, ws.lg2g};
     uint64_t *KC = ws.pst;
 
-    // Test switches (SALZ_SA, a comma-separated list): plcp, noalpha, dc3, doubling,
-    // noprobe, global, segmented, tiny=N, rank1; SALZ_CHECK=rounds,sa and SALZ_DEBUG=sa.
+    // Test switches (SALZ_SA, a comma-separated list): plcp, dc3, doubling, global, segmented;
+    // SALZ_CHECK=rounds,sa and SALZ_DEBUG=sa.
     static const bool dbg_rounds = env_flag("SALZ_CHECK", "rounds");
     ws.lcps_ok = !env_flag("SALZ_SA", "plcp");  // plcp: the LCP from the Phi/PLCP stage instead
     // Round 0's alphabet: texts of at most 127 distinct bytes get compacted keys (Alpha,
-    // common.hpp); SALZ_SA=noalpha keeps raw 8-byte keys (tests run both).
+    // common.hpp); others keep raw 8-byte keys.
     Alpha alpha{};
-    const bool alpha_on = !env_flag("SALZ_SA", "noalpha");
     // DC3 (dc3.hip) instead of doubling for repetitive single blocks: SALZ_SA=dc3 forces it,
     // =doubling never. By default a block of >= 1 MiB starts with DC3 when the repetition probe
     // finds half of its sampled 32-grams repeated, and otherwise switches once the sort has reached depth 32
@@ -1449,45 +1485,24 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // that wide; text keeps ~17% at depth 32, Fibonacci and periodic blocks all of them).
     const bool dc3_force = env_flag("SALZ_SA", "dc3") && bl.nb == 1 && n >= 2 && !dist;
     const bool dc3_auto = !env_flag("SALZ_SA", "doubling") && bl.nb == 1 && n >= (1u << 20) && !dist;
-    // SALZ_SA=noprobe: no repetition probe (only the depth-32 switch); noscan: the evenly spaced
-    // samples only (round 4's probe), no scan of every position
-    const bool dc3_probe_off = env_flag("SALZ_SA", "noprobe");
-    const bool dc3_scan = !env_flag("SALZ_SA", "noscan") && n >= 64;
     bool dc3_now = false;
     Alpha codes{};  // the block's byte codes 1..sigma for DC3 (raw bytes + 1 when not known)
     int codes_raw = 1;
-    if (alpha_on && n >= 64) {
+    if (n >= 64) {
         uint32_t *words = reinterpret_cast<uint32_t *>(ws.dscal) + 240;
         SALZ_HIP(fill_async(words, 0, 8 * sizeof(uint32_t), st));
         const size_t P = (size_t)n + 8;
         hipLaunchKernelGGL(k_alpha_presence, dim3(grid_for(P, kT * 16) < 2048 ? grid_for(P, kT * 16) : 2048),
                            dim3(kT), 0, st, ws.text, P, words);
         SALZ_LAUNCH_CHECK();
-        if (dc3_auto && !dc3_probe_off) {
-            // sample table, scan and count in u1 (free until round 0's survivor counts)
-            uint32_t *ptab = ws.u1, *pmul = ws.u1 + kProbeSlots, *gcnt = ws.u1 + 2 * kProbeSlots;
-            uint32_t *pfilt = ws.u1 + 3 * kProbeSlots, *pslot = pfilt + kFilterBits / 32;
-            hipLaunchKernelGGL(k_repeat_probe, dim3(1), dim3(kProbeThreads), 0, st, ws.text, n, words + 8,
-                               dc3_scan ? ptab : nullptr, pmul, gcnt, pfilt, pslot);
+        if (dc3_auto) {  // (sample table, scan and count in u1: free until round 0's survivor counts)
+            launch_repeat_probe(ws, n);
             SALZ_LAUNCH_CHECK();
-            if (dc3_scan) {
-                const uint32_t groups = (n - 32u) / 64u + 1u;  // 8 aligned grams per thread
-                const uint32_t grid = grid_for(groups, kScanThreads) < 1024 ? grid_for(groups, kScanThreads) : 1024;
-                hipLaunchKernelGGL(k_repeat_scan, dim3(grid), dim3(kScanThreads), 0, st, ws.text, n, words + 8,
-                                   ptab, pfilt, gcnt);
-                SALZ_LAUNCH_CHECK();
-                hipLaunchKernelGGL(k_repeat_count, dim3(1), dim3(kProbePoints), 0, st, words + 8, pmul, gcnt, pslot,
-                                   words + 9);
-                SALZ_LAUNCH_CHECK();
-            }
         }
         if (read_scalars(ws, 960, 48, "sa.alpha") != 0)
             return -1;
-        // half the samples repeated among themselves (long repeats everywhere), or three quarters
-        // of them anywhere in the block (what the depth-32 switch below tests): DC3 from the start
-        const uint32_t *hs = reinterpret_cast<const uint32_t *>(ws.hscal);
-        dc3_now = dc3_auto && !dc3_probe_off &&
-                  (hs[248] * 2 >= kProbe || (dc3_scan && (uint64_t)hs[249] * 4 >= 3ull * kProbePoints));
+        // the probe's verdict: DC3 from the start
+        dc3_now = dc3_auto && probe_repetitive(reinterpret_cast<const uint32_t *>(ws.hscal));
         const uint32_t *pw = reinterpret_cast<const uint32_t *>(ws.hscal) + 240;
         uint32_t sigma = 0;
         for (int c = 0; c < 256; c++)
@@ -1508,16 +1523,6 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             // blocks 12.3 against 11.9.
             alpha.bits = bits;
             alpha.k = 64u / bits;
-        } else if (bl.nb == 1 && !dist && env_flag("SALZ_SA", "rawtext")) {
-            // SALZ_SA=rawtext: more than 127 distinct bytes (binary or mixed data) keyed so that
-            // round 1 can be keyed by the text too (symbols >= 1): 8 symbols of 8 bits for 128..255
-            // distinct bytes (the depth of raw keys), 7 of 9 bits (byte + 1) for all 256 (depth 7).
-            // Not the default: on the mixed input the SA went 24.76 -> 25.57 ms and C3 2977 ->
-            // 2897 MB/s (round 5, tools/ab_env.sh on one box). Its long repeats leave large groups
-            // at depth 7 whose 63-bit text keys take 8 radix passes plus the group passes, where a
-            // rank round sorts (large group, rank) in 4 or 5; and round 0 at depth 7 finishes fewer.
-            alpha.bits = sigma <= 255 ? 8u : 9u;
-            alpha.k = sigma <= 255 ? 8u : 7u;
         }
     }
     if (dc3_force || dc3_now)
@@ -1528,9 +1533,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     // round): one byte per position, zero padded. (A split block's bucket list lives in u3 and
     // its round 0 reads the raw text: no mapped copy there.)
     uint8_t *tmapped = nullptr;
-    if (alpha.bits == 9) {
-        tmapped = ws.text;  // (9-bit symbols are the raw bytes + 1: nothing to map)
-    } else if (alpha.bits && !dist) {
+    if (alpha.bits && !dist) {
         tmapped = reinterpret_cast<uint8_t *>(ws.u3);
         const size_t P = (size_t)n + 8;
         hipLaunchKernelGGL(k_map_text, dim3(grid_for(P + 64, kT * 16)), dim3(kT), 0, st, ws.text, P, alpha,
@@ -1585,24 +1588,23 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     const int kb = bit_width(n);
     static const bool verbose = env_flag("SALZ_DEBUG", "sa");
     const bool mode_global = env_flag("SALZ_SA", "global"), mode_seg = env_flag("SALZ_SA", "segmented");
-    const bool lg_flat = env_flag("SALZ_SA", "lgflat");
-    // groups of at most seg_tiny members are ordered by counting in k_seg_sort (SALZ_SA=tiny=0:
-    // LSD passes everywhere). C2 SA 21.9 / 21.0 / 20.9 / 20.8 / 20.6 / 20.5 / 20.4 / 22.7 ms at
-    // 0 / 8 / 16 / 32 / 64 / 128 / 256 / 2048; mixed 100 MB 27.2 (0) -> 25.7 ms (64-256)
+    // groups of at most seg_tiny members are ordered by counting in k_seg_sort, larger ones by LSD
+    // passes in LDS. C2 SA 21.9 / 21.0 / 20.9 / 20.8 / 20.6 / 20.5 / 20.4 / 22.7 ms at 0 / 8 / 16 /
+    // 32 / 64 / 128 / 256 / 2048; mixed 100 MB 27.2 (0) -> 25.7 ms (64-256)
     // (profiles/r04n_tiny_sweep.txt)
-    const uint32_t seg_tiny = (uint32_t)env_num("SALZ_SA", "tiny", 128);
+    constexpr uint32_t seg_tiny = 128;
     // the text round counts groups of up to 256 (C2 SA 20.02 -> 19.89 ms, enwik9-sized blocks
     // 12.2 -> 12.0 ms; the rank rounds of mixed data are faster at 128: profiles/r04w_c3_ab.txt)
-    const uint32_t seg_tiny_text = (uint32_t)env_num("SALZ_SA", "tiny", 256);
+    constexpr uint32_t seg_tiny_text = 256;
     // The text round's LDS passes sort (group, top key bits) to 48 bits (6 passes) and leave the
     // rarer ties to k_seg_text_fix: C2 SA 20.29 -> 20.18 ms against 40 bits (5 passes), 52 bits
     // (7 passes) 20.28 (profiles/r04w_c3_ab.txt).
     constexpr int lsd_bits = 48;
     // Round 1 keyed by text (see k_keys_text): one block or a batch, the block's own sort (not a
     // split block's bucket), an alphabet of at most 127 bytes (symbols >= 1, so zero padding
-    // is unambiguous). SALZ_SA=rank1 keeps round 1 on ranks.
+    // is unambiguous); blocks of more than 127 distinct bytes keep round 1 on ranks.
     // (a split block: the decision every rank made in dist_suffix_array, from the same alphabet)
-    const bool text1 = dist ? dist->text1 : !env_flag("SALZ_SA", "rank1") && alpha.bits > 0;
+    const bool text1 = dist ? dist->text1 : alpha.bits > 0;
     if (text1 && (!alpha.bits || !tmapped)) {
         set_error("suffix sort: text round without a compacted alphabet");
         return -1;
@@ -1671,9 +1673,10 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             hipLaunchKernelGGL(k_seg_text_fix, dim3(nwin), dim3(kSegThreads), 0, st, K, V, plan, rb, need);
             SALZ_LAUNCH_CHECK();
             // the large groups: each in whole radix tiles on its 63 key bits (7 passes of 9), or
-            // (SALZ_SA=lgflat) radix-sorted on the key and then on their large group
+            // (one large group, or too many tiles for the segmented scan) radix-sorted on the key
+            // and then on their large group
             const size_t tseg_words = 2 * (size_t)lgtiles + 2 * (size_t)GL + (size_t)kMaxDigits * GL;
-            const bool tlg_seg = mL && GL > 1 && !lg_flat && lgtiles <= kSegScanMaxTiles &&
+            const bool tlg_seg = mL && GL > 1 && lgtiles <= kSegScanMaxTiles &&
                                  (size_t)lgtiles * kRadixTile <= ws.cap_s && tseg_words <= ws.cap_s;
             if (tlg_seg) {
                 if (sort_large_segmented(tbits) != 0)
@@ -1715,10 +1718,11 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
             // groups + global sort of the large ones on (large group, rank): pick the one
             // with less HBM traffic (32 B per element and 8-bit pass; 24 B per LDS-sorted or
             // extracted/put-back element).
-            // the large groups in whole tiles, sorted each on its own (SALZ_SA=lgflat: on (large
-            // group, rank) in one list); tile tables in u1 (free until k_surv)
+            // the large groups in whole tiles, sorted each on its own (one large group, or too many
+            // tiles: on (large group, rank) in one list); tile tables in u1 (free until k_surv).
+            // Round 5: mixed 100 MB SA 24.76 -> 24.24 ms against the one list.
             const size_t seg_words = 2 * (size_t)lgtiles + 2 * (size_t)GL + (size_t)kMaxDigits * GL;
-            const bool lg_seg = mL && GL > 1 && !lg_flat && lgtiles <= kSegScanMaxTiles &&
+            const bool lg_seg = mL && GL > 1 && lgtiles <= kSegScanMaxTiles &&
                                 (size_t)lgtiles * kRadixTile <= ws.cap_s && seg_words <= ws.cap_s;
             const int bits_all = kb + bit_width(G_act - 1),
                       bits_large = lg_seg ? kb : kb + bit_width(GL ? GL - 1 : 0);
@@ -1842,10 +1846,9 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         const uint32_t span = (uint32_t)(((uint64_t)n + parts - 1) / parts);
         uint32_t *later = reinterpret_cast<uint32_t *>(Kx);  // free until k_keys
         const uint32_t ihi = mode == 0 ? 0xffffffffu : mode == 1 ? span : 0u;
-        // (the text round's keys with the survivors' entries, where Kx is not the rank list: SALZ_SA=
-        // keystext keeps the separate gather)
-        const bool keys_apart = env_flag("SALZ_SA", "keystext");
-        const bool fuse_keys = textnext && mode == 0 && !keys_apart;
+        // (the text round's keys with the survivors' entries, where Kx is not the rank list: round
+        // 5, C2 SA -0.35 ms against the separate gather, which staged blocks keep)
+        const bool fuse_keys = textnext && mode == 0;
         const TextNext tn{tmapped, fuse_keys ? Kx : nullptr, bl, alpha, h};
         hipLaunchKernelGGL(k_commit, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, headpos,
                            P, reinterpret_cast<unsigned long long *>(d64 + 1), offo, offn, Vx, textnext ? gin : ngid,

@@ -294,6 +294,9 @@ def encode_block_split(src, device: int = 0, group=None, ctx=None, comm: Optiona
     round: through the library's own RCCL communicator when `comm` is given (DistComm, nccl
     groups), else through torch.distributed callbacks (any backend; gloo stages through host
     memory). Rank 0 gathers the pieces (and their LCPs) and runs the rest of the pipeline.
+    A block of 2^20 suffixes or more that the repetition probe sends to DC3 is not split (the
+    split sorter is prefix doubling only, dsa.hip): rank 0 encodes it whole on its GPU instead, and
+    cache["split"] says which way the last block went.
     `cache` (a dict kept by the caller) holds the device buffers across calls. Returns the stream
     on rank 0 (bit-identical to salz_encode_safe; with as_tensor, the uint8 tensor of it in HBM,
     a view of the cached output buffer), None elsewhere."""
@@ -305,7 +308,9 @@ def encode_block_split(src, device: int = 0, group=None, ctx=None, comm: Optiona
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     dev = torch.device("cuda", device)
     if isinstance(src, torch.Tensor):
-        text = src if src.device == dev else src.to(dev)
+        if src.dtype != torch.uint8:
+            raise TypeError(f"encode_block_split: a uint8 tensor is required, not {src.dtype}")
+        text = (src if src.device == dev else src.to(dev)).reshape(-1).contiguous()
     else:
         s = np.ascontiguousarray(np.asarray(src, dtype=np.uint8).reshape(-1))
         text = torch.from_numpy(s.copy()).to(dev)
@@ -316,9 +321,11 @@ def encode_block_split(src, device: int = 0, group=None, ctx=None, comm: Optiona
         ctx = salz_amd.Context(device, N)
     bufs = cache if cache is not None else {}
     try:
-        if bufs.get("N") != N:
+        key = (N, dev.index, rank)  # (device buffers: one set per block size, device and rank)
+        if bufs.get("key") != key:
             xcap = N + 64
-            bufs.update(N=N, xcap=xcap,
+            bufs.clear()
+            bufs.update(key=key, xcap=xcap,
                         xsend=torch.empty(xcap, dtype=torch.int32, device=dev),
                         xrecv=torch.empty(xcap, dtype=torch.int32, device=dev),
                         sa_piece=torch.empty(max(n, 1), dtype=torch.int32, device=dev),
@@ -343,8 +350,16 @@ def encode_block_split(src, device: int = 0, group=None, ctx=None, comm: Optiona
                 ctx.handle, text.data_ptr(), N, world, rank, ctypes.byref(coll.ops), xsend.data_ptr(),
                 xrecv.data_ptr(), bufs["xcap"], sa_piece.data_ptr(), lcp_piece.data_ptr(), offs, ctypes.byref(lcp_ok))
             err = coll.error or ""
+        if rc == 1:  # not split (a repetitive block, every rank alike): rank 0 encodes it whole (DC3)
+            bufs["split"] = False
+            if rank != 0:
+                return None
+            out = bufs["out"]
+            olen = ctx.encode_device(text.data_ptr(), N, out.data_ptr(), out.numel())
+            return out[:olen] if as_tensor else out[:olen].cpu().numpy().tobytes()
         if rc != 0:
             raise salz_amd.SalzError(f"split suffix sort failed: {salz_amd.last_error()} {err}")
+        bufs["split"] = True
         offsets = [int(offs[i]) for i in range(world + 1)]
         if world > 1:
             ok = torch.tensor([lcp_ok.value], dtype=torch.int64, device="cpu" if host else dev)

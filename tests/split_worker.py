@@ -42,10 +42,16 @@ def main():
     perblock = opt == "perblock"
     ctx = None if perblock else salz_amd.Context(0, max(len(data[k]) for k in names))
     out = {}
+    info = []  # per block (rank 0): split or not, and the DC3 levels of the encode
+    cache = {}
     for k in names:
-        s = encode_block_split(data[k], 0, ctx=ctx, comm=comm)
+        s = encode_block_split(data[k], 0, ctx=ctx, comm=comm, cache=cache)
         if rank == 0:
             out[k] = np.frombuffer(s, np.uint8)
+            lv = ctx.stats()["sa_dc3_levels"] if ctx is not None else -1
+            info.append((k, int(cache["split"]), lv))
+    if rank == 0:
+        out["__info__"] = np.array(repr(info))
     if ctx is not None:
         ctx.close()
     if comm is not None:

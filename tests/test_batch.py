@@ -92,7 +92,7 @@ def test_batch_matches_per_block_oracle(ctx, kind, size, block):
 
 
 @pytest.mark.parametrize("env", [("SALZ_SA", "plcp"), ("SALZ_SA", "global"), ("SALZ_SA", "segmented"),
-                                 ("SALZ_SA", "rank1"), ("SALZ_PARSE", "klog=6"), ("SALZ_PARSE", "klog=9"),
+                                 ("SALZ_PARSE", "klog=6"), ("SALZ_PARSE", "klog=9"),
                                  ("SALZ_PARSE", "noskip")])
 @pytest.mark.parametrize("kind,size,block", [("mixed", 16384 * 25 + 4321, 16384),
                                              ("patch", 8192 * 30 + 100, 8192)])

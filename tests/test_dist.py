@@ -123,3 +123,68 @@ def test_gather_container_world1_process_group():
     ok = q.get(timeout=120)
     p.join(timeout=60)
     assert ok and p.exitcode == 0
+
+
+def _xchg_worker(rank, world, port, q):
+    """One exchange of the split suffix sort both ways: torch's all_to_all_single with split sizes
+    (the gloo callbacks' path, salz_amd/dist.py) and the grouped point-to-point sends and receives
+    of the in-library RCCL path (dsa.hip RcclXchg) at the offsets the library computes."""
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    import salz_amd
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(100 + rank)
+        sc = [int(x) for x in rng.integers(0, 40, world)]
+        sc[(rank + 1) % world] = 0  # a peer that gets nothing
+        rc_t = torch.zeros(world, dtype=torch.int64)
+        dist.all_to_all_single(rc_t, torch.tensor(sc, dtype=torch.int64))
+        rc = [int(x) for x in rc_t]
+        xsend = torch.tensor([rank * 1_000_000 + d * 1000 + k for d in range(world) for k in range(sc[d])],
+                             dtype=torch.int64)
+        want = torch.zeros(sum(rc), dtype=torch.int64)
+        dist.all_to_all_single(want, xsend, rc, sc)
+        so, ro = salz_amd.xchg_offsets(sc, rc)
+        got = torch.full((sum(rc),), -1, dtype=torch.int64)
+        reqs = []
+        for r in range(world):
+            if r == rank:
+                got[ro[r]:ro[r] + rc[r]] = xsend[so[r]:so[r] + sc[r]]
+                continue
+            if sc[r]:
+                reqs.append(dist.isend(xsend[so[r]:so[r] + sc[r]].clone(), r))
+            if rc[r]:
+                buf = torch.empty(rc[r], dtype=torch.int64)
+                reqs.append((dist.irecv(buf, r), buf, ro[r]))
+        for x in reqs:
+            if isinstance(x, tuple):
+                x[0].wait()
+                got[x[2]:x[2] + len(x[1])] = x[1]
+            else:
+                x.wait()
+        q.put((rank, bool(torch.equal(got, want)), sc, rc))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rccl_exchange_offsets_match_all_to_all(world):
+    """The in-library RCCL exchange's packing: the per-peer send and receive offsets
+    it uses for its grouped ncclSend / ncclRecv give, rank by rank, exactly what all_to_all_single
+    with split sizes (the gloo callbacks' path) delivers, with empty runs among them. The RCCL calls
+    themselves run only at world 1 on the one-GPU box (tests/test_dist_split.py); a multi-rank RCCL
+    exchange is not covered by this suite."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_xchg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _, _ in res), res

@@ -35,6 +35,12 @@ def _inputs():
     }
 
 
+def _rep_inputs():
+    """Blocks of 2^20 suffixes or more that the repetition probe sends to DC3: not split."""
+    runs = np.repeat(np.random.default_rng(5).integers(0, 3, (3 << 20) // 50 + 1, dtype=np.uint8), 50)[:3 << 20]
+    return {"fib3m": gen("fib", 3 << 20), "runs3m": runs.copy()}
+
+
 def _run_split(tmp_path, world, inputs, *extra, sa_env=""):
     src = tmp_path / "in.npz"
     out = tmp_path / "out.npz"
@@ -60,20 +66,35 @@ def _run_split(tmp_path, world, inputs, *extra, sa_env=""):
         rc, ref = oracle_encode(s)
         assert rc == 0
         assert got[k].tobytes() == ref, k
+    import ast
+
+    return {k: (split, lv) for k, split, lv in ast.literal_eval(str(got["__info__"]))}
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_split_suffix_array_matches_oracle(tmp_path, world):
     """World 1 reads rank[i + h] locally (no collective); the others exchange requests every
     doubling round but round 1 of text blocks, which is keyed by the text every rank holds."""
-    _run_split(tmp_path, world, _inputs())
+    info = _run_split(tmp_path, world, _inputs())
+    assert all(split for split, _ in info.values()), info
 
 
-@pytest.mark.parametrize("world,sa_env", [(1, "xchg"), (2, "rank1"), (3, "rank1,xchg")])
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_split_repetitive_blocks_encode_whole(tmp_path, world):
+    """A 3 MiB Fibonacci block and runs of 50 equal bytes (the repetition probe's DC3 blocks) are
+    not split into ~log2(max LCP) exchanged doubling rounds: every rank takes the probe's decision
+    and rank 0 encodes the block whole with DC3; the streams equal the CPU
+    port's."""
+    info = _run_split(tmp_path, world, _rep_inputs())
+    for k, (split, levels) in info.items():
+        assert not split and levels > 0, (k, split, levels)
+
+
+@pytest.mark.parametrize("world,sa_env", [(1, "xchg"), (3, "xchg")])
 def test_split_exchange_variants(tmp_path, world, sa_env):
-    """The exchange forced at one rank (SALZ_SA=xchg: requests to itself through the collectives),
-    and round 1 on ranks instead of text (rank1: one exchange more per block, the idle ranks'
-    sequence without the skipped round)."""
+    """The exchange forced at one rank (SALZ_SA=xchg: requests to itself through the collectives)
+    and at three (where it runs anyway; round 1 of the mixed block is on ranks, one exchange more
+    than the text blocks', so the idle ranks' sequences differ by block)."""
     _run_split(tmp_path, world, _inputs(), sa_env=sa_env)
 
 

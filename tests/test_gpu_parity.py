@@ -83,12 +83,10 @@ def test_stages_match_oracle(ctx, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
-@pytest.mark.parametrize("scan", ["", "3pass"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("mixed", 3000000, 4, 0), ("text", 1500000, 8, 0)])
-def test_scan_launch_shapes(ctx, monkeypatch, scan, kind, n, seed, alpha):
-    """Scans of 2..1024 tiles with each tile reducing its own carry (the default) or with the
-    tile totals scanned by a launch of their own (SALZ_SCAN=3pass) give the oracle's stream."""
-    monkeypatch.setenv("SALZ_SCAN", scan)
+def test_scan_launch_shapes(ctx, kind, n, seed, alpha):
+    """Scans of 2..1024 tiles, each tile reducing its own carry from the tile totals before it,
+    give the oracle's stream."""
     src = _make(kind, n, seed, alpha)
     rc, ref = oracle_encode(src)
     assert rc == 0 and ctx.encode(src) == ref
@@ -268,31 +266,21 @@ def test_encode_batch_grows_workspace(salz, cap, block, size):
         assert rc == 0 and got[k] == s, k
 
 
-@pytest.mark.parametrize("keys", ["", "noalpha", "tiny=2048", "tiny=0", "rank1", "rank1,tiny=2048",
-                                  "noalpha,tiny=2048", "d9", "rank1,d9", "rawtext", "lgflat", "keystext"])
 @pytest.mark.parametrize("mode", ["global", "segmented"])
 @pytest.mark.parametrize("kind,n,seed,alpha", [("text", 600000, 5, 0), ("mixed", 500000, 6, 0),
                                                ("fib", 300000, 0, 0), ("smx", 200000, 2, 2),
                                                ("smx", 150000, 3, 20), ("runs", 120000, 0, 0),
                                                ("zeros", 70000, 0, 0), ("smx", 300000, 4, 100),
                                                ("runs40", 700001, 0, 0), ("smx", 250000, 8, 200)])
-def test_suffix_sort_modes(ctx, monkeypatch, keys, mode, kind, n, seed, alpha):
+def test_suffix_sort_modes(ctx, monkeypatch, mode, kind, n, seed, alpha):
     """Both doubling-round sorts (global radix on (group, rank); LDS sort of small groups +
-    extracted large groups; SALZ_SA=global / segmented), with round-0 keys from the compacted
-    alphabet (the default for texts of <= 127 distinct bytes: 2 to 32 symbols per key) or raw
-    bytes ("noalpha"), give the unique suffix array; blocks of more than 127 distinct bytes with raw
-    8-byte keys (the default) or with symbols >= 1 ("rawtext": 8-bit codes for 128..255 distinct
-    bytes, byte + 1 as 9-bit symbols for all 256, 7 per key) so that round 1 can be keyed by text;
-    round 1 keyed by the text at i + h0 (the default for alphabets of symbols >= 1) or by ranks
-    ("rank1"); groups of up to 128 members (rank rounds)
-    or 256 (the text round) placed by counting and larger ones by LSD passes in LDS (the
-    default), every group by counting ("tiny=2048"), or every group by the LSD passes ("tiny=0":
-    on the repetitive small-alphabet "runs40" block the text round's LSD leaves runs of equal top
-    key bits longer than 64 entries, which k_seg_text_fix orders with its bitonic network); radix passes of 8-bit digits (the default) or of 9-bit digits where they save a
-    pass ("d9": 63-bit text keys in 7 passes); the large groups of a rank round in whole radix
-    tiles sorted each on its rank bits (the default) or in one list on (large group, rank)
-    ("lgflat"); the text round's keys gathered by round 0's commit (the default) or apart ("keystext")."""
-    monkeypatch.setenv("SALZ_SA", ",".join(x for x in (mode, keys) if x))
+    extracted large groups; SALZ_SA=global / segmented) give the unique suffix array, with round-0
+    keys from the compacted alphabet (texts of <= 127 distinct bytes: 2 to 32 symbols per key,
+    round 1 keyed by the text at i + h0) or raw 8-byte keys (more than 127 distinct bytes, round 1
+    on ranks); groups of up to 128 members (rank rounds) or 256 (the text round) placed by counting
+    and larger ones by LSD passes in LDS; the large groups of a rank round in whole radix tiles
+    sorted each on its rank bits, or in one list on (large group, rank) where there is one."""
+    monkeypatch.setenv("SALZ_SA", mode)
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
     o = oracle_stages(src)
@@ -306,14 +294,13 @@ DC3_CASES = STAGE_CASES + [("text", 300001, 4, 0), ("smx", 40000, 7, 200), ("mix
                            ("fib", 65537, 0, 0), ("zeros", 3000, 0, 0)]
 
 
-@pytest.mark.parametrize("keys", ["1", "0", "1s"])
 @pytest.mark.parametrize("kind,n,seed,alpha", DC3_CASES)
-def test_dc3_matches_oracle(ctx, monkeypatch, keys, kind, n, seed, alpha):
+def test_dc3_matches_oracle(ctx, monkeypatch, kind, n, seed, alpha):
     """The DC3 suffix sorter (dc3.hip, forced with SALZ_SA=dc3) gives the unique suffix array on
-    every input kind, from the block's byte codes (the default) or raw bytes + 1 ("noalpha"), with
-    the levels of small triples named from their presence bitmap (the default) or every level
-    named by sorting ("1s", dc3sort)."""
-    monkeypatch.setenv("SALZ_SA", {"1": "dc3", "0": "dc3,noalpha", "1s": "dc3,dc3sort"}[keys])
+    every input kind, from the block's byte codes (at most 255 distinct bytes) or raw bytes + 1 (all
+    256), with the levels of small triples named from their presence bitmap and the others by
+    sorting."""
+    monkeypatch.setenv("SALZ_SA", "dc3")
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
     assert ctx.stats()["sa_dc3_levels"] > 0
@@ -376,14 +363,10 @@ def test_dc3_edge_sizes(ctx, monkeypatch):
             assert rc == 0 and out == ref, (N, kind)
 
 
-@pytest.mark.parametrize("keys", ["", "ansv2", "ansvsp"])
 @pytest.mark.parametrize("kind,n,seed", [("text", 6_000_007, 8), ("mixed", 5_000_001, 9)])
-def test_ansv_staging_levels(ctx, monkeypatch, keys, kind, n, seed):
-    """Candidates of blocks past 2^22 positions through one staging level (the default) or two
-    (SALZ_SA=ansv2: each 2^20-position run re-sorted into 2^17-position sub-runs before the scatter
-    into cand), staged with the suffix's position bits packed into the answer (the default) or in a
-    position array of their own ("ansvsp"): psv/nsv and their lengths equal the oracle's."""
-    monkeypatch.setenv("SALZ_SA", keys)
+def test_ansv_staging_levels(ctx, kind, n, seed):
+    """Candidates of blocks past 2^22 positions, staged by text range with the suffix's position
+    bits packed into the answer: psv/nsv and their lengths equal the oracle's."""
     src = gen(kind, n, seed)
     out, d = ctx.encode_dump(src)
     o = oracle_stages(src)
@@ -416,14 +399,14 @@ def test_suffix_sort_round_checks():
     assert r.returncode == 0 and "round checks ok" in r.stdout, (r.stdout + r.stderr)[-3000:]
 
 
-@pytest.mark.parametrize("algo", ["", "noscan", "noprobe", "doubling"])
+@pytest.mark.parametrize("algo", ["", "doubling"])
 def test_dc3_auto_switch(ctx, monkeypatch, algo):
-    """A repetitive block of >= 1 MiB goes to DC3 by default. Before round 0 when the repetition
+    """A repetitive block of >= 1 MiB goes to DC3 by default, before round 0: when the repetition
     probe finds its evenly spaced 32-gram samples repeated among themselves (Fibonacci, period 3),
     or finds three quarters of them occurring elsewhere in the block by scanning every position
-    (a text repeated once at distance n / 2, runs of 40 equal bytes: the samples rarely meet there;
-    SALZ_SA=noscan leaves those to the depth-32 switch); with SALZ_SA=noprobe at depth 32; text
-    does not go; SALZ_SA=doubling keeps prefix doubling. All give the reference stream."""
+    (a text repeated once at distance n / 2, runs of 40 equal bytes: the samples rarely meet
+    there); text does not go; SALZ_SA=doubling keeps prefix doubling. All give the reference
+    stream."""
     monkeypatch.setenv("SALZ_SA", algo)
     for kind, n in (("fib", 3 << 20), ("period3", 2 << 20), ("text", 2 << 20), ("halves", (2 << 20) + 4321),
                     ("runs40", (3 << 20) + 77)):
@@ -433,8 +416,7 @@ def test_dc3_auto_switch(ctx, monkeypatch, algo):
         st = ctx.stats()
         assert (st["sa_dc3_levels"] > 0) == rep, kind
         if rep:  # the probe skips round 0 of doubling
-            early = algo == "" or (algo == "noscan" and kind in ("fib", "period3"))
-            assert (st["sa_rounds"] == 0) == early, (kind, st["sa_rounds"])
+            assert st["sa_rounds"] == 0, (kind, st["sa_rounds"])
         rc, ref = oracle_encode(src)
         assert rc == 0 and out == ref, kind
 
@@ -454,7 +436,7 @@ def test_lcp_paths(ctx, monkeypatch, lcp_sa, kind, n, seed, alpha):
     assert rc == 0 and out == ref
 
 
-@pytest.mark.parametrize("skip", ["1", "1l0", "1s0", "1n2", "1r0", "0", "1p0", "1t0", "1m0"])
+@pytest.mark.parametrize("skip", ["1", "0"])
 @pytest.mark.parametrize("kind,n,seed,alpha,klog", [("mixed", 3_000_000, 3, 0, "6"),
                                                     ("mixed", 2_000_001, 7, 0, "9"),
                                                     ("text", 1_500_000, 2, 0, "7"),
@@ -462,18 +444,10 @@ def test_lcp_paths(ctx, monkeypatch, lcp_sa, kind, n, seed, alpha):
                                                     ("runs", 400_000, 0, 0, "6")])
 def test_parse_wave_skip(ctx, monkeypatch, skip, kind, n, seed, alpha, klog):
     """From the third pass on, waves of chunks whose decisions would repeat skip the pass
-    (parse.hip k_parse_mark; SALZ_PARSE=noskip turns it off): decisions, the exact suffix
-    costs and the stream match the oracle with and without skipping, with the chunk range test
-    (the default) and the per-candidate test alone ("1r0", norange), on the packed candidates
-    (the default) and the full ones ("1p0", nopack), with the lazy per-chunk cost offsets of the
-    skipping passes (the default) and without ("1l0", nolazy), and with the per-candidate test
-    as a wave per listed chunk (the default) or inside the test kernel ("1s0", nosplit), and with
-    the exit set compacted a thread per node ("1n2", nodes=2; by default only where it is
-    sparse), and with the exit set re-packed only in the tiles the walk touched (the default) or
-    in every tile ("1t0", notouch); emission marks the path in one launch (the default) or a launch per
-    jump level ("1m0", marksteps)."""
-    flags = {"0": "noskip", "1l0": "nolazy", "1s0": "nosplit", "1n2": "nodes=2", "1r0": "norange",
-             "1p0": "nopack", "1t0": "notouch", "1m0": "marksteps"}.get(skip)
+    (parse.hip k_parse_mark: the chunk range test, then a wave per listed chunk; lazy per-chunk
+    cost offsets; exit set re-packed only in the tiles the walk touched) and without
+    (SALZ_PARSE=noskip): decisions, the exact suffix costs and the stream match the oracle."""
+    flags = {"0": "noskip"}.get(skip)
     monkeypatch.setenv("SALZ_PARSE", f"klog={klog}" + (f",{flags}" if flags else ""))
     src = _make(kind, n, seed, alpha)
     out, d = ctx.encode_dump(src)
@@ -619,13 +593,12 @@ def test_cli_multi_batch_ring_and_exact_multiple(salz, tmp_path):
                                     (4096 * 4096, 24), (4096 * 4096 + 1, 64), (8192 * 4096 + 3000, 33),
                                     (24576 * 4096 + 4097, 40), (100_003, 9), (200_001, 45),
                                     (24576 * 4096 + 4097, 63)])
-@pytest.mark.parametrize("digits", ["", "d9"])
-def test_radix_sort_selftest(salz, monkeypatch, m, bits, digits):
+@pytest.mark.parametrize("nine", [False, True])
+def test_radix_sort_selftest(salz, m, bits, nine):
     """The LSD radix sort (radix.hip) on random keys, and on keys with few distinct values for
     stability: sorted, stable and a permutation of its input, at tile counts that are and are not
     multiples of the 8 XCDs (the scatter's XCD-contiguous tile order) and across the row scan's
     shapes (256-thread rows up to 4096 tiles, 512 up to 8192, 1024 beyond, looping past 24576);
     digit plans of 8-bit passes (the default; 24, 40, 64 bits), 9-bit passes (9, 45, 63 bits: one pass fewer)
-    and both (17, 33 bits) under SALZ_SA=d9."""
-    monkeypatch.setenv("SALZ_SA", digits)
-    assert salz.radix_selftest(m, bits, iters=2, seed=7) == 0
+    and both (17, 33 bits) with 9-bit digits allowed (the rank rounds' plan)."""
+    assert salz.radix_selftest(m, bits, iters=2, seed=7, nine=nine) == 0

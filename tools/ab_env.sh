@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B timing of environment settings on one GPU box: R rounds, each running the bench once per
 # setting (a setting is a space-separated list of VAR=value, "-" for none).
-#   R=3 ARGS="--kind mixed" bash tools/ab_env.sh "SALZ_SA=rank1" -
+#   R=3 ARGS="--kind mixed" bash tools/ab_env.sh "SALZ_SA=global" -
 R=${R:-3}
 mkdir -p gpurun_out/ab_env
 for r in $(seq 1 $R); do
