@@ -53,36 +53,33 @@ struct PhiSrc {
     }
 };
 
-__global__ void k_plcp_short(const uint8_t *__restrict__ T, const uint32_t *__restrict__ phi,
-                             Blocks bl, uint32_t *__restrict__ plv, uint32_t *__restrict__ queue,
-                             uint32_t *__restrict__ qcount)
+// PLCP[i] of position i by its first kShortBytes bytes: plv[i] = PLCP[i] + i for an irreducible
+// i, 0 for a reducible one (the max-scan fills it in); returns true when i needs a longer compare.
+__device__ __forceinline__ bool plcp_short_one(const uint8_t *__restrict__ T, const uint32_t *__restrict__ phi,
+                                               const Blocks &bl, uint32_t i, uint32_t *__restrict__ plv)
 {
-    size_t ii = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (ii >= bl.npos)
-        return;
-    uint32_t i = (uint32_t)ii;
     const uint32_t e = bl.end(i), b0 = bl.start(i);
     if (i >= e) {  // a batch's dead position: no suffix (the max-scan carries past it)
         plv[i] = 0;
-        return;
+        return false;
     }
     const uint32_t j = phi[i];
     if (j == kNone) {  // smallest suffix of its block: PLCP = 0
         plv[i] = i;
-        return;
+        return false;
     }
-    bool irr = i == b0 || j == b0 || T[i - 1] != T[j - 1];  // (j is in i's block)
+    const bool irr = i == b0 || j == b0 || T[i - 1] != T[j - 1];  // (j is in i's block)
     if (!irr) {
         plv[i] = 0;
-        return;
+        return false;
     }
-    uint32_t limit = e - (i > j ? i : j);
+    const uint32_t limit = e - (i > j ? i : j);
     uint32_t L = 0;
     bool done = false;
 #pragma unroll
     for (int w = 0; w < (int)(kShortBytes / 8); w++) {
         if (!done && L < limit) {
-            uint64_t x = load_u64_any(T, (size_t)i + L) ^ load_u64_any(T, (size_t)j + L);
+            const uint64_t x = load_u64_any(T, (size_t)i + L) ^ load_u64_any(T, (size_t)j + L);
             if (x) {
                 L += (uint32_t)__builtin_ctzll(x) >> 3;
                 done = true;
@@ -95,13 +92,62 @@ __global__ void k_plcp_short(const uint8_t *__restrict__ T, const uint32_t *__re
         L = limit;
         done = true;
     }
-    if (done) {
-        plv[i] = L + i;
-    } else {
-        plv[i] = 0;
-        uint32_t q = atomicAdd(qcount, 1u);
-        queue[q] = i;
+    plv[i] = done ? L + i : 0u;
+    return !done;
+}
+
+// Every position's short compare; the positions left for the long compares are gathered per
+// workgroup in LDS and appended to the queue with one global atomic per workgroup (the grid is
+// at most kShortGrid workgroups looping over the positions). A global counter bumped per wave
+// served ~88 appends per microsecond: runs of 64 equal bytes at 256 MiB queue 4 M positions
+// (one per run), which took ~45 ms that way.
+constexpr uint32_t kShortGrid = 2048;
+constexpr uint32_t kQBuf = 2048;  // LDS queue entries per workgroup before a flush
+__global__ __launch_bounds__(kT) void k_plcp_short(const uint8_t *__restrict__ T, const uint32_t *__restrict__ phi,
+                                                   Blocks bl, uint32_t *__restrict__ plv, uint32_t *__restrict__ queue,
+                                                   uint32_t *__restrict__ qcount)
+{
+    __shared__ uint32_t lq[kQBuf];
+    __shared__ uint32_t ln, lbase;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0)
+        ln = 0;
+    __syncthreads();
+    auto flush = [&](uint32_t cnt) {  // (workgroup-uniform)
+        if (tid == 0)
+            lbase = atomicAdd(qcount, cnt);
+        __syncthreads();
+        for (uint32_t k = tid; k < cnt; k += kT)
+            queue[lbase + k] = lq[k];
+        __syncthreads();
+        if (tid == 0)
+            ln = 0;
+        __syncthreads();
+    };
+    const size_t step = (size_t)gridDim.x * kT;
+    for (size_t base = (size_t)blockIdx.x * kT; base < bl.npos; base += step) {  // (uniform bound)
+        const size_t ii = base + tid;
+        const bool push = ii < bl.npos && plcp_short_one(T, phi, bl, (uint32_t)ii, plv);
+        const uint64_t m = wave_ballot(push);
+        if (m) {
+            const int leader = (int)__ffsll((unsigned long long)m) - 1;
+            uint32_t at = 0;
+            if ((int)lane_id() == leader)
+                at = atomicAdd(&ln, (uint32_t)__popcll(m));
+            at = shfl_u32(at, leader);
+            if (push)
+                lq[at + count_below(m)] = (uint32_t)ii;
+        }
+        __syncthreads();
+        const uint32_t cur = ln;
+        __syncthreads();
+        if (cur + kT > kQBuf)  // the next round could overflow the buffer
+            flush(cur);
     }
+    const uint32_t cur = ln;
+    __syncthreads();
+    if (cur)
+        flush(cur);
 }
 
 // One wave per 512-byte task: task t -> item t / nch, bytes [L + (t % nch) * 512, +512).
@@ -145,13 +191,22 @@ __global__ void k_plcp_resolve(const uint32_t *__restrict__ phi, Blocks bl,
     uint32_t i = items[x], j = phi[i];
     uint32_t limit = bl.end(i) - (i > j ? i : j);
     uint32_t f = found[x];
-    if (f != kNone) {
+    bool more = false;
+    if (f != kNone)
         plv[i] = f + i;
-    } else if (window_end >= limit) {
+    else if (window_end >= limit)
         plv[i] = limit + i;
-    } else {
-        uint32_t q = atomicAdd(next_count, 1u);
-        next_items[q] = i;
+    else
+        more = true;
+    const uint64_t m = wave_ballot(more);  // one atomic per wave
+    if (m) {
+        const int leader = (int)__ffsll((unsigned long long)m) - 1;
+        uint32_t q = 0;
+        if ((int)lane_id() == leader)
+            q = atomicAdd(next_count, (uint32_t)__popcll(m));
+        q = shfl_u32(q, leader);
+        if (more)
+            next_items[q + count_below(m)] = i;
     }
 }
 
@@ -187,8 +242,8 @@ int stage_lcp(Workspace &ws, const Blocks &bl, uint32_t *lcp_out)
         SALZ_LAUNCH_CHECK();
     }
     SALZ_HIP(fill_async(cnt, 0, 8, st));
-    hipLaunchKernelGGL(k_plcp_short, dim3(grid_for(n, kT)), dim3(kT), 0, st, ws.text, phi, bl, plv,
-                       qa, cnt);
+    hipLaunchKernelGGL(k_plcp_short, dim3(grid_for(n, kT) < kShortGrid ? grid_for(n, kT) : kShortGrid), dim3(kT), 0,
+                       st, ws.text, phi, bl, plv, qa, cnt);
     SALZ_LAUNCH_CHECK();
     if (read_scalars(ws, 0, 256, "lcp.q0") != 0)
         return -1;

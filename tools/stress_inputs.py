@@ -16,6 +16,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--size", type=int, default=64 << 20)
 ap.add_argument("--parity", action="store_true")
 ap.add_argument("--cases", default="", help="comma-separated subset of the cases (default: all)")
+ap.add_argument("--stages", action="store_true", help="a second encode with stage timing: ms per stage")
 a = ap.parse_args()
 n = a.size
 cases = {
@@ -48,4 +49,12 @@ for name, make in cases.items():
     if a.parity:
         rc, ref = oracle_encode(src)
         line += f"  parity {rc == 0 and ref == out}"
+    if a.stages:  # (timed stages synchronise between stages: a separate encode)
+        ctx.set_timing(True)
+        ctx.encode(src)
+        ctx.set_timing(False)
+        st = ctx.stats()
+        line += "  |" + " ".join(f"{k[3:]} {st[k]:.1f}" for k in ("ms_upload", "ms_sa", "ms_lcp", "ms_ansv",
+                                                                    "ms_parse", "ms_emit", "ms_total"))
+        line += f" parse_iters {st['parse_iters']}"
     print(line, flush=True)
