@@ -68,14 +68,18 @@ __global__ void k_dc3_sample_keys(const uint2 *__restrict__ tr, uint32_t ns, uin
     val[j] = (uint32_t)j;
 }
 
-// Second phase of a split triple sort: key = first symbol of the (already sorted) sample.
-__global__ void k_dc3_first_keys(const uint2 *__restrict__ tr, const uint32_t *__restrict__ val, uint32_t ns,
-                                 uint32_t n1, uint64_t *__restrict__ key)
+// Second phase of a split triple sort: key = first symbol << 32 | the name of the (second, third)
+// pair in the sample sorted by those two (pn: 1 + the distinct pairs below, coalesced), so the
+// stable sort on the first symbol leaves every triple's full identity in its key and the names
+// come from comparing neighbouring keys (before, k_dc3_heads read both neighbours' triples from
+// TR: two random 24-byte runs per sample).
+__global__ void k_dc3_first_keys(const uint2 *__restrict__ tr, const uint32_t *__restrict__ val,
+                                 const uint32_t *__restrict__ pn, uint32_t ns, uint32_t n1, uint64_t *__restrict__ key)
 {
     const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= ns)
         return;
-    key[c] = tr[dc3_pos(val[c], n1)].x;
+    key[c] = (uint64_t)tr[dc3_pos(val[c], n1)].x << 32 | pn[c];
 }
 
 // Levels whose triples fit kLutMaxBits bits (up to 8 bits a symbol: Fibonacci's first seven
@@ -191,23 +195,15 @@ __global__ void k_dc3_names_lut(const uint32_t *__restrict__ keys, uint32_t ns, 
     child[j] = make_uint2(1u + pre[w] + (uint32_t)__popc(bits[w] & ((1u << (key & 31u)) - 1u)), 0u);
 }
 
-// Name boundaries of the sorted sample: a new triple starts a new name.
-__global__ void k_dc3_heads(const uint64_t *__restrict__ key, const uint32_t *__restrict__ val,
-                            const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1, int full,
-                            uint32_t *__restrict__ flag)
+// Name boundaries of the sorted sample: a new key (triple, or first symbol and pair name) starts
+// a new name.
+__global__ void k_dc3_heads(const uint64_t *__restrict__ key, uint32_t ns, uint32_t *__restrict__ flag)
 {
     const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     if (c >= ns)
         return;
     const size_t cp = c ? c - 1 : 0;  // unconditional loads (clamped)
-    bool head;
-    if (full) {
-        head = c == 0 || key[c] != key[cp];
-    } else {
-        const uint32_t p = dc3_pos(val[c], n1), q = dc3_pos(val[cp], n1);
-        head = c == 0 || tr[p].x != tr[q].x || tr[p + 1].x != tr[q + 1].x || tr[p + 2].x != tr[q + 2].x;
-    }
-    flag[c] = head ? 1u : 0u;
+    flag[c] = c == 0 || key[c] != key[cp] ? 1u : 0u;
 }
 
 // The child's string: R[j] = name of sample j (rank part zero).
@@ -507,21 +503,28 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
         }
     }
     uint32_t *flag = ws.u0, *name = ws.u1;
+    // the radix passes' digit bytes (u16 for 9-bit digits) in u3, free during DC3: each pass's
+    // histogram reads them instead of the 8-byte keys; 9-bit digits wherever they save a pass
+    uint8_t *rdig = reinterpret_cast<uint8_t *>(ws.u3);
     if (!sar) {
         hipLaunchKernelGGL(k_dc3_sample_keys, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, ns, n1, b, full ? 1 : 0, K,
                            V);
         SALZ_LAUNCH_CHECK();
         if (radix_sort_pairs(&K, &V, K == ws.keyA ? ws.keyB : ws.keyA, V == ws.valA ? ws.valB : ws.valA, ns, 0,
-                             full ? 3 * b : 2 * b, ws, st) != 0)
+                             full ? 3 * b : 2 * b, ws, st, nullptr, nullptr, nullptr, rdig, false, true) != 0)
             return -1;
-        if (!full) {
-            hipLaunchKernelGGL(k_dc3_first_keys, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, V, ns, n1, K);
+        if (!full) {  // names of the (second, third) pairs, then the stable sort on the first symbol
+            hipLaunchKernelGGL(k_dc3_heads, dim3(grid_for(ns, kT)), dim3(kT), 0, st, K, ns, flag);
             SALZ_LAUNCH_CHECK();
-            if (radix_sort_pairs(&K, &V, K == ws.keyA ? ws.keyB : ws.keyA, V == ws.valA ? ws.valB : ws.valA, ns, 0, b,
-                                 ws, st) != 0)
+            if (scan_sum_u32(flag, name, ns, true, nullptr, ws, st) != 0)
+                return -1;
+            hipLaunchKernelGGL(k_dc3_first_keys, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, V, name, ns, n1, K);
+            SALZ_LAUNCH_CHECK();
+            if (radix_sort_pairs(&K, &V, K == ws.keyA ? ws.keyB : ws.keyA, V == ws.valA ? ws.valB : ws.valA, ns, 32,
+                                 32 + b, ws, st, nullptr, nullptr, nullptr, rdig, false, true) != 0)
                 return -1;
         }
-        hipLaunchKernelGGL(k_dc3_heads, dim3(grid_for(ns, kT)), dim3(kT), 0, st, K, V, tr, ns, n1, full ? 1 : 0, flag);
+        hipLaunchKernelGGL(k_dc3_heads, dim3(grid_for(ns, kT)), dim3(kT), 0, st, K, ns, flag);
         SALZ_LAUNCH_CHECK();
         if (scan_sum_u32(flag, name, ns, true, d32, ws, st) != 0)
             return -1;
@@ -572,7 +575,8 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
     hipLaunchKernelGGL(k_dc3_mod0, dim3(grid_for(ns, kT)), dim3(kT), 0, st, sar, name, ns, n1, n0, tr, K, V,
                        d.derr, packb);
     SALZ_LAUNCH_CHECK();
-    if (radix_sort_pairs(&K, &V, ws.keyB, ws.valB, n0, 0, b, ws, st) != 0)
+    if (radix_sort_pairs(&K, &V, ws.keyB, ws.valB, n0, 0, b, ws, st, nullptr, nullptr, nullptr, rdig, false, true) !=
+        0)
         return -1;
     // merge
     MergeIn mi{sar, ns - dummy, dummy, n1, V, n0, tr, K, packb};
