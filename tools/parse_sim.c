@@ -77,6 +77,69 @@ int parse_sim(const int32_t *psv, const int32_t *lp, const int32_t *nsv, const i
     uint32_t *oc = malloc(4ull * (ovl + 1)), *oe = malloc(4ull * (ovl + 1)), *os = malloc(4ull * (ovl + 1));
     int it;
     int64_t exits = 0;
+    /* PARSE_SIM_SEG=S: Gauss-Seidel over S segments of chunks, right to left: a segment's chunks
+       read the exact costs the pass already made for later segments, and the segment's own exact
+       costs are formed before the next segment walks (one cost array, cin) */
+    const int32_t segs = getenv("PARSE_SIM_SEG") ? atoi(getenv("PARSE_SIM_SEG")) : 0;
+    if (segs > 0) {
+        const int32_t nch = (n + chunk - 1) / chunk, per = (nch + segs - 1) / segs;
+        for (it = 0; it < 100000; it++) {
+            long changed = 0;
+            const int inter = getenv("PARSE_SIM_INTERLEAVE") != NULL;
+            for (int32_t sg = segs - 1; sg >= 0; sg--) {
+                const int32_t s0 = inter ? sg * chunk : sg * per * chunk;
+                const int32_t s1 = inter ? n : ((sg + 1) * per * chunk < n ? (sg + 1) * per * chunk : n);
+                if (s0 >= s1)
+                    continue;
+                for (int32_t a = s0; a < s1; a += inter ? segs * chunk : chunk) {
+                    int32_t b = a + chunk < n ? a + chunk : n;
+                    for (int32_t p = b - 1; p >= a; p--) {
+                        uint32_t nx1 = p + 1;
+                        uint32_t best = 9u + (nx1 >= (uint32_t)b ? cin[nx1] : cout[nx1]);
+                        uint32_t len = 1, w = 9;
+                        uint8_t ch = 0;
+                        if (p) {
+                            if (lp[p] >= 3) {
+                                uint32_t q = p + lp[p], wf = fbits(p - psv[p], lp[p]);
+                                uint32_t alt = wf + (q >= (uint32_t)b ? cin[q] : cout[q]);
+                                if ((int32_t)alt < (int32_t)best) { best = alt; len = lp[p]; w = wf; ch = 1; }
+                            }
+                            if (ln[p] >= 3) {
+                                uint32_t q = p + ln[p], wf = fbits(p - nsv[p], ln[p]);
+                                uint32_t alt = wf + (q >= (uint32_t)b ? cin[q] : cout[q]);
+                                if ((int32_t)alt < (int32_t)best) { best = alt; len = ln[p]; w = wf; ch = 2; }
+                            }
+                        }
+                        uint32_t nx = p + len;
+                        if (nx >= (uint32_t)b) { ex[p] = nx; sm[p] = w; }
+                        else { ex[p] = ex[nx]; sm[p] = w + sm[nx]; }
+                        cout[p] = best;
+                        changed += ch != chold[p];
+                        chold[p] = ch;
+                    }
+                }
+                if (inter) { /* exact costs of the current decisions everywhere */
+                    cin[n] = 0;
+                    for (int32_t q = n - 1; q >= 0; q--)
+                        cin[q] = sm[q] + cin[ex[q]];
+                } else {
+                    for (int32_t q = s1 - 1; q >= s0; q--) /* the segment's exact costs */
+                        cin[q] = sm[q] + cin[ex[q]];
+                }
+            }
+            if (getenv("PARSE_SIM_VERBOSE"))
+                fprintf(stderr, "seg it %d changed %ld\n", it, changed);
+            if (!changed)
+                break;
+        }
+        int ok = 1;
+        for (int32_t p = 1; p < n; p++)
+            if (chold[p] != refch[p]) { ok = 0; break; }
+        *iters_out = it + 1;
+        *exits_out = 0;
+        free(oc); free(oe); free(os); free(cin); free(cout); free(ex); free(sm); free(ref); free(chold); free(chnew); free(flag); free(refch);
+        return ok;
+    }
     for (it = 0; it < 100000; it++) {
         long changed = 0;
         const int32_t V = it < ovl_it ? ovl : 0;
