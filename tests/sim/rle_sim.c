@@ -16,7 +16,7 @@
 int oracle_suffix_array(const uint8_t *T, int32_t *SA, int32_t n);
 void datagen_mixed(uint8_t *out, size_t n, uint64_t seed);
 void datagen_text(uint8_t *out, size_t n, uint64_t seed);
-static uint64_t *gs; static int cmpu(const void*a,const void*b){uint64_t x=*(uint64_t*)a,y=*(uint64_t*)b;return x<y?-1:x>y;}
+static int cmpu(const void*a,const void*b){uint64_t x=*(uint64_t*)a,y=*(uint64_t*)b;return x<y?-1:x>y;}
 int main(int argc,char**argv){
   size_t N=atol(argv[1]); int kind=atoi(argv[2]); uint8_t*T=calloc(N+64,1);
   if(kind) datagen_mixed(T,N,1); else datagen_text(T,N,1);
