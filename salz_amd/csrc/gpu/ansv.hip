@@ -36,9 +36,14 @@ constexpr uint32_t kInf = 0xffffffffu;
 constexpr uint32_t kNear = 16;  // linear neighbour scan before the tree walk
 constexpr uint32_t kScan = 8;   // leaves under the deepest global tree node (scanned by the global walk)
 constexpr uint32_t kWQ = 1408;  // LDS walk-queue entries per block
-constexpr uint32_t kShards = 16;      // global-queue shards (blockIdx mod kShards)
-constexpr size_t kQCountWord = 800;   // u32 index into Workspace::dscal: 2 * kShards counters
+// Global-queue shards (blockIdx mod kShards), each with its own counter: about as many as
+// workgroups are resident at once, so concurrent blocks append to different words. With 16
+// shards, blocks whose queries nearly all leave them (a sorted run of equal bytes: every PSV is
+// none) serialised on 16 counters (~88 appends per microsecond each): zeros at 256 MiB spent ~10
+// ms of its 25 ms k_ansv_local there.
+constexpr uint32_t kShards = 1024;
 constexpr uint32_t kMaxRanges = 256;  // staging text ranges per block (rlog is raised to fit)
+constexpr size_t kQMaxWord = 800;     // u32 index into Workspace::dscal: the largest shard per side
 static_assert(kMaxRanges <= kT, "one thread per range");
 
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
@@ -80,16 +85,56 @@ __device__ __forceinline__ void put_nsv(uint4 *cand, uint32_t klog, uint32_t p, 
 }
 
 // First queue slot of shard s: the shards' regions hold as many entries as their blocks
-// have leaves (a leaf misses at most once per side), so they tile [0, n) exactly.
+// have leaves (a leaf misses at most once per side), so they tile [0, n) exactly. Shard t holds
+// blocks t, t + kShards, ...: q + (t < rem) of them; the last block is short by short_by leaves.
 __device__ __forceinline__ uint32_t shard_base(uint32_t s, uint32_t used_blocks, uint32_t n)
 {
-    const uint32_t last = used_blocks - 1u, short_by = used_blocks * kB - n;
-    uint32_t base = 0;
-    for (uint32_t t = 0; t < s; t++) {
-        const uint32_t nb = (used_blocks + kShards - 1u - t) / kShards;
-        base += nb * kB - (last % kShards == t ? short_by : 0u);
+    const uint32_t q = used_blocks / kShards, rem = used_blocks % kShards;
+    const uint32_t before = s * q + (s < rem ? s : rem);  // blocks of the shards below s
+    const uint32_t short_by = used_blocks * kB - n;
+    return before * kB - ((used_blocks - 1u) % kShards < s ? short_by : 0u);
+}
+
+// The largest shard per side (one workgroup): qmax[0] PSV, qmax[1] NSV.
+__global__ __launch_bounds__(1024) void k_queue_max(const uint32_t *__restrict__ qcount, uint32_t *__restrict__ qmax)
+{
+    __shared__ uint32_t m[2];
+    if (threadIdx.x < 2)
+        m[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t a = 0, b = 0;
+    for (uint32_t s = threadIdx.x; s < kShards; s += 1024) {
+        a = qcount[2 * s] > a ? qcount[2 * s] : a;
+        b = qcount[2 * s + 1] > b ? qcount[2 * s + 1] : b;
     }
-    return base;
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t x = shfl_xor_u32(a, o), y = shfl_xor_u32(b, o);
+        a = x > a ? x : a;
+        b = y > b ? y : b;
+    }
+    if (lane_id() == 0) {
+        atomicMax(&m[0], a);
+        atomicMax(&m[1], b);
+    }
+    __syncthreads();
+    if (threadIdx.x < 2)
+        qmax[threadIdx.x] = m[threadIdx.x];
+}
+
+// The min-tree's levels above the blocks with at most kTopNodes nodes, in one workgroup (a
+// launch per level before: ~10 launches of a few microseconds each).
+constexpr uint32_t kTopNodes = 1024;
+__global__ __launch_bounds__(1024) void k_tree_top(uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp,
+                                                   uint32_t top)
+{
+    for (uint32_t lo = top; lo >= 1; lo >>= 1) {
+        for (uint32_t x = threadIdx.x; x < lo; x += 1024) {
+            const uint32_t k = lo + x;
+            tsa[k] = umin(tsa[2 * k], tsa[2 * k + 1]);
+            tlcp[k] = umin(tlcp[2 * k], tlcp[2 * k + 1]);
+        }
+        __syncthreads();  // (global writes of this level visible to the next in the workgroup)
+    }
 }
 
 // One queued query of the block (e = leaf << 1 | nsv) walks the block's LDS min-tree; a
@@ -541,8 +586,13 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
     uint32_t *tsa = reinterpret_cast<uint32_t *>(ws.keyA);
     uint32_t *tlcp = reinterpret_cast<uint32_t *>(ws.keyB);
     uint32_t *qp = ws.valA, *qpl = ws.valB, *qn = ws.offA, *qnl = ws.offB;
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(ws.dscal) + kQCountWord;
-
+    // range fills (rfill) in radix_counts[0, kMaxRanges), the shards' counters after them
+    uint32_t *cnt = ws.radix_counts + kMaxRanges;
+    uint32_t *qmax = reinterpret_cast<uint32_t *>(ws.dscal) + kQMaxWord;
+    if (ws.radix_counts_elems < kMaxRanges + 2 * (size_t)kShards) {
+        set_error("ansv: queue counters do not fit");
+        return -1;
+    }
     SALZ_HIP(fill_async(cnt, 0, 2 * kShards * sizeof(uint32_t), st));
     uint32_t nblocks = np2 / kB;
     uint32_t used_blocks = (n + kB - 1) / kB;
@@ -583,23 +633,26 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
     hipLaunchKernelGGL(k_cand_scatter, dim3(sgrid), dim3(kT), 0, st, sp, stage, npos, ws.cand,
                        ws.klog, rlog, nranges, rfill, derr, pk);
     SALZ_LAUNCH_CHECK();
-    for (uint32_t lo = nblocks / 2; lo >= 1; lo >>= 1) {
+    uint32_t lo = nblocks / 2;
+    for (; lo > kTopNodes; lo >>= 1) {
         hipLaunchKernelGGL(k_tree_level, dim3(grid_for(lo, kT)), dim3(kT), 0, st, tsa, tlcp, lo,
                            lo);
         SALZ_LAUNCH_CHECK();
     }
-    if (read_scalars(ws, 0, (kQCountWord + 2 * kShards) * sizeof(uint32_t), "ansv.q") != 0)
+    if (lo >= 1) {
+        hipLaunchKernelGGL(k_tree_top, dim3(1), dim3(1024), 0, st, tsa, tlcp, lo);
+        SALZ_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_queue_max, dim3(1), dim3(1024), 0, st, cnt, qmax);
+    SALZ_LAUNCH_CHECK();
+    if (read_scalars(ws, 0, (kQMaxWord + 2) * sizeof(uint32_t), "ansv.q") != 0)
         return -1;
     if (const uint32_t e = reinterpret_cast<uint32_t *>(ws.hscal)[kErrWord]) {
         set_error("ansv: device index check failed (code 0x%x): suffix array corrupt", e);
         return -1;
     }
-    uint32_t nqp = 0, nqn = 0;  // largest shard per side
-    for (uint32_t s = 0; s < kShards; s++) {
-        const uint32_t *h = reinterpret_cast<uint32_t *>(ws.hscal) + kQCountWord + 2 * s;
-        nqp = h[0] > nqp ? h[0] : nqp;
-        nqn = h[1] > nqn ? h[1] : nqn;
-    }
+    const uint32_t nqp = reinterpret_cast<uint32_t *>(ws.hscal)[kQMaxWord];  // largest shard per side
+    const uint32_t nqn = reinterpret_cast<uint32_t *>(ws.hscal)[kQMaxWord + 1];
     Tree t{tsa, tlcp, ws.sa, lcp, n, np2};
     if (nqp) {
         hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqp, kT), kShards), dim3(kT), 0, st, t,

@@ -257,7 +257,8 @@ int workspace_alloc(Workspace &ws, int device, size_t max_block)
     ws.cap_s = (ws.cap_n + 1 + kLayoutPad - 1) / kLayoutPad * kLayoutPad;
     const size_t n1 = ws.cap_s > ws.cap_n + 2 ? ws.cap_s : ws.cap_n + 2;
     const size_t ntiles = (ws.cap_n + kRadixTile - 1) / kRadixTile;
-    ws.radix_counts_elems = (size_t)kMaxDigits * ntiles + kMaxDigits;
+    // (at least 4096 words: ANSV keeps its range fills and 2 x 1024 queue counters there)
+    ws.radix_counts_elems = (size_t)kMaxDigits * ntiles + kMaxDigits < 4096 ? 4096 : (size_t)kMaxDigits * ntiles + kMaxDigits;
     ws.out_cap = out_bound(N);
     size_t scan_elems = scan_temp_elems(ws.radix_counts_elems > n1 ? ws.radix_counts_elems : n1);
     ws.scan_tmp_bytes = scan_elems * sizeof(uint64_t);
