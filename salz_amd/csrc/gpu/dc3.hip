@@ -122,18 +122,32 @@ __global__ __launch_bounds__(kT) void k_dc3_presence(const uint2 *__restrict__ t
             atomicOr(&bits[i], sb[i]);
 }
 
-// The same into a global bitmap of up to 2^kLutMaxBits bits (read before set: a bit is set by few
-// atomics), and the popcount of every word for the prefix scan.
-__global__ void k_dc3_presence_global(const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1, int b,
-                                      uint32_t *__restrict__ bits, uint32_t *__restrict__ keys)
+// The same into a global bitmap of up to 2^kLutMaxBits bits (read before set), whose words'
+// popcounts then feed the prefix scan. A grid of at most
+// kPresenceGrid workgroups loops over the sample, and each workgroup remembers the keys it set in a
+// direct-mapped LDS filter: a periodic block has few distinct triples, and every sample testing and
+// setting the same global word (one workgroup per 256 samples) serialised on it (zeros at 256 MiB:
+// 8.8 ms for one level).
+constexpr uint32_t kPresenceGrid = 2048;
+constexpr uint32_t kFilter = 2048;
+__global__ __launch_bounds__(kT) void k_dc3_presence_global(const uint2 *__restrict__ tr, uint32_t ns, uint32_t n1,
+                                                            int b, uint32_t *__restrict__ bits,
+                                                            uint32_t *__restrict__ keys)
 {
-    const size_t j = (size_t)blockIdx.x * kT + threadIdx.x;
-    if (j >= ns)
-        return;
-    const uint32_t key = triple_key(tr, (uint32_t)j, n1, b), w = key >> 5, m = 1u << (key & 31u);
-    keys[j] = key;
-    if (!(bits[w] & m))  // (a stale cached 0 only costs a redundant atomic)
-        atomicOr(&bits[w], m);
+    __shared__ uint32_t filt[kFilter];
+    for (uint32_t k = threadIdx.x; k < kFilter; k += kT)
+        filt[k] = 0xffffffffu;  // (no triple key: keys have at most kLutMaxBits bits)
+    __syncthreads();
+    for (size_t j = (size_t)blockIdx.x * kT + threadIdx.x; j < ns; j += (size_t)gridDim.x * kT) {
+        const uint32_t key = triple_key(tr, (uint32_t)j, n1, b), w = key >> 5, m = 1u << (key & 31u);
+        keys[j] = key;
+        const uint32_t h = (key * 0x9E3779B1u) >> 21;  // (kFilter = 2^11 slots)
+        if (filt[h] == key)
+            continue;  // set by this workgroup already
+        filt[h] = key;  // (racing lanes may both store; either way the bit is set below)
+        if (!(bits[w] & m))  // (a stale cached 0 only costs a redundant atomic)
+            atomicOr(&bits[w], m);
+    }
 }
 
 __global__ void k_dc3_popc(const uint32_t *__restrict__ bits, uint32_t nwords, uint32_t *__restrict__ cnt)
@@ -477,8 +491,9 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
             hipLaunchKernelGGL(k_dc3_lut_scan, dim3(1), dim3(1024), 0, st, bits, nwords, pre, d32);
             SALZ_LAUNCH_CHECK();
         } else {
-            hipLaunchKernelGGL(k_dc3_presence_global, dim3(grid_for(ns, kT)), dim3(kT), 0, st, tr, ns, n1, b, bits,
-                               tkeys);
+            hipLaunchKernelGGL(k_dc3_presence_global,
+                               dim3(grid_for(ns, kT) < kPresenceGrid ? grid_for(ns, kT) : kPresenceGrid), dim3(kT), 0,
+                               st, tr, ns, n1, b, bits, tkeys);
             SALZ_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_dc3_popc, dim3(grid_for(nwords, kT)), dim3(kT), 0, st, bits, nwords, pre);
             SALZ_LAUNCH_CHECK();

@@ -13,7 +13,7 @@ timeout -k 10 300 python bench.py --workload enwik9 --steps 2 --warmup 1 > $out/
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof_fib -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-pmc --no-e2e --workload fib256 --steps 2 --warmup 1 > $out/fib_prof.json 2> $out/fib_prof.err &&
 python tools/prof_summary.py $out/prof_fib/prof_kernel_stats.csv > $out/fib256_kernel_stats.txt &&
 timeout -k 10 300 python tools/bench_levels.py --size 50000003 > $out/levels.jsonl 2> $out/levels.err &&
-timeout -k 10 400 python tools/stress_inputs.py --size 268435456 > $out/stress256M.txt 2> $out/stress.err
+timeout -k 10 500 python tools/stress_inputs.py --size 268435456 --stages > $out/stress256M.txt 2> $out/stress.err
 rc=$?
 for f in $out/bench_*.json; do echo $f; cut -c1-300 $f; done
 exit $rc
