@@ -620,13 +620,17 @@ static int encode_core(Workspace &ws, const uint8_t *src, bool src_dev, size_t P
     // 3224 / 3191 -> 3570 / 3567 MB/s (profiles/r03zzz_c3text_klog_ab.txt), though one block alone
     // parses 0.4 ms slower than at K = 64: fewer chunks and exits cost less GPU time in total
     // while other slots keep the GPU busy.
-    // A block the suffix sort sent to DC3 (long repeats everywhere: its factors are long, so its
-    // pass count barely depends on K) parses at K = 128 as well: Fibonacci 256 MiB 5 -> 6 passes,
-    // parse 9.9 -> 7.9 ms (profiles/r04zd_klog_probe.txt; random small alphabets, which stay on
-    // prefix doubling, need twice the passes at K = 128).
+    // A block the suffix sort sent to DC3 over an alphabet of at most 4 bytes (Fibonacci, zeros,
+    // short periods: long factors everywhere, so its pass count barely depends on K) parses at
+    // K = 128 as well: Fibonacci 256 MiB parse 9.9 -> 7.9 ms (profiles/r04zd_klog_probe.txt; random
+    // small alphabets, which stay on prefix doubling, need twice the passes at K = 128). Other DC3
+    // blocks keep the size rule, wider alphabets included: their factors mix long and short, and K
+    // = 512 takes fewer passes (256 MiB, K = 128 -> 512: runs of 64 equal bytes 16 -> 13 passes,
+    // parse 26.5 -> 22.7 ms; a text repeated at distance n / 2, 6 -> 3 passes, 11.6 -> 8.1 ms; a
+    // period of 1000 or a 0..255 sawtooth 4.4 -> 5.0 ms; profiles/r06g_klog_probe.txt).
     const bool repetitive = ws.stats.sa_dc3_levels > 0;
-    if (nbz == 1 && !env_flag("SALZ_PARSE", "klog") &&
-        (((ws.sigma > 127 || repetitive) && ws.klog > 7) || (ws.klog < 7 && n > (8u << 20))))
+    const bool k128 = repetitive ? ws.sigma <= 4 : ws.sigma > 127;
+    if (nbz == 1 && !env_flag("SALZ_PARSE", "klog") && ((k128 && ws.klog > 7) || (ws.klog < 7 && n > (8u << 20))))
         ws.klog = 7;
     if (guard_check(ws, "sa") || (nbz == 1 && check_stage(ws, n, 2))) return -1;
     if (mark(ws, EV_SA)) return -1;
