@@ -82,7 +82,7 @@ __global__ void k_dc3_first_keys(const uint2 *__restrict__ tr, const uint32_t *_
     key[c] = (uint64_t)tr[dc3_pos(val[c], n1)].x << 32 | pn[c];
 }
 
-// Levels whose triples fit kLutMaxBits bits (up to 8 bits a symbol: Fibonacci's first seven
+// Levels whose triples fit kLutMaxBits bits (up to 9 bits a symbol: Fibonacci's first seven
 // levels, byte texts' first) are named without sorting: the names are the ranks of the distinct
 // triples, so a presence bitmap of the triple keys and its prefix counts give every sample its
 // name in sample order, written coalesced into the child string (no radix sort of the sample, no
@@ -91,7 +91,7 @@ __global__ void k_dc3_first_keys(const uint2 *__restrict__ tr, const uint32_t *_
 // sorting path for that order. Bitmaps of up to kLutBits bits are built in LDS per workgroup.
 constexpr int kLutBits = 18;
 constexpr uint32_t kLutWords = 1u << (kLutBits - 5);
-constexpr int kLutMaxBits = 24;
+constexpr int kLutMaxBits = 27;  // (9-bit symbols: blocks of all 256 byte values)
 
 __device__ __forceinline__ uint32_t triple_key(const uint2 *__restrict__ tr, uint32_t j, uint32_t n1, int b)
 {
