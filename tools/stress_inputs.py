@@ -32,6 +32,9 @@ cases = {
     "mixed": lambda: gen("mixed", n, 17),
 }
 ctx = salz_amd.Context(0, n)
+# one output buffer, touched once: the timed encode is H2D, encode and D2H, not the host's page
+# faults on a fresh 300 MB array or a copy into Python bytes (as bench.py's e2e step)
+obuf = np.zeros(salz_amd.encoded_len_max(n), np.uint8)
 want = [c for c in a.cases.split(",") if c]
 for name, make in cases.items():
     if want and name not in want:
@@ -39,8 +42,9 @@ for name, make in cases.items():
     src = make()
     ctx.encode(src[: 1 << 20])  # warm
     t0 = time.perf_counter()
-    out = ctx.encode(src)
+    olen = ctx.encode_into(src, obuf)
     t1 = time.perf_counter()
+    out = obuf[:olen].tobytes()
     ok = salz_amd.decode_safe(out, n, frame=True) == src.tobytes()
     st = ctx.stats()
     algo = f"dc3 {st['sa_dc3_levels']} levels" if st["sa_dc3_levels"] else f"doubling {st['sa_rounds']} rounds"
@@ -51,7 +55,7 @@ for name, make in cases.items():
         line += f"  parity {rc == 0 and ref == out}"
     if a.stages:  # (timed stages synchronise between stages: a separate encode)
         ctx.set_timing(True)
-        ctx.encode(src)
+        ctx.encode_into(src, obuf)
         ctx.set_timing(False)
         st = ctx.stats()
         line += "  |" + " ".join(f"{k[3:]} {st[k]:.1f}" for k in ("ms_upload", "ms_sa", "ms_lcp", "ms_ansv",
