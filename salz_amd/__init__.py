@@ -95,8 +95,9 @@ lib.salz_debug_init_order.restype = ctypes.c_int
 lib.salz_debug_radix_selftest.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                           ctypes.c_int]
 lib.salz_debug_radix_selftest.restype = ctypes.c_long
-lib.salz_debug_xchg_offsets.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_uint64)] * 4
-lib.salz_debug_xchg_offsets.restype = ctypes.c_int
+if hasattr(lib, "salz_debug_xchg_offsets"):  # (absent from older builds loaded for A/B runs)
+    lib.salz_debug_xchg_offsets.argtypes = [ctypes.c_int] + [ctypes.POINTER(ctypes.c_uint64)] * 4
+    lib.salz_debug_xchg_offsets.restype = ctypes.c_int
 lib.salz_encode_blocks.argtypes = [_u8p, _sz, _sz, _u8p, _szp, ctypes.c_int]
 lib.salz_encode_blocks.restype = ctypes.c_int
 lib.salz_blocks_len_max.argtypes = [_sz, _sz]
