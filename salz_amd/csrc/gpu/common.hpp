@@ -266,15 +266,6 @@ __device__ __forceinline__ uint64_t round0_key(const uint8_t *T, uint32_t i, uin
         return __builtin_bswap64(w);
     }
     uint64_t key = 0;
-    if (a.k == 8) {  // the usual text case: one load, 8 table lookups, unrolled
-        const uint64_t w = load_u64_any(T, i);
-#pragma unroll
-        for (uint32_t j = 0; j < 8; j++) {
-            const uint32_t c = j < left ? code[(w >> (8 * j)) & 255u] : 0u;
-            key = (key << a.bits) | c;
-        }
-        return key;
-    }
     for (uint32_t j0 = 0; j0 < a.k; j0 += 8) {
         const uint64_t w = load_u64_any(T, (size_t)i + j0);
         const uint32_t cnt = a.k - j0 < 8 ? a.k - j0 : 8u;
@@ -297,7 +288,7 @@ __device__ __forceinline__ uint64_t round0_key_mapped(const uint8_t *Tm, uint32_
 {
     const uint32_t left = e - i;
     uint64_t key = 0;
-    if (a.k == 8 || a.k == 9) {  // the usual text cases: straight-line, so the loads of a thread's items batch
+    if (a.k == 9) {  // the usual text case (7-bit symbols): straight-line, so the loads of a thread's items batch
         // the two aligned words holding Tm[i, i + 8): the second also holds Tm[i + 8]
         const uint64_t *wp = reinterpret_cast<const uint64_t *>(Tm + ((size_t)i & ~(size_t)7));
         const unsigned sh = (unsigned)(i & 7u) * 8u;
@@ -312,11 +303,8 @@ __device__ __forceinline__ uint64_t round0_key_mapped(const uint8_t *Tm, uint32_
         x = (x & 0x00FF00FF00FF00FFull) | (((x >> 8) & 0x00FF00FF00FF00FFull) << b);
         x = (x & 0x0000FFFF0000FFFFull) | (((x >> 16) & 0x0000FFFF0000FFFFull) << (2 * b));
         x = (x & 0xFFFFFFFFull) | ((x >> 32) << (4 * b));
-        if (a.k == 9) {  // a ninth symbol (7-bit alphabets: 63 bits), zero past the end
-            const uint32_t s9 = (uint32_t)(w1 >> sh) & 255u;  // Tm[i + 8]
-            x = (x << b) | (left > 8 ? s9 : 0u);
-        }
-        return x;
+        const uint32_t s9 = (uint32_t)(w1 >> sh) & 255u;  // the ninth symbol, Tm[i + 8], zero past the end
+        return (x << b) | (left > 8 ? s9 : 0u);
     }
     for (uint32_t j0 = 0; j0 < a.k; j0 += 8) {
         uint64_t w = load_u64_any(Tm, (size_t)i + j0);

@@ -53,7 +53,7 @@ __device__ __forceinline__ uint64_t init_key(const TextSrc &t, uint32_t i, const
 
 // Round-0 key of suffix i from 16 window bytes (w: the 8 at i, w9: the one at i + 8) for the
 // key shapes of round0_key / round0_key_mapped that the single-block text pass serves (raw
-// bytes, or 8 / 9 symbols of a mapped text).
+// bytes, or 9 symbols of 7 bits of a mapped text).
 __device__ __forceinline__ uint64_t window_key(uint64_t w, uint32_t w9, uint32_t left, const Alpha &a)
 {
     if (left < 8)
@@ -116,10 +116,10 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
                 atomicAdd(&mine[digit_of(kMode, 0, vals[base + i], shift, txt)], 1u);
         }
     } else if (kMode == 1 && shift == 0 &&
-               (txt.a.bits == 0 || ((txt.a.k == 8 || txt.a.k == 9) && txt.a.bits >= 4))) {
+               (txt.a.bits == 0 || txt.a.k == 9)) {
         // Round 0's first digit is its key's low 8 or 9 bits: the 8th byte (raw keys; 9-bit digits
-        // add the 7th byte's low bit), or the last symbol with the low bits of the one before (8
-        // or 9 symbols of >= 4 bits): two byte loads per suffix instead of the whole key. Loads
+        // add the 7th byte's low bit), or the last symbol with the low bits of the one before (9
+        // symbols of 7 bits): two byte loads per suffix instead of the whole key. Loads
         // unconditional (the text is padded), past the suffix's end masked to 0 like the key's bytes.
         const uint32_t b = txt.a.bits ? txt.a.bits : 8u, kl = txt.a.bits ? txt.a.k - 1u : 7u;
         const bool prev = txt.a.bits ? true : DB > 8;  // (the digit takes bits of the byte before)
@@ -717,7 +717,7 @@ int radix_sort_pairs(uint64_t **keys, uint32_t **vals, uint64_t *keys_alt, uint3
     const int blk_bits = blocks && g.nb > 1 ? bit_width(g.nb - 1u) : 0;
     // one block with raw-byte or 8/9-symbol keys: the text pass builds keys from an LDS window
     const bool text_win = g.nb == 1 && g.npos >= 7 &&
-                          (!alpha || alpha->bits == 0 || alpha->k == 8 || alpha->k == 9);
+                          (!alpha || alpha->bits == 0 || alpha->k == 9);
     // 9-bit digits: key passes of 512 threads only (the generic text pass of a batch and the
     // materialised round-0 list's byte digits keep 8 bits)
     int width[64];
