@@ -1835,7 +1835,9 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         //           (scatter_staged, XCD-aware), for rank arrays far past the cache.
         // Default: up to 512 MB of ranks split from 32M updates, above it stage from 4M, 1 MB
         // windows (Fibonacci 256 MiB: SA 554 -> 505 ms; text 100 MB: SA 24.8 ms split, 25.3
-        // staged; profiles/r02l_*).
+        // staged; profiles/r02l_*). With round 6's LDS-ordered staging tiles C2's rounds after
+        // the text round staged come out even with the split (3765 / 3765 against 3785 / 3752 MB/s
+        // on one box, profiles/r06t_staged_scatter_ab.txt).
         int mode = (uint64_t)n * 4 <= (512ull << 20) ? (m >= (32u << 20) ? 1 : 0) : (m >= (4u << 20) ? 2 : 0);
         // round 0 before the text round writes only the ranks of the suffixes it finishes
         const bool textnext = round0 && text1;

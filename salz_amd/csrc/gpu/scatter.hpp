@@ -3,12 +3,19 @@
 // arrays).
 //
 // A direct scatter of m random 4-byte writes into a 1-2 GB array pays a full HBM line per
-// write. Here k_sc_stage bins the (index, value) pairs by destination window (2^rlog words,
-// one LDS count per window and tile, one global atomic per window and tile) into per-window
-// runs, and k_sc_apply writes the runs window by window, XCD-aware (workgroup g runs on XCD
-// g mod 8, so XCD x takes windows x, x + 8, ...): the writes in flight on one XCD fall in one
-// L2-sized window. Every window receives at most 2^rlog pairs (each index at most once), so
-// the runs sit at fixed offsets (window << rlog) of the staging buffer.
+// write. Here k_sc_stage bins the (index, value) pairs by destination window (2^rlog words)
+// into per-window runs, and k_sc_apply writes the runs window by window, XCD-aware (workgroup g
+// runs on XCD g mod 8, so XCD x takes windows x, x + 8, ...): the writes in flight on one XCD
+// fall in one L2-sized window. Every window receives at most 2^rlog pairs (each index at most
+// once), so the runs sit at fixed offsets (window << rlog) of the staging buffer.
+//
+// A staging tile is 8192 pairs (1024 threads, 72 KB of LDS: two workgroups per CU), ordered by
+// window in LDS before it leaves: its run for a window (8 pairs on average over 1024 windows) is
+// written as one contiguous 64-byte piece, and each window's counter takes one atomic per tile.
+// 4096-pair tiles written straight from registers took one device atomic per window and tile
+// (~66 M for a 2^28-pair scatter) and wrote 32-byte pieces: Phi at 256 MiB 2.69 -> 1.63 ms at
+// 16384-pair tiles; C5 3139 / 3112 -> 3298 / 3284 MB/s (16384) and 3312 / 3307 (8192) on one box,
+// profiles/r06t_staged_scatter_ab.txt.
 #pragma once
 
 #include "internal.hpp"
@@ -18,44 +25,67 @@
 namespace salz {
 namespace {  // kernels instantiated per translation unit
 
-constexpr uint32_t kScTile = 4096;
-constexpr uint32_t kScThreads = 256;
+constexpr uint32_t kScThreads = 256;   // k_sc_apply
 constexpr uint32_t kScWindows = 1024;
+constexpr uint32_t kStThreads = 1024;  // k_sc_stage: one thread per window
+constexpr uint32_t kStItems = 8;
+constexpr uint32_t kStTile = kStThreads * kStItems;
 
 // Src: __device__ bool operator()(size_t c, uint32_t &index, uint32_t &value) const
 template <class Src>
-__global__ __launch_bounds__(kScThreads) void k_sc_stage(Src src, uint32_t m, uint32_t rlog,
+__global__ __launch_bounds__(kStThreads) void k_sc_stage(Src src, uint32_t m, uint32_t rlog,
                                                          uint32_t *__restrict__ rfill, uint2 *__restrict__ stage)
 {
-    __shared__ uint32_t cnt[kScWindows];
-    constexpr uint32_t kItems = kScTile / kScThreads;
+    __shared__ uint2 buf[kStTile];
+    __shared__ uint32_t cnt[kScWindows];  // pairs per window, then the window's offset in buf
+    __shared__ uint32_t delta[kScWindows];  // stage slot - buf offset (mod 2^32)
+    __shared__ uint32_t wsum[kStThreads / 64];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t r = tid; r < kScWindows; r += kScThreads)
-        cnt[r] = 0;
+    cnt[tid] = 0;
     __syncthreads();
-    const size_t base = (size_t)blockIdx.x * kScTile;
-    uint32_t iv[kItems], vv[kItems], loc[kItems];
-    bool ok[kItems];
+    const size_t base = (size_t)blockIdx.x * kStTile;
+    uint32_t iv[kStItems], vv[kStItems], loc[kStItems];
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; j++) {
-        const size_t c = base + (size_t)j * kScThreads + tid;
-        ok[j] = src(c < m ? c : 0, iv[j], vv[j]) && c < m;  // loads unconditional (clamped)
+    for (uint32_t j = 0; j < kStItems; j++) {
+        const size_t c = base + (size_t)j * kStThreads + tid;
+        const bool ok = src(c < m ? c : 0, iv[j], vv[j]) && c < m;  // loads unconditional (clamped)
+        loc[j] = ok ? atomicAdd(&cnt[iv[j] >> rlog], 1u) : 0xffffffffu;
     }
-#pragma unroll
-    for (uint32_t j = 0; j < kItems; j++)
-        loc[j] = ok[j] ? atomicAdd(&cnt[iv[j] >> rlog], 1u) : 0u;
     __syncthreads();
-    for (uint32_t r = tid; r < kScWindows; r += kScThreads)
-        if (cnt[r])
-            cnt[r] = (r << rlog) + atomicAdd(&rfill[r], cnt[r]);
+    // exclusive scan of the window counts (thread = window), then one atomic per used window
+    const uint32_t c = cnt[tid], lane = tid & 63u, wv = tid >> 6;
+    uint32_t x = c;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = shfl_up_u32(x, d);
+        x += lane >= d ? y : 0u;
+    }
+    if (lane == 63u)
+        wsum[wv] = x;
+    __syncthreads();
+    uint32_t off = x - c, total = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kStThreads / 64; w++) {
+        off += w < wv ? wsum[w] : 0u;
+        total += wsum[w];
+    }
+    cnt[tid] = off;
+    delta[tid] = c ? (tid << rlog) + atomicAdd(&rfill[tid], c) - off : 0u;
     __syncthreads();
 #pragma unroll
-    for (uint32_t j = 0; j < kItems; j++)
-        if (ok[j])
-            stage[cnt[iv[j] >> rlog] + loc[j]] = make_uint2(iv[j], vv[j]);
+    for (uint32_t j = 0; j < kStItems; j++)
+        if (loc[j] != 0xffffffffu)
+            buf[cnt[iv[j] >> rlog] + loc[j]] = make_uint2(iv[j], vv[j]);
+    __syncthreads();
+    for (uint32_t s = tid; s < total; s += kStThreads) {
+        const uint2 e = buf[s];
+        stage[delta[e.x >> rlog] + s] = e;
+    }
 }
 
-// dst[index * stride + field] = value, window by window
+// dst[index * stride + field] = value, window by window (one pair per thread: with 8 per thread,
+// two windows were in flight per XCD and their dirty lines shared its L2, apply 7.7 -> 11.2 ms
+// on the 256 MiB halves block)
 __global__ __launch_bounds__(kScThreads) void k_sc_apply(const uint2 *__restrict__ stage,
                                                          const uint32_t *__restrict__ rfill, uint32_t rlog,
                                                          uint32_t nwin, uint32_t *__restrict__ dst,
@@ -90,7 +120,7 @@ int scatter_staged(Src src, uint32_t m, uint32_t nidx, uint32_t *dst, uint32_t s
         return -1;
     }
     SALZ_HIP(fill_async(rfill, 0, nwin * sizeof(uint32_t), st));
-    hipLaunchKernelGGL(k_sc_stage<Src>, dim3(grid_for(m, kScTile)), dim3(kScThreads), 0, st, src, m, rlog, rfill,
+    hipLaunchKernelGGL(k_sc_stage<Src>, dim3(grid_for(m, kStTile)), dim3(kStThreads), 0, st, src, m, rlog, rfill,
                        stage);
     SALZ_LAUNCH_CHECK();
     const uint32_t agrid = 8u * ((nwin + 7u) / 8u) << (rlog - 8);

@@ -344,6 +344,27 @@ def test_dc3_large_blocks_match_oracle(ctx, monkeypatch, kind, n):
     assert rc == 0 and out == ref
 
 
+def test_dc3_presence_27bit_level(salz, monkeypatch):
+    """A 64 MiB block of runs over all 256 byte values: DC3 level 0 has 9-bit symbols, so its
+    triples are 27-bit keys, named from the 2^27-bit presence bitmap (dc3.hip kLutMaxBits; the
+    block's radix counts, 512 words a tile, hold the bitmap and its prefix from 2^26 bytes up),
+    and the stream equals the oracle's."""
+    monkeypatch.setenv("SALZ_SA", "dc3")
+    rng = np.random.default_rng(27)
+    n = (64 << 20) + 1001
+    k = n // 40 + 2
+    src = np.repeat(rng.integers(0, 256, k).astype(np.uint8), rng.integers(20, 61, k))[:n]
+    assert len(np.unique(src)) == 256
+    big = salz.Context(0, n)
+    try:
+        out = big.encode(src)
+        assert big.stats()["sa_dc3_levels"] > 0
+    finally:
+        big.close()
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and out == ref
+
+
 def test_dc3_edge_sizes(ctx, monkeypatch):
     """DC3 at every suffix count 1..200 (each n mod 3, the dummy sample, one-level and
     recursing strings) and around powers of two."""
