@@ -606,9 +606,11 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
                                 sizeof(uint32_t) * (nblocks - used_blocks), st));
     }
     // Staging: text ranges of 2^rlog positions (cand windows of 16 << rlog bytes; 16 MB by
-    // default: 2^19 and 2^21 measured slower), at most kMaxRanges of them. Slots sp / stage
-    // alias scratch that is free here.
-    uint32_t rlog = 20;
+    // default: 2^19 and 2^21 measured slower on C2), at most kMaxRanges of them. Slots sp / stage
+    // alias scratch that is free here. Past 2^27 positions (unpacked staging) 2^21: half the
+    // range reservations, one global atomic per range and workgroup (C5 ANSV 11.83 -> 11.56 ms,
+    // three of three on one box, profiles/r06u_ansv_ranges_ab.txt).
+    uint32_t rlog = npos > (1u << 27) ? 21 : 20;
     while ((((uint64_t)npos - 1) >> rlog) + 1 > kMaxRanges)
         rlog++;
     uint32_t *rfill = ws.radix_counts;
