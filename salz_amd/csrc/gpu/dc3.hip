@@ -621,6 +621,28 @@ static size_t dc3_arena_bytes(uint32_t n)
     return bytes + 4096;
 }
 
+uint8_t *dc3_arena_reserve(Workspace &ws, size_t need)
+{
+    if (ws.dc3_bytes < need) {
+        if (ws.dc3 && hipFree(ws.dc3) != hipSuccess) {
+            set_error("dc3: hipFree of the arena failed");
+            return nullptr;
+        }
+        ws.bytes -= ws.dc3_bytes;
+        ws.dc3 = nullptr;
+        ws.dc3_bytes = 0;
+        void *p = nullptr;
+        if (hipMalloc(&p, need) != hipSuccess) {
+            set_error("dc3: hipMalloc of %zu bytes failed", need);
+            return nullptr;
+        }
+        ws.dc3 = static_cast<uint8_t *>(p);
+        ws.dc3_bytes = need;
+        ws.bytes += need;
+    }
+    return ws.dc3;
+}
+
 int stage_suffix_array_dc3(Workspace &ws, const Blocks &bl, const Alpha &codes, int raw)
 {
     hipStream_t st = ws.stream;
@@ -629,19 +651,8 @@ int stage_suffix_array_dc3(Workspace &ws, const Blocks &bl, const Alpha &codes, 
         set_error("dc3: one block per pass only");
         return -1;
     }
-    const size_t need = dc3_arena_bytes(n);
-    if (ws.dc3_bytes < need) {
-        if (ws.dc3)
-            SALZ_HIP(hipFree(ws.dc3));
-        ws.bytes -= ws.dc3_bytes;
-        ws.dc3 = nullptr;
-        ws.dc3_bytes = 0;
-        void *p = nullptr;
-        SALZ_HIP(hipMalloc(&p, need));
-        ws.dc3 = static_cast<uint8_t *>(p);
-        ws.dc3_bytes = need;
-        ws.bytes += need;
-    }
+    if (!dc3_arena_reserve(ws, dc3_arena_bytes(n)))
+        return -1;
     uint32_t *derr = reinterpret_cast<uint32_t *>(ws.dscal) + kErrWord;
     Dc3 d{ws, st, ws.dc3, ws.dc3 + ws.dc3_bytes, derr};
     uint2 *tr = arena_take<uint2>(d, (size_t)n + 8);

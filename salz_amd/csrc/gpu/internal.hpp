@@ -225,13 +225,15 @@ int dist_suffix_array_comm(Workspace &ws, uint32_t n, DistComm *c, uint32_t *xse
 int dist_idle_rounds(Workspace &ws, const DistSa &d, int round);
 // The round-0 alphabet's symbol width (0: raw bytes), as stage_suffix_array computes it (sa.hip).
 int block_alpha_bits(Workspace &ws, uint32_t n);
-// 1 when the repetition probe (sa.hip) would send this single block of n suffixes to DC3 (blocks
-// of at least 2^20 suffixes), 0 otherwise, -1 on failure.
+// 1 when the repetition probe (sa.hip) finds this single block of n suffixes repetitive (blocks
+// of at least 2^20 suffixes: DC3, or doubling with twin pairs), 0 otherwise, -1 on failure.
 int block_repetitive(Workspace &ws, uint32_t n);
 int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist = nullptr);  // sa.hip -> ws.sa
 // dc3.hip -> ws.sa for one block (repetitive inputs); symbols = codes.code[byte] (1..sigma) or
 // byte + 1 when raw
 int stage_suffix_array_dc3(Workspace &ws, const Blocks &bl, const Alpha &codes, int raw);
+// dc3.hip: the DC3 arena grown to at least `bytes` (the twin-pair table of sa.hip borrows it)
+uint8_t *dc3_arena_reserve(Workspace &ws, size_t bytes);
 int stage_lcp(Workspace &ws, const Blocks &bl, uint32_t *lcp_out); // lcp.hip  -> lcp[r]
 int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp);  // ansv.hip -> ws.cand
 int stage_parse(Workspace &ws, const Blocks &bl);                  // parse.hip

@@ -171,7 +171,8 @@ __device__ __forceinline__ uint32_t gram_tag(uint64_t h) { return (((uint32_t)(h
 __global__ __launch_bounds__(kProbeThreads) void k_repeat_probe(const uint8_t *__restrict__ T, uint32_t n,
                                                                 uint32_t *__restrict__ out, uint32_t *__restrict__ ptab,
                                                                 uint32_t *__restrict__ pmul, uint32_t *__restrict__ gcnt,
-                                                                uint32_t *__restrict__ pfilt, uint32_t *__restrict__ pslot)
+                                                                uint32_t *__restrict__ pfilt, uint32_t *__restrict__ pslot,
+                                                                uint32_t *__restrict__ hpos)
 {
     __shared__ uint32_t key[kProbeSlots];
     __shared__ uint32_t cnt[kProbeSlots];
@@ -223,6 +224,8 @@ __global__ __launch_bounds__(kProbeThreads) void k_repeat_probe(const uint8_t *_
             ptab[i] = key[i];
             pmul[i] = cnt[i];
             gcnt[i] = 0u;
+            hpos[i] = 0xffffffffu;  // lowest and highest aligned hit (k_repeat_scan)
+            hpos[kProbeSlots + i] = 0u;
         }
     }
     if (ptab)
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(kScanThreads) void k_repeat_scan(const uint8_t *__r
                                                               const uint32_t *__restrict__ dups,
                                                               const uint32_t *__restrict__ ptab,
                                                               const uint32_t *__restrict__ pfilt,
-                                                              uint32_t *__restrict__ gcnt)
+                                                              uint32_t *__restrict__ gcnt, uint32_t *__restrict__ hpos)
 {
     __shared__ uint32_t tab[kProbeSlots];  // tag | hits in this workgroup (2 bits, saturating)
     __shared__ uint32_t filt[kFilterBits / 32];
@@ -283,8 +286,20 @@ __global__ __launch_bounds__(kScanThreads) void k_repeat_scan(const uint8_t *__r
                 if (e == 0u)
                     break;
                 if ((e & ~3u) == tag) {  // bit 0: hit once, bit 1: hit twice (or-ed, so never past 3)
-                    if (!(e & 2u) && (atomicOr(&tab[slot], 1u) & 1u))
-                        atomicOr(&tab[slot], 2u);
+                    // the first two hits per workgroup also leave their positions (lowest and
+                    // highest over the grid): a gram with one aligned copy besides its own has
+                    // both recorded, for the twin distance (k_repeat_count)
+                    bool rec = false;
+                    if (!(e & 2u)) {
+                        rec = !(atomicOr(&tab[slot], 1u) & 1u);
+                        if (!rec)
+                            rec = !(atomicOr(&tab[slot], 2u) & 2u);
+                    }
+                    if (rec) {
+                        const uint32_t p = (uint32_t)(g * 8 + j) * 8u;
+                        atomicMin(&hpos[slot], p);
+                        atomicMax(&hpos[kProbeSlots + slot], p);
+                    }
                     break;
                 }
                 slot = (slot + 1u) & (kProbeSlots - 1u);
@@ -300,29 +315,55 @@ __global__ __launch_bounds__(kScanThreads) void k_repeat_scan(const uint8_t *__r
 }
 
 // out[0]: the sample points (of kProbePoints) one of whose grams occurs at an aligned position
-// other than its own, or is shared with another sample.
+// other than its own, or is shared with another sample. out[1], out[2]: the twin distance d most
+// points share and how many do. A point's twin distance is that of its first gram that no other
+// sample shares and that has exactly one aligned copy besides its own (a block holding a text
+// twice, at distance d: every point but those in the text's own repeats).
 __global__ __launch_bounds__(kProbePoints) void k_repeat_count(const uint32_t *__restrict__ dups,
                                                                const uint32_t *__restrict__ pmul,
                                                                const uint32_t *__restrict__ gcnt,
                                                                const uint32_t *__restrict__ pslot,
+                                                               const uint32_t *__restrict__ hpos, uint32_t n,
                                                                uint32_t *__restrict__ out)
 {
     __shared__ uint32_t tot;
-    if (threadIdx.x == 0)
+    __shared__ uint32_t dist[kProbePoints];
+    __shared__ unsigned long long best;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) {
         tot = 0;
-    __syncthreads();
+        best = 0;
+    }
     bool rep = false;
+    uint32_t dd = 0;
     if (dups[0] * 2u < kProbe)
         for (uint32_t i = 0; i < 8; i++) {
-            const uint32_t e = pslot[threadIdx.x * 8u + i], sl = e >> 1;
-            rep = rep || pmul[sl] >= 2u || gcnt[sl] >= 1u + (e & 1u);
+            const uint32_t e = pslot[t * 8u + i], sl = e >> 1, own = e & 1u;
+            rep = rep || pmul[sl] >= 2u || gcnt[sl] >= 1u + own;
+            if (!dd && pmul[sl] == 1u && gcnt[sl] == 1u + own) {
+                const uint32_t q = (uint32_t)((size_t)t * (n - 40u) / kProbePoints) + i;
+                const uint32_t lo = hpos[sl], hi = hpos[kProbeSlots + sl];
+                const uint32_t other = own && lo == q ? hi : lo;
+                dd = other > q ? other - q : q - other;
+            }
         }
+    dist[t] = dd;
+    __syncthreads();
     const uint64_t b = wave_ballot(rep);
     if (lane_id() == 0)
         atomicAdd(&tot, (uint32_t)__popcll(b));
+    if (dd) {
+        uint32_t same = 0;
+        for (uint32_t u = 0; u < kProbePoints; u++)
+            same += dist[u] == dd ? 1u : 0u;
+        atomicMax(&best, (unsigned long long)same << 32 | dd);
+    }
     __syncthreads();
-    if (threadIdx.x == 0)
-        *out = tot;
+    if (t == 0) {
+        out[0] = tot;
+        out[1] = (uint32_t)best;
+        out[2] = (uint32_t)(best >> 32);
+    }
 }
 
 // Group-head flags travel as one 64-bit ballot per wave of the sorted list (hmask) plus its
@@ -528,10 +569,13 @@ constexpr uint32_t kLcpLane = 32;
 constexpr uint32_t kLcpMaxHk = 4096;
 
 // k_heads with the LCP of every new head (writes the head ballots like k_heads).
+// Twin mode (tw, twd: k_twin_pairs): a twin pair {x, x + d} that splits on the ranks of a twin pair
+// resolved earlier shares far more than 2 hk symbols; its LCP is read from the twin table.
 __global__ __launch_bounds__(kT) void k_heads_lcp(
     const uint64_t *__restrict__ K, const uint32_t *__restrict__ V, HeadBits hb,
     const uint32_t *__restrict__ off_old, uint32_t m, Blocks bl, Alpha a, int kb_old, uint32_t hk, int round0,
-    const uint8_t *__restrict__ T, uint32_t *__restrict__ lcps, uint32_t *err)
+    const uint8_t *__restrict__ T, uint32_t *__restrict__ lcps, uint32_t *err, const uint32_t *__restrict__ tw,
+    uint32_t twd)
 {
     const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
     const bool in = c < m;
@@ -567,7 +611,10 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
                 // (the keys differ, so the suffixes differ within hk bytes; lim bounds the
                 // compare by the end of the text)
                 lim = e1 - mx - hk;
-                if (hk <= kLcpLane) {
+                if (tw && mx - (i < j ? i : j) == twd) {
+                    const uint32_t x = i < j ? i : j;
+                    lcps[pos] = (tw[x] >> 1) - x;
+                } else if (hk <= kLcpLane) {
                     uint32_t l = lim;
                     for (uint32_t off = 0; off < lim; off += 8) {
                         const uint64_t x = load_u64_any(T, (size_t)i + hk + off) ^
@@ -620,6 +667,155 @@ __global__ __launch_bounds__(kT) void k_heads_lcp(
         }
         if (have && sl8 == 0)
             lcps[sp] = hk + umin_(mis, sl);
+    }
+}
+
+// Twin pairs. A block that holds a text twice at distance d (the probe's twin distance) keeps
+// every suffix x and its twin x + d in one group for ~log2(n / 2) rounds: their order and LCP are
+// decided only by the first mismatch on diagonal d, j = min{j >= x : T[j] != T[j + d] or j + d = n},
+// and the twin ends first when j + d = n (it is then a prefix of x's suffix). TW[x] = j << 1 | (x
+// first) for x <= L = n - d, a suffix minimum of g[j] = that value at the mismatches and ~0
+// elsewhere: per tile of kTwTile positions (k_twin_tiles), across tiles (k_twin_carry), then per
+// position (k_twin_fill). Every round then splits the two-member groups {x, x + d} at once
+// (k_twin_pairs), so the rounds carry what a text without its copy would.
+constexpr uint32_t kTwItems = 16;
+constexpr uint32_t kTwTile = kT * kTwItems;
+
+__device__ __forceinline__ uint32_t twin_g(const uint8_t *__restrict__ T, uint32_t j, uint32_t d, uint32_t L)
+{
+    if (j > L)
+        return 0xffffffffu;
+    if (j == L)
+        return j << 1;  // the twin ends: it sorts first
+    const uint8_t a = T[j], b = T[j + d];
+    return a != b ? (j << 1) | (a < b ? 1u : 0u) : 0xffffffffu;
+}
+
+// per thread: the suffix minimum over its kTwItems positions (written back into v)
+__device__ __forceinline__ uint32_t twin_thread(const uint8_t *__restrict__ T, uint32_t x0, uint32_t d, uint32_t L,
+                                                uint32_t *v)
+{
+    uint32_t mn = 0xffffffffu;
+#pragma unroll
+    for (int k = (int)kTwItems - 1; k >= 0; k--) {
+        mn = umin_(mn, twin_g(T, x0 + (uint32_t)k, d, L));
+        v[k] = mn;
+    }
+    return mn;
+}
+
+__global__ __launch_bounds__(kT) void k_twin_tiles(const uint8_t *__restrict__ T, uint32_t d, uint32_t L,
+                                                   uint32_t *__restrict__ tmin)
+{
+    __shared__ uint32_t wm[kT / 64];
+    uint32_t v[kTwItems];
+    const uint32_t x0 = blockIdx.x * kTwTile + threadIdx.x * kTwItems;
+    const uint32_t mn = wave_min_u32(twin_thread(T, x0, d, L, v));
+    if (lane_id() == 0)
+        wm[threadIdx.x >> 6] = mn;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        tmin[blockIdx.x] = umin_(umin_(wm[0], wm[1]), umin_(wm[2], wm[3]));
+}
+
+// tmin[t] := the minimum over the tiles after t (one workgroup: a segment of tiles per thread)
+constexpr uint32_t kTwCarryT = 1024;
+__global__ __launch_bounds__(kTwCarryT) void k_twin_carry(uint32_t *__restrict__ tmin, uint32_t ntiles)
+{
+    __shared__ uint32_t seg[kTwCarryT];
+    const uint32_t t = threadIdx.x, per = (ntiles + kTwCarryT - 1) / kTwCarryT;
+    const uint32_t lo = t * per, hi = umin_(lo + per, ntiles);
+    uint32_t mn = 0xffffffffu;
+    for (uint32_t k = lo; k < hi; k++)
+        mn = umin_(mn, tmin[k]);
+    seg[t] = mn;
+    __syncthreads();
+    for (uint32_t s = 1; s < kTwCarryT; s <<= 1) {  // suffix minima of the segments
+        const uint32_t o = t + s < kTwCarryT ? seg[t + s] : 0xffffffffu;
+        __syncthreads();
+        seg[t] = umin_(seg[t], o);
+        __syncthreads();
+    }
+    uint32_t after = t + 1 < kTwCarryT ? seg[t + 1] : 0xffffffffu;
+    for (uint32_t k = hi; k > lo; k--) {
+        const uint32_t x = tmin[k - 1];
+        tmin[k - 1] = after;
+        after = umin_(after, x);
+    }
+}
+
+__global__ __launch_bounds__(kT) void k_twin_fill(const uint8_t *__restrict__ T, uint32_t d, uint32_t L,
+                                                  const uint32_t *__restrict__ tafter, uint32_t *__restrict__ tw)
+{
+    __shared__ uint32_t sm[kT];
+    uint32_t v[kTwItems];
+    const uint32_t tid = threadIdx.x, x0 = blockIdx.x * kTwTile + tid * kTwItems;
+    sm[tid] = twin_thread(T, x0, d, L, v);
+    __syncthreads();
+    for (uint32_t s = 1; s < kT; s <<= 1) {  // suffix minima of the threads' minima
+        const uint32_t o = tid + s < kT ? sm[tid + s] : 0xffffffffu;
+        __syncthreads();
+        sm[tid] = umin_(sm[tid], o);
+        __syncthreads();
+    }
+    const uint32_t after = umin_(tid + 1 < kT ? sm[tid + 1] : 0xffffffffu, tafter[blockIdx.x]);
+#pragma unroll
+    for (uint32_t k = 0; k < kTwItems; k++)
+        if (x0 + k <= L)
+            tw[x0 + k] = umin_(v[k], after);
+}
+
+// Two-member groups {x, x + d} of the sorted list in order, split into singletons: a wave per
+// 64-entry word of the head ballots (the heads of the word and the two after it are read before
+// any is set; a pair's second entry, the new head, is followed by a head, so no other wave's pair
+// test depends on it). With the sort's LCPs, the new head's LCP is j - x.
+__global__ __launch_bounds__(kT) void k_twin_pairs(uint32_t *__restrict__ V, const uint64_t *__restrict__ K,
+                                                   const uint32_t *__restrict__ gin, const uint32_t *__restrict__ off_old,
+                                                   int kb_old, int round0, HeadBits hb, uint32_t m, uint32_t d,
+                                                   const uint32_t *__restrict__ tw, uint32_t *__restrict__ lcps)
+{
+    const size_t c = (size_t)blockIdx.x * kT + threadIdx.x;
+    const size_t w = c >> 6, nw = ((size_t)m + 63) / 64;
+    if (w >= nw)
+        return;  // whole wave
+    const uint32_t lane = (uint32_t)(c & 63u);
+    const uint64_t h = hb.hmask[w], hn = w + 1 < nw ? hb.hmask[w + 1] : 0ull;
+    auto head = [&](size_t e) {
+        if (e >= m)
+            return true;
+        const uint64_t wd = (e >> 6) == w ? h : hn;
+        return ((wd >> (e & 63u)) & 1ull) != 0;
+    };
+    bool done = false;
+    uint32_t lcp = 0;
+    if (c + 1 < m && head(c) && !head(c + 1) && head(c + 2)) {
+        const uint32_t a = V[c], b = V[c + 1];
+        if ((a > b ? a - b : b - a) == d) {
+            const uint32_t x = a < b ? a : b, v = tw[x];
+            const uint32_t first = (v & 1u) ? x : x + d;
+            if (a != first) {
+                V[c] = first;
+                V[c + 1] = a;
+            }
+            lcp = (v >> 1) - x;
+            done = true;
+        }
+    }
+    const uint64_t nb = wave_ballot(done);
+    if (lane == 0 && nb) {
+        const uint64_t in = nb << 1;  // the new heads at c + 1
+        if (in) {
+            atomicOr(reinterpret_cast<unsigned long long *>(&hb.hmask[w]), (unsigned long long)in);
+            atomicAdd(&hb.wcnt[w], (uint32_t)__popcll(in));
+        }
+        if (nb >> 63) {
+            atomicOr(reinterpret_cast<unsigned long long *>(&hb.hmask[w + 1]), 1ull);
+            atomicAdd(&hb.wcnt[w + 1], 1u);
+        }
+    }
+    if (lcps && done) {
+        const uint32_t o = round0 ? 0u : off_old[gin ? gin[c] : (uint32_t)(K[c] >> kb_old)];
+        lcps[(uint32_t)c + o + 1u] = lcp;
     }
 }
 
@@ -1387,21 +1583,23 @@ __global__ void k_putback_text(const uint64_t *__restrict__ KS, const uint32_t *
 }  // namespace
 
 // The repetition probe's three launches (k_repeat_probe, k_repeat_scan, k_repeat_count) over the
-// block's n suffixes (n >= 64): results in the u32 words 248 (samples sharing a fingerprint) and
-// 249 (repeated points) of dscal, read back by the caller; scratch in u1.
+// block's n suffixes (n >= 64): results in the u32 words 248 (samples sharing a fingerprint), 249
+// (repeated points), 250 (twin distance) and 251 (its points) of dscal, read back by the caller;
+// scratch in u1.
 static void launch_repeat_probe(Workspace &ws, uint32_t n)
 {
     hipStream_t st = ws.stream;
     uint32_t *words = reinterpret_cast<uint32_t *>(ws.dscal) + 240;
     uint32_t *ptab = ws.u1, *pmul = ws.u1 + kProbeSlots, *gcnt = ws.u1 + 2 * kProbeSlots;
-    uint32_t *pfilt = ws.u1 + 3 * kProbeSlots, *pslot = pfilt + kFilterBits / 32;
+    uint32_t *pfilt = ws.u1 + 3 * kProbeSlots, *pslot = pfilt + kFilterBits / 32, *hpos = pslot + kProbe;
     hipLaunchKernelGGL(k_repeat_probe, dim3(1), dim3(kProbeThreads), 0, st, ws.text, n, words + 8, ptab, pmul, gcnt,
-                       pfilt, pslot);
+                       pfilt, pslot, hpos);
     const uint32_t groups = (n - 32u) / 64u + 1u;  // 8 aligned grams per thread
     const uint32_t grid = grid_for(groups, kScanThreads) < 1024 ? grid_for(groups, kScanThreads) : 1024;
     hipLaunchKernelGGL(k_repeat_scan, dim3(grid), dim3(kScanThreads), 0, st, ws.text, n, words + 8, ptab, pfilt,
-                       gcnt);
-    hipLaunchKernelGGL(k_repeat_count, dim3(1), dim3(kProbePoints), 0, st, words + 8, pmul, gcnt, pslot, words + 9);
+                       gcnt, hpos);
+    hipLaunchKernelGGL(k_repeat_count, dim3(1), dim3(kProbePoints), 0, st, words + 8, pmul, gcnt, pslot, hpos, n,
+                       words + 9);
 }
 
 // The probe's verdict from the words read back (hs: ws.hscal as u32): half the samples repeated
@@ -1486,6 +1684,7 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     const bool dc3_force = env_flag("SALZ_SA", "dc3") && bl.nb == 1 && n >= 2 && !dist;
     const bool dc3_auto = !env_flag("SALZ_SA", "doubling") && bl.nb == 1 && n >= (1u << 20) && !dist;
     bool dc3_now = false;
+    uint32_t twin_d = 0;  // twin distance (k_twin_pairs), 0: none
     Alpha codes{};  // the block's byte codes 1..sigma for DC3 (raw bytes + 1 when not known)
     int codes_raw = 1;
     if (n >= 64) {
@@ -1501,8 +1700,14 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
         }
         if (read_scalars(ws, 960, 48, "sa.alpha") != 0)
             return -1;
-        // the probe's verdict: DC3 from the start
-        dc3_now = dc3_auto && probe_repetitive(reinterpret_cast<const uint32_t *>(ws.hscal));
+        // the probe's verdict: DC3 from the start, or doubling with twin pairs when three quarters
+        // of the sample points have one copy at the same distance
+        const uint32_t *hs = reinterpret_cast<const uint32_t *>(ws.hscal);
+        dc3_now = dc3_auto && probe_repetitive(hs);
+        if (dc3_now && (uint64_t)hs[251] * 4 >= 3ull * kProbePoints && hs[250] > 0 && hs[250] < n) {
+            twin_d = hs[250];
+            dc3_now = false;
+        }
         const uint32_t *pw = reinterpret_cast<const uint32_t *>(ws.hscal) + 240;
         uint32_t sigma = 0;
         for (int c = 0; c < 256; c++)
@@ -1527,6 +1732,25 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
     }
     if (dc3_force || dc3_now)
         return stage_suffix_array_dc3(ws, bl, codes, codes_raw);
+    // the twin table (L + 1 entries) and its tile carries, in the DC3 arena
+    uint32_t *twin = nullptr;
+    if (twin_d) {
+        const uint32_t L = n - twin_d, ntw = (L + kTwTile) / kTwTile;  // tiles over [0, L]
+        uint8_t *ar = dc3_arena_reserve(ws, ((size_t)L + 1 + ntw) * sizeof(uint32_t) + 256);
+        if (!ar)
+            return -1;
+        twin = reinterpret_cast<uint32_t *>(ar);
+        uint32_t *tmin = twin + L + 1;
+        hipLaunchKernelGGL(k_twin_tiles, dim3(ntw), dim3(kT), 0, st, ws.text, twin_d, L, tmin);
+        SALZ_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_twin_carry, dim3(1), dim3(kTwCarryT), 0, st, tmin, ntw);
+        SALZ_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_twin_fill, dim3(ntw), dim3(kT), 0, st, ws.text, twin_d, L, tmin, twin);
+        SALZ_LAUNCH_CHECK();
+        if (env_flag("SALZ_DEBUG", "sa"))
+            fprintf(stderr, "sa twin pairs at distance %u (%u of %u probe points)\n", twin_d,
+                    reinterpret_cast<const uint32_t *>(ws.hscal)[251], kProbePoints);
+    }
     const uint32_t h0 = alpha.bits ? alpha.k : 8u;
     // The text mapped to symbols for the text-sourced radix pass and the text round's keys (u3
     // is free until round 0's commit writes the group ids, which go to `gin` before a text
@@ -1793,11 +2017,17 @@ int stage_suffix_array(Workspace &ws, const Blocks &bl, const DistSa *dist)
                                h / 2, ws.lcps_ok ? ws.lcps : nullptr);
         else if (ws.lcps_ok)
             hipLaunchKernelGGL(k_heads_lcp, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, hb, offo, m, bl,
-                               alpha, kb_old, round0 ? 0u : h / 2, round0, ws.text, ws.lcps, derr);
+                               alpha, kb_old, round0 ? 0u : h / 2, round0, ws.text, ws.lcps, derr, twin, twin_d);
         else
             hipLaunchKernelGGL(k_heads, dim3(grid_for(m, kT)), dim3(kT), 0, st, K, V, m, bl, h0, round0,
                                hb);
         SALZ_LAUNCH_CHECK();
+        if (twin) {
+            hipLaunchKernelGGL(k_twin_pairs, dim3(grid_for(((size_t)m + 63) / 64 * 64, kT)), dim3(kT), 0, st, V, K,
+                               textr ? gin : nullptr, offo, kb_old, round0, hb, m, twin_d, twin,
+                               ws.lcps_ok ? ws.lcps : nullptr);
+            SALZ_LAUNCH_CHECK();
+        }
         if (scan_sum_u32(hb.wcnt, hb.wpre, ((size_t)m + 63) / 64, false, d32 + 0, ws, st) != 0)
             return -1;
         hipLaunchKernelGGL(k_headpos, dim3(grid_for(((size_t)m + 64 * kHpWords - 1) / (64 * kHpWords) * 64, kT)),

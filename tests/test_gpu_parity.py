@@ -47,6 +47,14 @@ def _special(kind, n):
         return np.repeat(rng.integers(0, 64, n // 40 + 1, dtype=np.uint8), 40)[:n].copy()
     if kind == "halves":  # a text repeated once at distance ~n / 2
         return np.resize(gen("text", n // 2 + 1, 11), n)
+    if kind == "halves_edit":  # the same with 24 bytes of the copy changed (mismatches on the diagonal)
+        src = np.resize(gen("text", n // 2 + 3, 12), n)
+        rng = np.random.default_rng(7)
+        for p in rng.integers(n // 2 + 3, n, 24):
+            src[p] = (int(src[p]) + int(rng.integers(1, 40))) % 95 + 32
+        return src
+    if kind == "thirds":  # a text repeated twice more (three copies: no twins)
+        return np.resize(gen("text", n // 3 + 5, 13), n)
     raise ValueError(kind)
 
 
@@ -64,7 +72,7 @@ STAGE_CASES = [
 
 
 def _make(kind, n, seed, alpha):
-    if kind in ("zeros", "period3", "runs", "runs40", "halves"):
+    if kind in ("zeros", "period3", "runs", "runs40", "halves", "halves_edit", "thirds"):
         return _special(kind, n)
     return gen(kind, n, seed, alpha)
 
@@ -425,21 +433,45 @@ def test_dc3_auto_switch(ctx, monkeypatch, algo):
     """A repetitive block of >= 1 MiB goes to DC3 by default, before round 0: when the repetition
     probe finds its evenly spaced 32-gram samples repeated among themselves (Fibonacci, period 3),
     or finds three quarters of them occurring elsewhere in the block by scanning every position
-    (a text repeated once at distance n / 2, runs of 40 equal bytes: the samples rarely meet
-    there); text does not go; SALZ_SA=doubling keeps prefix doubling. All give the reference
-    stream."""
+    (runs of 40 equal bytes, a text three times: the samples rarely meet there); a text repeated
+    once at distance d (three quarters of the points with one copy at d) stays with doubling and
+    splits its twin pairs; text does not go; SALZ_SA=doubling keeps prefix doubling. All give the
+    reference stream."""
     monkeypatch.setenv("SALZ_SA", algo)
     for kind, n in (("fib", 3 << 20), ("period3", 2 << 20), ("text", 2 << 20), ("halves", (2 << 20) + 4321),
-                    ("runs40", (3 << 20) + 77)):
+                    ("runs40", (3 << 20) + 77), ("thirds", (3 << 20) + 11)):
         src = _make(kind, n, 1, 0)
         out = ctx.encode(src)
-        rep = kind != "text" and algo != "doubling"
+        rep = kind not in ("text", "halves") and algo != "doubling"
         st = ctx.stats()
         assert (st["sa_dc3_levels"] > 0) == rep, kind
         if rep:  # the probe skips round 0 of doubling
             assert st["sa_rounds"] == 0, (kind, st["sa_rounds"])
+        if kind == "halves" and algo == "":  # twin pairs: as many rounds as text (doubling alone: ~18)
+            assert 0 < st["sa_rounds"] <= 13, st["sa_rounds"]
         rc, ref = oracle_encode(src)
         assert rc == 0 and out == ref, kind
+
+
+@pytest.mark.parametrize("lcp_sa", ["", "plcp"])
+@pytest.mark.parametrize("kind,n", [("halves", (2 << 20) + 4321), ("halves", (5 << 20) + 6),
+                                    ("halves_edit", (3 << 20) + 5)])
+def test_twin_pairs_match_oracle(ctx, monkeypatch, lcp_sa, kind, n):
+    """Twin pairs (sa.hip k_twin_pairs): two-member groups {x, x + d} ordered and split by the first
+    mismatch on diagonal d (the copy running to the end of the block, or edited bytes in it): the
+    suffix array, the LCPs from the sort (and from the PLCP stage), the candidates and the stream
+    equal the oracle's."""
+    monkeypatch.setenv("SALZ_SA", lcp_sa)
+    src = _make(kind, n, 0, 0)
+    out, d = ctx.encode_dump(src)
+    st = ctx.stats()
+    assert st["sa_dc3_levels"] == 0 and 0 < st["sa_rounds"] <= 13, st
+    o = oracle_stages(src)
+    for k in ("sa", "psv", "nsv", "lp", "ln"):
+        i = _first_diff(d[k], o[k])
+        assert i < 0, f"{k} differs at {i}: gpu {d[k][i]} oracle {o[k][i]}"
+    rc, ref = oracle_encode(src)
+    assert rc == 0 and out == ref
 
 
 @pytest.mark.parametrize("lcp_sa", ["1", "0"])
