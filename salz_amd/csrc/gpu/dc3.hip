@@ -277,16 +277,27 @@ __global__ void k_dc3_mod0_flags(const uint32_t *__restrict__ sar, uint32_t ns, 
         flag[r] = sar[r] < n1 ? 1u : 0u;
 }
 
-// Mod-0 suffixes in rank[i + 1] order (the dummy stands for i = n - 1), keyed by t[i]. With
-// packb (symbols of at most 4 bits, positions and ranks under 2^28) the rest of the merge's
-// comparison operands of i ride along, read from the same TR run as t[i], so the merge reads no
-// TR for them: key = t[i] | rank[i + 1] << 8 | rank[i + 2] << 36 (the sort's one 8-bit digit is
-// t[i] alone), value = i | t[i + 1] << 28.
-constexpr int kRankBits = 28;
-constexpr uint32_t kPosMask = (1u << kRankBits) - 1u;
+// Mod-0 suffixes in rank[i + 1] order (the dummy stands for i = n - 1), keyed by t[i]. With a
+// packing (symbols of at most 8 bits, and rank and position fields that leave room for t[i + 1])
+// the rest of the merge's comparison operands of i ride along, read from the same TR run as t[i],
+// so the merge reads no TR for them: key = t[i] | rank[i + 1] << 8 | rank[i + 2] << (8 + R) |
+// t[i + 1]'s high bits << (8 + 2R) (the sort's one 8-bit digit is t[i] alone), value = i | t[i + 1]'s
+// low bits << P. (Round 6: up to 8-bit symbols with fields sized per level, was 4 bits with 28-bit
+// fields: Fibonacci's levels 3-5 pack too.)
+struct Pack {
+    uint32_t R, P;  // rank bits, position bits; R = 0: not packed
+};
+
+__device__ __forceinline__ uint64_t pack_key(uint2 x0, uint2 x1, uint2 x2, Pack k)
+{
+    const uint32_t hs = 8u + 2u * k.R;
+    const uint64_t hi = hs < 64u ? (uint64_t)(x1.x >> (32u - k.P)) << hs : 0ull;
+    return x0.x | ((uint64_t)x1.y << 8) | ((uint64_t)x2.y << (8u + k.R)) | hi;
+}
+
 __global__ void k_dc3_mod0(const uint32_t *__restrict__ sar, const uint32_t *__restrict__ idx, uint32_t ns,
                            uint32_t n1, uint32_t n0, const uint2 *__restrict__ tr, uint64_t *__restrict__ key,
-                           uint32_t *__restrict__ val, uint32_t *err, int packb)
+                           uint32_t *__restrict__ val, uint32_t *err, Pack pk)
 {
     const size_t r = (size_t)blockIdx.x * kT + threadIdx.x;
     if (r >= ns)
@@ -297,10 +308,10 @@ __global__ void k_dc3_mod0(const uint32_t *__restrict__ sar, const uint32_t *__r
     const uint32_t c = idx[r], i = 3u * j;
     if (bad_index(c >= n0, err, kErrDc3))
         return;
-    if (packb) {
+    if (pk.R) {
         const uint2 x0 = tr[i], x1 = tr[i + 1], x2 = tr[i + 2];
-        key[c] = x0.x | ((uint64_t)x1.y << 8) | ((uint64_t)x2.y << (8 + kRankBits));
-        val[c] = i | (x1.x << kRankBits);
+        key[c] = pack_key(x0, x1, x2, pk);
+        val[c] = i | (x1.x << pk.P);
     } else {
         key[c] = tr[i].x;
         val[c] = i;
@@ -339,23 +350,25 @@ struct MergeIn {
     const uint32_t *posb;  // sorted mod-0 positions (B)
     uint32_t nb;
     const uint2 *tr;
-    const uint64_t *keyb;  // B's sorted keys: with packb, their operands (k_dc3_mod0)
-    int packb;
+    const uint64_t *keyb;  // B's sorted keys: when packed, their operands (k_dc3_mod0)
+    Pack pk;
 };
 
 // Position and comparison operands of B element k (sorted mod-0 index)
 __device__ __forceinline__ uint32_t b_pos(const MergeIn &m, uint32_t k)
 {
-    return m.packb ? m.posb[k] & kPosMask : m.posb[k];
+    return m.pk.R ? m.posb[k] & ((1u << m.pk.P) - 1u) : m.posb[k];
 }
 
 __device__ __forceinline__ Quad b_quad(const MergeIn &m, uint32_t k)
 {
-    if (!m.packb)
+    if (!m.pk.R)
         return quad_of(m.tr, m.posb[k]);
     const uint64_t x = m.keyb[k];
-    return Quad{(uint32_t)x & 255u, m.posb[k] >> kRankBits, (uint32_t)(x >> 8) & kPosMask,
-                (uint32_t)(x >> (8 + kRankBits))};
+    const uint32_t R = m.pk.R, P = m.pk.P, hs = 8u + 2u * R, rmask = (1u << R) - 1u;
+    const uint32_t hi = hs < 64u ? (uint32_t)(x >> hs) << (32u - P) : 0u;
+    return Quad{(uint32_t)x & 255u, (m.posb[k] >> P) | hi, (uint32_t)(x >> 8) & rmask,
+                (uint32_t)(x >> (8u + R)) & rmask};
 }
 
 __device__ __forceinline__ uint32_t a_pos(const MergeIn &m, uint32_t r)
@@ -585,16 +598,19 @@ int dc3_level(Dc3 &d, uint2 *tr, uint32_t n, int b, uint32_t *sa_out)
         return -1;
     K = ws.keyA;
     V = ws.valA;
-    // (symbols of more than 4 bits: unpacked keys, the merge reading every operand from TR)
-    const int packb = b <= 4 && n < (1u << kRankBits) && ns < (1u << kRankBits) ? b : 0;
+    // (symbols of more than 8 bits, or fields too wide for t[i + 1]: unpacked keys, the merge
+    // reading every operand from TR)
+    Pack pk{(uint32_t)bit_width(ns), (uint32_t)bit_width(n)};
+    if (b > 8 || pk.P > 31 || 8 + 2 * pk.R > 64 || (64 - 8 - 2 * pk.R) + (32 - pk.P) < (uint32_t)b)
+        pk = Pack{0u, 0u};
     hipLaunchKernelGGL(k_dc3_mod0, dim3(grid_for(ns, kT)), dim3(kT), 0, st, sar, name, ns, n1, n0, tr, K, V,
-                       d.derr, packb);
+                       d.derr, pk);
     SALZ_LAUNCH_CHECK();
     if (radix_sort_pairs(&K, &V, ws.keyB, ws.valB, n0, 0, b, ws, st, nullptr, nullptr, nullptr, rdig, false, true) !=
         0)
         return -1;
     // merge
-    MergeIn mi{sar, ns - dummy, dummy, n1, V, n0, tr, K, packb};
+    MergeIn mi{sar, ns - dummy, dummy, n1, V, n0, tr, K, pk};
     const uint32_t ntiles = grid_for(n, kMergeTile);
     uint32_t *split = ws.offA;
     hipLaunchKernelGGL(k_dc3_partition, dim3(grid_for((size_t)ntiles + 1, kT)), dim3(kT), 0, st, mi, ntiles, split);
