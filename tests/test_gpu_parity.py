@@ -407,7 +407,8 @@ def test_ansv_staging_levels(ctx, kind, n, seed):
 
 def test_suffix_sort_round_checks():
     """SALZ_CHECK=rounds,sa (the suffix sorter's per-round invariants, the text round's keys and
-    order included, and the final permutation check) pass, and the streams equal the oracle's.
+    order included, and the final permutation check) pass, and the streams equal the oracle's;
+    the halves blocks run with twin pairs.
     The switch is read once per process, so the encodes run in a child process."""
     import subprocess
     import sys
@@ -419,7 +420,8 @@ def test_suffix_sort_round_checks():
         "ctx = salz_amd.Context(0, 1 << 21)\n"
         "for kind, n, seed, alpha in (('text', 600000, 5, 0), ('mixed', 300000, 6, 0), ('smx', 200000, 2, 20),\n"
         "                             ('fib', 100000, 0, 0), ('runs40', 400001, 0, 0), ('mixed', 2000000, 7, 0),\n"
-        "                             ('text', 2000000, 9, 0)):\n"
+        "                             ('text', 2000000, 9, 0), ('halves', 2000003, 0, 0),\n"
+        "                             ('halves_edit', 1500001, 0, 0)):\n"
         "    src = _make(kind, n, seed, alpha)\n"
         "    assert ctx.encode(src) == oracle_encode(src)[1], kind\n"
         "print('round checks ok')\n" % ROOT)
