@@ -798,9 +798,12 @@ __global__ __launch_bounds__(kT) void k_cost_rest(ExitBits eb, const uint32_t *_
 
 // Lazy passes, after the exact costs of the exit set: per chunk, whether its costs all moved by
 // one delta (no decision changed in this pass's walk, at most kSumm (8) distinct exits, all
-// moving by the same delta, every exit cost under 2^29 so that no cost of the chunk reaches
-// 2^30: a path inside one chunk adds far less) -> Lnew = Lcur + delta; otherwise the chunk is
-// rewritten (k_lazy_rewrite) with offset 0.
+// moving by the same delta, every exit cost before and after under 2^30 - 2^20 so that no cost of
+// the chunk reaches 2^30: a path inside one chunk adds far less than 2^20, and no compare wraps)
+// -> Lnew = Lcur + delta; otherwise the chunk is rewritten (k_lazy_rewrite) with offset 0.
+// (The bound was 2^29 on the new cost: a block whose stream passes 2^29 bits, mixed 256 MiB,
+// rewrote the chunks of its first half in every pass.)
+constexpr uint32_t kLazyMax = (1u << 30) - (1u << 20);
 __global__ __launch_bounds__(kT) void k_lazy_chunks(uint32_t nchunks, const uint32_t *__restrict__ summ,
                                                     const uint8_t *__restrict__ chg, ExitBits eb,
                                                     const uint32_t *__restrict__ js, const uint32_t *__restrict__ ce,
@@ -820,7 +823,7 @@ __global__ __launch_bounds__(kT) void k_lazy_chunks(uint32_t nchunks, const uint
         const uint32_t x = bits_index(eb.mask, eb.wpre, sidx(e, klog));
         const uint32_t v = js[x], d = v - ce[x];
         d0 = k == 0 ? d : d0;
-        u &= d == d0 && v < (1u << 29);
+        u &= d == d0 && v < kLazyMax && ce[x] < kLazyMax;
     }
     uni[c] = u ? 1u : 0u;
     dl[c] = d0;
