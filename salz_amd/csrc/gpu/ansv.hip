@@ -336,13 +336,28 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     __shared__ uint32_t wq_n;
     const uint32_t qbase = shard_base(blockIdx.x % kShards, gridDim.x, n);
     auto slot_of = [&](uint32_t l) { return rbase[vsa[kB + l] >> rlog] + loc[l]; };
-    auto enqueue = [&](uint32_t e) {
-        const uint32_t slot = atomicAdd(&wq_n, 1u);
-        if (slot < kWQ)
-            wq[slot] = (uint16_t)e;
-        else
-            block_walk(e, slot_of(e >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len, qcount,
-                       qbase, bl, pk, rlog);
+    // Both sides' misses of a wave's leaves take their queue slots with one LDS atomic per wave
+    // (one per query before: a block whose PSVs all lie to its left, as in every descending run
+    // of a periodic block's suffix array, queued 2048 queries through one LDS word).
+    auto enqueue2 = [&](bool needP, bool needN, uint32_t l) {
+        const uint64_t mP = wave_ballot(needP), mN = wave_ballot(needN);
+        if (!(mP | mN))
+            return;
+        const int leader = (int)__ffsll((unsigned long long)(mP | mN)) - 1;
+        uint32_t base = 0;
+        if ((int)lane_id() == leader)
+            base = atomicAdd(&wq_n, (uint32_t)(__popcll(mP) + __popcll(mN)));
+        base = shfl_u32(base, leader);
+        for (int side = 0; side < 2; side++) {
+            if (!(side ? needN : needP))
+                continue;
+            const uint32_t q = base + (side ? (uint32_t)__popcll(mP) + count_below(mN) : count_below(mP));
+            const uint32_t e = l << 1 | (uint32_t)side;
+            if (q < kWQ)
+                wq[q] = (uint16_t)e;
+            else
+                block_walk(e, slot_of(l), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len, qcount, qbase, bl, pk, rlog);
+        }
     };
     if (tid == 0)
         wq_n = 0;
@@ -392,26 +407,19 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
             const uint2 hp = pk_half(hitP != kInf ? half(v, pvP, lmP, bl) : make_uint2(0u, 0u), v, rlog, 0);
             const uint2 hn = pk_half(hitN != kInf ? half(v, pvN, lmN, bl) : make_uint2(0u, 0u), v, rlog, 1);
             stage[slot] = make_uint4(hp.x, hp.y, hn.x, hn.y);
-            if (hitP == kInf)
-                enqueue(l << 1);
-            if (hitN == kInf)
-                enqueue(l << 1 | 1u);
-            continue;
-        }
-        sp[slot] = v;
-        if (hitP != kInf && hitN != kInf) {
-            const uint2 hp = half(v, pvP, lmP, bl), hn = half(v, pvN, lmN, bl);
-            stage[slot] = make_uint4(hp.x, hp.y, hn.x, hn.y);
         } else {
-            if (hitP != kInf)
-                sh[2 * slot] = half(v, pvP, lmP, bl);
-            else
-                enqueue(l << 1);
-            if (hitN != kInf)
-                sh[2 * slot + 1] = half(v, pvN, lmN, bl);
-            else
-                enqueue(l << 1 | 1u);
+            sp[slot] = v;
+            if (hitP != kInf && hitN != kInf) {
+                const uint2 hp = half(v, pvP, lmP, bl), hn = half(v, pvN, lmN, bl);
+                stage[slot] = make_uint4(hp.x, hp.y, hn.x, hn.y);
+            } else {
+                if (hitP != kInf)
+                    sh[2 * slot] = half(v, pvP, lmP, bl);
+                if (hitN != kInf)
+                    sh[2 * slot + 1] = half(v, pvN, lmN, bl);
+            }
         }
+        enqueue2(hitP == kInf, hitN == kInf, l);
     }
     __syncthreads();
 
