@@ -142,8 +142,22 @@ __global__ __launch_bounds__(kT) void k_dc3_presence_global(const uint2 *__restr
         const uint32_t key = triple_key(tr, (uint32_t)j, n1, b), w = key >> 5, m = 1u << (key & 31u);
         keys[j] = key;
         const uint32_t h = (key * 0x9E3779B1u) >> 21;  // (kFilter = 2^11 slots)
-        if (filt[h] == key)
-            continue;  // set by this workgroup already
+        bool todo = filt[h] != key;  // (not set by this workgroup yet)
+        // Up to four distinct keys of the wave go through one lane each: in the first pass of the
+        // grid every workgroup's filter is empty, and all lanes of a periodic block (one key)
+        // reached the same global word (2048 x 256 atomics on one address; zeros at 256 MiB:
+        // 4.4 ms for one level)
+        uint64_t pend = wave_ballot(todo);
+        for (int it = 0; it < 4 && pend; it++) {
+            const int ld = (int)__ffsll((unsigned long long)pend) - 1;
+            const uint32_t k0 = shfl_u32(key, ld);
+            const bool same = todo && key == k0;
+            pend &= ~wave_ballot(same);
+            if (same && (int)lane_id() != ld)
+                todo = false;
+        }
+        if (!todo)
+            continue;
         filt[h] = key;  // (racing lanes may both store; either way the bit is set below)
         if (!(bits[w] & m))  // (a stale cached 0 only costs a redundant atomic)
             atomicOr(&bits[w], m);
