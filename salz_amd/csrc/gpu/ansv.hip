@@ -44,6 +44,8 @@ constexpr uint32_t kWQ = 1408;  // LDS walk-queue entries per block
 constexpr uint32_t kShards = 1024;
 constexpr uint32_t kMaxRanges = 256;  // staging text ranges per block (rlog is raised to fit)
 constexpr size_t kQMaxWord = 800;     // u32 index into Workspace::dscal: the largest shard per side
+constexpr size_t kLinkWord = 2304;    // u32 index into Workspace::radix_counts: the block links
+static_assert(kLinkWord >= 256 + 2 * 1024 && kLinkWord % 4 == 0, "past the range and queue counters, 16-byte aligned");
 static_assert(kMaxRanges <= kT, "one thread per range");
 
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
@@ -502,21 +504,12 @@ struct Tree {
     }
 };
 
-// Queries that left their block: continue the climb from the block root. blockIdx.y is the
-// queue shard.
-__global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
-                              const uint32_t *__restrict__ qlen,
-                              const uint32_t *__restrict__ qcount, uint32_t used_blocks, int nsv,
-                              uint4 *__restrict__ cand, uint32_t klog, Blocks bl)
+// Climb from `node` (a node over >= kScan leaves, or a block root) towards the root: the first
+// sibling on the query's side holding a smaller suffix is descended to its nearest node over
+// kScan leaves, whose leaves are scanned. Returns the answer's rank (kInf: none); lm accumulates
+// the LCP minimum (PSV: over the ranks passed to the left; NSV: up to and including the answer).
+__device__ __forceinline__ uint32_t tree_walk(const Tree &t, uint32_t node, uint32_t v, uint32_t &lm, int nsv)
 {
-    const uint32_t x = blockIdx.x * kT + threadIdx.x;
-    if (x >= qcount[2u * blockIdx.y + (uint32_t)nsv])
-        return;
-    const uint32_t e = shard_base(blockIdx.y, used_blocks, t.n) + x;
-    const uint32_t r = q[e];
-    uint32_t lm = qlen[e];
-    const uint32_t v = t.sa[r];
-    uint32_t node = t.np2 / kB + r / kB, hit = kInf;
     const uint32_t low = t.np2 / kScan;  // nodes over kScan leaves: [low, 2 low)
     while (node > 1) {
         bool side = nsv ? !(node & 1u) : (node & 1u);
@@ -556,13 +549,113 @@ __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
                         m = h == kInf ? umin(m, lv[q]) : m;
                 }
                 lm = m;
-                hit = h;
-                break;
+                return h;
             }
             lm = umin(lm, t.lmin(s));
         }
         node >>= 1;
     }
+    return kInf;
+}
+
+// Block links: per block B, the PSV of its left neighbour rank b0 - 1 and the NSV of its right
+// neighbour b1 = b0 + kB with their LCP minima (x, y: PSV rank, minimum over (x, b0 - 1]; z, w: NSV
+// rank, minimum over [b1, z]; kInf: none). A query that leaves its block with a suffix above the
+// neighbour's but below the link's has the link as its answer: every rank between holds a larger
+// suffix. In a periodic block's suffix array each phase is one descending run of positions across
+// many blocks, whose PSVs all lie at the end of the run before: one walk per block instead of one
+// per query.
+__global__ void k_ansv_links(Tree t, uint32_t used_blocks, uint4 *__restrict__ link)
+{
+    const uint32_t B = blockIdx.x * kT + threadIdx.x;
+    if (B >= used_blocks)
+        return;
+    const uint32_t low = t.np2 / kScan;
+    uint4 out = make_uint4(kInf, kInf, kInf, kInf);
+    if (B > 0 && (uint64_t)B * kB <= t.n) {
+        const uint32_t r1 = B * kB - 1u, v1 = t.sa[r1], g0 = r1 & ~(kScan - 1u);
+        uint32_t lm = t.lcp[r1], hit = kInf;
+        for (uint32_t k = r1; k-- > g0;) {
+            if (t.sa[k] < v1) {
+                hit = k;
+                break;
+            }
+            lm = umin(lm, t.lcp[k]);
+        }
+        if (hit == kInf)
+            hit = tree_walk(t, low + r1 / kScan, v1, lm, 0);
+        out.x = hit;
+        out.y = lm;
+    }
+    if ((uint64_t)(B + 1) * kB < t.n) {
+        const uint32_t r1 = (B + 1) * kB, v1 = t.sa[r1];
+        const uint32_t gend = (r1 | (kScan - 1u)) + 1u < t.n ? (r1 | (kScan - 1u)) + 1u : t.n;
+        uint32_t lm = t.lcp[r1], hit = kInf;
+        for (uint32_t k = r1 + 1; k < gend; k++) {
+            lm = umin(lm, t.lcp[k]);
+            if (t.sa[k] < v1) {
+                hit = k;
+                break;
+            }
+        }
+        if (hit == kInf)
+            hit = tree_walk(t, low + r1 / kScan, v1, lm, 1);
+        out.z = hit;
+        out.w = lm;
+    }
+    link[B] = out;
+}
+
+// Queries that left their block: the block's neighbour or link when it answers (above), else the
+// climb from the block root. blockIdx.y is the queue shard.
+__global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
+                              const uint32_t *__restrict__ qlen,
+                              const uint32_t *__restrict__ qcount, uint32_t used_blocks, int nsv,
+                              uint4 *__restrict__ cand, uint32_t klog, Blocks bl, const uint4 *__restrict__ link)
+{
+    const uint32_t x = blockIdx.x * kT + threadIdx.x;
+    if (x >= qcount[2u * blockIdx.y + (uint32_t)nsv])
+        return;
+    const uint32_t e = shard_base(blockIdx.y, used_blocks, t.n) + x;
+    const uint32_t r = q[e];
+    uint32_t lm = qlen[e];
+    const uint32_t v = t.sa[r], B = r / kB;
+    uint32_t hit = kInf;
+    bool done = false;  // (answered by the neighbour or the link, or none: the link has none)
+    const uint4 lk = link ? link[B] : make_uint4(0u, 0u, 0u, 0u);
+    if (!link) {
+    } else if (!nsv) {
+        if (B > 0) {
+            const uint32_t r1 = B * kB - 1u;
+            if (t.sa[r1] < v) {
+                hit = r1;
+                done = true;
+            } else if (lk.x == kInf) {
+                done = true;
+            } else if (t.sa[lk.x] < v) {
+                hit = lk.x;
+                lm = umin(lm, lk.y);
+                done = true;
+            }
+        }
+    } else {
+        const uint32_t r1 = (B + 1) * kB;
+        if ((uint64_t)(B + 1) * kB < t.n) {
+            if (t.sa[r1] < v) {
+                hit = r1;
+                lm = umin(lm, t.lcp[r1]);
+                done = true;
+            } else if (lk.z == kInf) {
+                done = true;
+            } else if (t.sa[lk.z] < v) {
+                hit = lk.z;
+                lm = umin(lm, lk.w);
+                done = true;
+            }
+        }
+    }
+    if (!done)
+        hit = tree_walk(t, t.np2 / kB + B, v, lm, nsv);
     uint32_t pos = hit == kInf ? kInf : t.sa[hit];
     if (nsv)
         put_nsv(cand, klog, v, pos, lm, bl);
@@ -664,14 +757,23 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
     const uint32_t nqp = reinterpret_cast<uint32_t *>(ws.hscal)[kQMaxWord];  // largest shard per side
     const uint32_t nqn = reinterpret_cast<uint32_t *>(ws.hscal)[kQMaxWord + 1];
     Tree t{tsa, tlcp, ws.sa, lcp, n, np2};
+    // block links in the radix counts past the range and queue counters
+    // (a workspace whose counters cannot hold them walks every query: link = null)
+    uint4 *link = ws.radix_counts_elems >= kLinkWord + 4 * (size_t)used_blocks
+                      ? reinterpret_cast<uint4 *>(ws.radix_counts + kLinkWord)
+                      : nullptr;
+    if ((nqp || nqn) && link) {
+        hipLaunchKernelGGL(k_ansv_links, dim3(grid_for(used_blocks, kT)), dim3(kT), 0, st, t, used_blocks, link);
+        SALZ_LAUNCH_CHECK();
+    }
     if (nqp) {
         hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqp, kT), kShards), dim3(kT), 0, st, t,
-                           qp, qpl, cnt, used_blocks, 0, ws.cand, ws.klog, bl);
+                           qp, qpl, cnt, used_blocks, 0, ws.cand, ws.klog, bl, link);
         SALZ_LAUNCH_CHECK();
     }
     if (nqn) {
         hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqn, kT), kShards), dim3(kT), 0, st, t,
-                           qn, qnl, cnt, used_blocks, 1, ws.cand, ws.klog, bl);
+                           qn, qnl, cnt, used_blocks, 1, ws.cand, ws.klog, bl, link);
         SALZ_LAUNCH_CHECK();
     }
     hipLaunchKernelGGL(k_cand_origin, dim3(grid_for(bl.nb, kT)), dim3(kT), 0, st, ws.cand, bl, ws.klog);
