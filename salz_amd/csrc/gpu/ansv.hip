@@ -19,7 +19,8 @@
 // The answers come out in rank order but cand is indexed by text position, so writing them
 // directly is a 16-byte random scatter over the whole 16n-byte array (1.6 GB at 100 MB, beyond
 // the 256 MB Infinity Cache). Instead each workgroup appends its answers to per-text-range
-// staging runs (ranges of 2^rlog positions, one global atomic per range and workgroup), and
+// staging runs (ranges of 2^rlog positions, one global atomic per range and workgroup; the
+// queries that leave the block keep their staging slot and k_ansv_global answers into it), and
 // k_cand_scatter moves the staged answers range by range: its concurrent writes then all fall
 // in one cache-resident window of the candidate array.
 #include "internal.hpp"
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(1024) void k_tree_top(uint32_t *__restrict__ tsa, u
 // query whose answer lies outside the block goes to the global queue (wave-aggregated).
 __device__ __forceinline__ void block_walk(uint32_t e, uint32_t slot, const uint32_t *vsa,
                                            const uint32_t *vlc, uint32_t b0, uint2 *sh, uint32_t *qp, uint32_t *qp_len,
-                                           uint32_t *qn, uint32_t *qn_len, uint32_t *qcount,
+                                           uint32_t *qn, uint32_t *qn_len, uint32_t *qps, uint32_t *qns, uint32_t *qcount,
                                            uint32_t qbase, const Blocks &bl, int pk, uint32_t rlog)
 {
     const uint32_t l = e >> 1, r = b0 + l;
@@ -224,6 +225,7 @@ __device__ __forceinline__ void block_walk(uint32_t e, uint32_t slot, const uint
             const uint32_t q = base + count_below(mask);
             (side ? qn : qp)[q] = r;
             (side ? qn_len : qp_len)[q] = lm;
+            (side ? qns : qps)[q] = slot;  // (k_ansv_global answers into the staging slot)
         }
     }
 }
@@ -232,7 +234,8 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     const uint32_t *__restrict__ sa, const uint32_t *__restrict__ lcp, uint32_t n, Blocks bl, uint32_t np2,
     uint32_t *__restrict__ tsa, uint32_t *__restrict__ tlcp, uint4 *__restrict__ stage,
     uint32_t *__restrict__ sp, uint32_t *__restrict__ rfill,
-    uint32_t rlog, uint32_t *__restrict__ qp, uint32_t *__restrict__ qp_len,
+    uint32_t rlog, uint32_t *__restrict__ qp, uint32_t *__restrict__ qp_len, uint32_t *__restrict__ qps,
+    uint32_t *__restrict__ qns,
     uint32_t *__restrict__ qn, uint32_t *__restrict__ qn_len, uint32_t *__restrict__ qcount, int pk)
 {
     __shared__ uint32_t vsa[2 * kB + kNear];  // heap: [1, kB) tree, [kB, 2kB) leaves, + pad
@@ -358,7 +361,8 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
             if (q < kWQ)
                 wq[q] = (uint16_t)e;
             else
-                block_walk(e, slot_of(l), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len, qcount, qbase, bl, pk, rlog);
+                block_walk(e, slot_of(l), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len, qps, qns, qcount, qbase, bl, pk,
+                           rlog);
         }
     };
     if (tid == 0)
@@ -429,13 +433,13 @@ __global__ __launch_bounds__(kT) void k_ansv_local(
     // the global queues (k_ansv_global continues from the block root).
     const uint32_t nw = wq_n < kWQ ? wq_n : kWQ;
     for (uint32_t w = tid; w < nw; w += kT)
-        block_walk(wq[w], slot_of(wq[w] >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len,
+        block_walk(wq[w], slot_of(wq[w] >> 1), vsa, vlc, b0, sh, qp, qp_len, qn, qn_len, qps, qns,
                    qcount, qbase, bl, pk, rlog);
 }
 
 // Staged answers -> cand in the interleaved text-order layout. Slots are grouped by text
-// range, so the workgroups in flight write into one cache-resident window of cand. Halves
-// that went to the global queues are garbage here; k_ansv_global overwrites them afterwards.
+// range, so the workgroups in flight write into one cache-resident window of cand. It runs last:
+// the halves that went to the global queues were filled in by k_ansv_global (round 6).
 __global__ __launch_bounds__(kT) void k_cand_scatter(const uint32_t *__restrict__ sp,
                                                      const uint4 *__restrict__ stage, uint32_t npos,
                                                      uint4 *__restrict__ cand, uint32_t klog,
@@ -607,11 +611,15 @@ __global__ void k_ansv_links(Tree t, uint32_t used_blocks, uint4 *__restrict__ l
 }
 
 // Queries that left their block: the block's neighbour or link when it answers (above), else the
-// climb from the block root. blockIdx.y is the queue shard.
+// climb from the block root. blockIdx.y is the queue shard. The answer goes into the query's
+// staging slot (qslot, from k_ansv_local), so k_cand_scatter moves it into cand with the block's
+// own answers, window by window (a periodic block's PSVs almost all leave their blocks: written
+// straight into cand in text order they were random 8-byte writes, period 3 at 256 MiB 10.7 ms).
 __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
-                              const uint32_t *__restrict__ qlen,
+                              const uint32_t *__restrict__ qlen, const uint32_t *__restrict__ qslot,
                               const uint32_t *__restrict__ qcount, uint32_t used_blocks, int nsv,
-                              uint4 *__restrict__ cand, uint32_t klog, Blocks bl, const uint4 *__restrict__ link)
+                              uint2 *__restrict__ sh, uint32_t rlog, int pk, Blocks bl,
+                              const uint4 *__restrict__ link)
 {
     const uint32_t x = blockIdx.x * kT + threadIdx.x;
     if (x >= qcount[2u * blockIdx.y + (uint32_t)nsv])
@@ -656,11 +664,9 @@ __global__ void k_ansv_global(Tree t, const uint32_t *__restrict__ q,
     }
     if (!done)
         hit = tree_walk(t, t.np2 / kB + B, v, lm, nsv);
-    uint32_t pos = hit == kInf ? kInf : t.sa[hit];
-    if (nsv)
-        put_nsv(cand, klog, v, pos, lm, bl);
-    else
-        put_psv(cand, klog, v, pos, lm, bl);
+    const uint32_t pos = hit == kInf ? kInf : t.sa[hit];
+    const uint2 hh = half(v, pos, lm, bl);
+    sh[2 * qslot[e] + (uint32_t)nsv] = pk ? pk_half(hh, v, rlog, nsv) : hh;
 }
 
 // Every block's first position: no PSV / NSV, lengths 1 (lib/salz.c:547-548).
@@ -728,13 +734,10 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
     // positions keep). A second staging level (each run re-sorted into 2 MB windows before the
     // scatter) measured slower in round 5 (C2 ANSV 3.65 -> 4.04 ms) and was removed in round 6.
     const int pk = npos <= (1u << 27) && rlog <= 20 ? 1 : 0;
+    // staging slots of the queued queries (u1, u2: free here)
+    uint32_t *qps = ws.u1, *qns = ws.u2;
     hipLaunchKernelGGL(k_ansv_local, dim3(used_blocks), dim3(kT), 0, st, ws.sa, lcp, n, bl, np2, tsa,
-                       tlcp, stage, sp, rfill, rlog, qp, qpl, qn, qnl, cnt, pk);
-    SALZ_LAUNCH_CHECK();
-    const uint32_t nranges = (uint32_t)((((uint64_t)npos - 1) >> rlog) + 1);
-    const uint32_t sgrid = 8u * ((nranges + 7u) / 8u) << (rlog - 8);
-    hipLaunchKernelGGL(k_cand_scatter, dim3(sgrid), dim3(kT), 0, st, sp, stage, npos, ws.cand,
-                       ws.klog, rlog, nranges, rfill, derr, pk);
+                       tlcp, stage, sp, rfill, rlog, qp, qpl, qps, qns, qn, qnl, cnt, pk);
     SALZ_LAUNCH_CHECK();
     uint32_t lo = nblocks / 2;
     for (; lo > kTopNodes; lo >>= 1) {
@@ -766,16 +769,23 @@ int stage_candidates(Workspace &ws, const Blocks &bl, const uint32_t *lcp)
         hipLaunchKernelGGL(k_ansv_links, dim3(grid_for(used_blocks, kT)), dim3(kT), 0, st, t, used_blocks, link);
         SALZ_LAUNCH_CHECK();
     }
+    uint2 *sh = reinterpret_cast<uint2 *>(stage);
     if (nqp) {
         hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqp, kT), kShards), dim3(kT), 0, st, t,
-                           qp, qpl, cnt, used_blocks, 0, ws.cand, ws.klog, bl, link);
+                           qp, qpl, qps, cnt, used_blocks, 0, sh, rlog, pk, bl, link);
         SALZ_LAUNCH_CHECK();
     }
     if (nqn) {
         hipLaunchKernelGGL(k_ansv_global, dim3(grid_for(nqn, kT), kShards), dim3(kT), 0, st, t,
-                           qn, qnl, cnt, used_blocks, 1, ws.cand, ws.klog, bl, link);
+                           qn, qnl, qns, cnt, used_blocks, 1, sh, rlog, pk, bl, link);
         SALZ_LAUNCH_CHECK();
     }
+    // every answer staged: into cand, window by window
+    const uint32_t nranges = (uint32_t)((((uint64_t)npos - 1) >> rlog) + 1);
+    const uint32_t sgrid = 8u * ((nranges + 7u) / 8u) << (rlog - 8);
+    hipLaunchKernelGGL(k_cand_scatter, dim3(sgrid), dim3(kT), 0, st, sp, stage, npos, ws.cand,
+                       ws.klog, rlog, nranges, rfill, derr, pk);
+    SALZ_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_cand_origin, dim3(grid_for(bl.nb, kT)), dim3(kT), 0, st, ws.cand, bl, ws.klog);
     SALZ_LAUNCH_CHECK();
     return 0;
