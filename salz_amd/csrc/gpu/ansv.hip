@@ -74,19 +74,6 @@ __device__ __forceinline__ uint2 pk_half(uint2 h, uint32_t p, uint32_t rlog, int
     return make_uint2((uint32_t)w, (uint32_t)(w >> 32));
 }
 
-// cand is stored in the parse's chunk-interleaved layout (common.hpp, sidx).
-__device__ __forceinline__ void put_psv(uint4 *cand, uint32_t klog, uint32_t p, uint32_t psv_pos,
-                                        uint32_t len, const Blocks &bl)
-{
-    reinterpret_cast<uint2 *>(cand)[2 * sidx(p, klog)] = half(p, psv_pos, len, bl);
-}
-
-__device__ __forceinline__ void put_nsv(uint4 *cand, uint32_t klog, uint32_t p, uint32_t nsv_pos,
-                                        uint32_t len, const Blocks &bl)
-{
-    reinterpret_cast<uint2 *>(cand)[2 * sidx(p, klog) + 1] = half(p, nsv_pos, len, bl);
-}
-
 // First queue slot of shard s: the shards' regions hold as many entries as their blocks
 // have leaves (a leaf misses at most once per side), so they tile [0, n) exactly. Shard t holds
 // blocks t, t + kShards, ...: q + (t < rem) of them; the last block is short by short_by leaves.
